@@ -1,0 +1,618 @@
+// HIP kernels and the device half of the C ABI (include/mirt.h).
+//
+// Frame kernel: one wave64 per 8x8 pixel tile (coherent primary rays share
+// their BVH walk), 4 waves per 256-thread workgroup. Each lane traces one
+// pixel through trace_path (trace.h); the wave walks the skip-threaded tree
+// with a wave-uniform cursor, so node and sphere reads are scalar loads of
+// an L2-resident array. Output is packed RGBA8 (one dword per pixel).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "internal.h"
+#include "trace.h"
+
+using namespace mirt;
+
+namespace {
+
+// Per-frame constants computed on the host with the reference's expressions
+// (ray.c:18-24, main.c:356) -- libm tan stays on the host.
+struct FrameConst {
+    float px, py, pz;  // camera position (ray origin)
+    float fx, fy, fz;  // forward
+    float hx, hy, hz;  // horizontal = right * (2 half_width)
+    float vx, vy, vz;  // vertical = up * (2 half_height)
+    float aspect, wf, hf;
+    int width, height, depth, use_bvh;
+    uint64_t seed;
+    uint32_t sample;
+    int accumulate;
+    float frames;
+    int row_block, shard, num_shards, num_rows;
+};
+
+FrameConst make_frame_const(const mirt_camera* cam, const mirt_frame_desc* fd)
+{
+    FrameConst f{};
+    const float aspect = (float)fd->width / (float)fd->height;                    // ray.c:18
+    const float fov_rad = (float)((double)cam->fov * (M_PI / 180.0));             // ray.c:19
+    const float half_h = (float)std::tan((double)(fov_rad / 2.0f));               // ray.c:20
+    const float half_w = aspect * half_h;                                         // ray.c:21
+    const float sw = 2.0f * half_w, sh = 2.0f * half_h;
+    f.px = cam->position.x; f.py = cam->position.y; f.pz = cam->position.z;
+    f.fx = cam->forward.x; f.fy = cam->forward.y; f.fz = cam->forward.z;
+    f.hx = cam->right.x * sw; f.hy = cam->right.y * sw; f.hz = cam->right.z * sw;  // ray.c:23
+    f.vx = cam->up.x * sh; f.vy = cam->up.y * sh; f.vz = cam->up.z * sh;          // ray.c:24
+    f.aspect = aspect;                                                            // main.c:356
+    f.wf = (float)fd->width;
+    f.hf = (float)fd->height;
+    f.width = fd->width;
+    f.height = fd->height;
+    f.depth = fd->max_depth;
+    f.use_bvh = fd->use_bvh;
+    f.seed = fd->seed;
+    f.sample = fd->sample;
+    f.accumulate = fd->accumulate;
+    f.frames = (float)fd->frames;
+    f.row_block = fd->row_block;
+    f.shard = fd->shard;
+    f.num_shards = fd->num_shards;
+    f.num_rows = shard_row_count(fd);
+    return f;
+}
+
+// Image row of compacted shard row r.
+__device__ __forceinline__ int shard_row_to_y(const FrameConst& f, int r)
+{
+    const int blk = r / f.row_block;
+    return (blk * f.num_shards + f.shard) * f.row_block + (r - blk * f.row_block);
+}
+
+// main.c:362-365 + ray.c:26-31 for pixel (x, y).
+__device__ __forceinline__ Ray camera_ray(const FrameConst& f, int x, int y)
+{
+    const float u = ((float)x / f.wf - 0.5f) * f.aspect;
+    const float v = -((float)y / f.hf - 0.5f);
+    float dx = f.fx + f.hx * u, dy = f.fy + f.hy * u, dz = f.fz + f.hz * u;
+    dx = dx + f.vx * v;
+    dy = dy + f.vy * v;
+    dz = dz + f.vz * v;
+    normalize3(dx, dy, dz);
+    return {f.px, f.py, f.pz, dx, dy, dz};
+}
+
+// Wave w of a block covers an 8x8 tile; tiles run along x, then shard rows.
+__device__ __forceinline__ void tile_pixel(const FrameConst& f, int& x, int& r)
+{
+    const int lane = threadIdx.x & 63;
+    const int tile = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int tiles_x = (f.width + 7) >> 3;
+    x = (tile % tiles_x) * 8 + (lane & 7);
+    r = (tile / tiles_x) * 8 + (lane >> 3);
+}
+
+__device__ __forceinline__ void add_counts(mirt_counts* out, const Counters& c)
+{
+    atomicAdd((unsigned long long*)&out->rays, (unsigned long long)c.rays);
+    atomicAdd((unsigned long long*)&out->nodes, (unsigned long long)c.nodes);
+    atomicAdd((unsigned long long*)&out->spheres, (unsigned long long)c.spheres);
+    atomicAdd((unsigned long long*)&out->hits, (unsigned long long)c.hits);
+}
+
+// The pixel loop of main.c:358-374 (fresh) / main.c:382-407 (accumulate).
+template <bool UNIFORM, bool COUNT>
+__global__ __launch_bounds__(256) void render_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
+                                                      float* __restrict__ acc, mirt_counts* counts)
+{
+    int x, r;
+    tile_pixel(f, x, r);
+    const bool alive = x < f.width && r < f.num_rows;
+    const int y = alive ? shard_row_to_y(f, r) : 0;
+    const Ray ray = camera_ray(f, alive ? x : 0, y);
+    const uint64_t key = pixel_key(f.seed, (uint32_t)(y * f.width + x), f.sample);
+    Counters cnt{0, 0, 0, 0};
+    const uint32_t c = trace_path<UNIFORM, COUNT>(sc, ray, alive, f.depth, f.use_bvh != 0, key, cnt);
+    if (COUNT) add_counts(counts, cnt);
+    if (!alive) return;
+    const size_t i = (size_t)r * f.width + x;
+    uint32_t shown = c;
+    if (acc) {
+        float* a = acc + 3 * i;
+        for (int ch = 0; ch < 3; ch++) {
+            const float v = (float)((c >> (8 * ch)) & 0xff) / 255.0f;  // main.c:368-370 / 394-396
+            if (f.accumulate) {
+                a[ch] = a[ch] + v;
+                const float avg = a[ch] / f.frames * 255.0f;           // main.c:398-400
+                const uint32_t q = (uint32_t)(int)fminf(avg, 255.0f);
+                shown = (shown & ~(0xffu << (8 * ch))) | ((q & 0xffu) << (8 * ch));
+            } else {
+                a[ch] = v;
+            }
+        }
+    }
+    out[i] = shown;
+}
+
+// trace_ray on explicit rays (renderer.c:21); ray i uses contract pixel i.
+template <bool UNIFORM>
+__global__ __launch_bounds__(256) void trace_rays_kernel(DevScene sc, const mirt_ray* __restrict__ rays, int n,
+                                                         int depth, int use_bvh, uint64_t seed, uint32_t sample,
+                                                         uint32_t* __restrict__ out)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool alive = i < n;
+    const mirt_ray& rr = rays[alive ? i : 0];
+    const Ray ray{rr.origin.x, rr.origin.y, rr.origin.z, rr.direction.x, rr.direction.y, rr.direction.z};
+    Counters cnt{0, 0, 0, 0};
+    const uint32_t c = trace_path<UNIFORM, false>(sc, ray, alive, depth, use_bvh != 0,
+                                                  pixel_key(seed, (uint32_t)i, sample), cnt);
+    if (alive) out[i] = c;
+}
+
+__device__ __forceinline__ void store_hit(const Ray& ray, float t, int s, const DevScene& sc, mirt_hit* o)
+{
+    mirt_hit h;
+    memset(&h, 0, sizeof h);
+    h.sphere = -1;
+    if (s >= 0) {
+        float p[3], nn[3];
+        hit_point_normal(ray, t, sc.geo[s], p, nn);
+        h.t = t;
+        h.point = {p[0], p[1], p[2]};
+        h.normal = {nn[0], nn[1], nn[2]};
+        h.hit = 1;
+        h.sphere = s;
+    }
+    *o = h;
+}
+
+// ray_bvh_intersect (hit.c:91) / brute-force closest hit (renderer.c:36-43)
+__global__ __launch_bounds__(256) void intersect_kernel(DevScene sc, const mirt_ray* __restrict__ rays, int n,
+                                                        int use_bvh, mirt_hit* __restrict__ out)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool alive = i < n;
+    const mirt_ray& rr = rays[alive ? i : 0];
+    const Ray ray{rr.origin.x, rr.origin.y, rr.origin.z, rr.direction.x, rr.direction.y, rr.direction.z};
+    Counters cnt{0, 0, 0, 0};
+    float t;
+    int s;
+    if (use_bvh)
+        closest_bvh<true, false>(sc, ray, alive, t, s, cnt);
+    else
+        closest_brute<false>(sc, ray, alive, t, s, cnt);
+    if (alive) store_hit(ray, t, s, sc, &out[i]);
+}
+
+// element-wise ray_sphere_intersect (hit.c:19-39)
+__global__ void sphere_pairs_kernel(const mirt_ray* __restrict__ rays, const mirt_sphere* __restrict__ sph, int n,
+                                    mirt_hit* __restrict__ out)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const mirt_ray rr = rays[i];
+    const Ray ray{rr.origin.x, rr.origin.y, rr.origin.z, rr.direction.x, rr.direction.y, rr.direction.z};
+    const float4 g = make_float4(sph[i].center.x, sph[i].center.y, sph[i].center.z, sph[i].radius);
+    const float t = sphere_t(sph_ray(ray), g);
+    mirt_hit h;
+    memset(&h, 0, sizeof h);
+    h.sphere = -1;
+    if (t > 0.0f) {
+        float p[3], nn[3];
+        hit_point_normal(ray, t, g, p, nn);
+        h.t = t;
+        h.point = {p[0], p[1], p[2]};
+        h.normal = {nn[0], nn[1], nn[2]};
+        h.hit = 1;
+        h.sphere = i;
+    }
+    out[i] = h;
+}
+
+// element-wise ray_aabb_intersect (hit.c:49-82)
+__global__ void aabb_pairs_kernel(const mirt_ray* __restrict__ rays, const mirt_aabb* __restrict__ boxes, int n,
+                                  int32_t* __restrict__ out)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const mirt_ray rr = rays[i];
+    const Ray ray{rr.origin.x, rr.origin.y, rr.origin.z, rr.direction.x, rr.direction.y, rr.direction.z};
+    const mirt_aabb b = boxes[i];
+    out[i] = slab_test(slab_ray(ray), b.min.x, b.min.y, b.min.z, b.max.x, b.max.y, b.max.z) ? 1 : 0;
+}
+
+__global__ void camera_rays_kernel(FrameConst f, mirt_ray* __restrict__ out)
+{
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int r = blockIdx.y;
+    if (x >= f.width || r >= f.num_rows) return;
+    const Ray ray = camera_ray(f, x, shard_row_to_y(f, r));
+    out[(size_t)r * f.width + x] = {{ray.ox, ray.oy, ray.oz}, {ray.dx, ray.dy, ray.dz}};
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ context
+
+struct mirt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    float last_ms = 0.0f;
+    // scene (replicated per device, uploaded once)
+    mirt_node* d_nodes = nullptr;
+    float4* d_geo = nullptr;
+    uint32_t* d_color = nullptr;
+    int num_nodes = 0, num_spheres = -1;
+    // frame buffers owned by the ctx (blocking API)
+    uint32_t* d_out = nullptr;
+    float* d_acc = nullptr;
+    size_t out_cap = 0, acc_cap = 0, acc_pixels = 0;
+    // staging for batch calls
+    void* d_in = nullptr;
+    void* d_res = nullptr;
+    size_t in_cap = 0, res_cap = 0;
+    mirt_counts* d_counts = nullptr;
+};
+
+namespace {
+
+int hip_fail(hipError_t e, const char* what)
+{
+    set_error("%s: %s", what, hipGetErrorString(e));
+    return MIRT_E_DEVICE;
+}
+
+#define HIP_TRY(expr)                                   \
+    do {                                                \
+        hipError_t e_ = (expr);                         \
+        if (e_ != hipSuccess) return hip_fail(e_, #expr); \
+    } while (0)
+
+int ensure(void** p, size_t* cap, size_t bytes)
+{
+    if (bytes <= *cap) return MIRT_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    HIP_TRY(hipMalloc(p, bytes));
+    *cap = bytes;
+    return MIRT_OK;
+}
+
+DevScene dev_scene(const mirt_ctx* c)
+{
+    return DevScene{c->d_nodes, c->d_geo, c->d_color, (uint32_t)c->num_nodes, c->num_spheres};
+}
+
+bool ctx_ok(mirt_ctx* c, bool need_scene, const char* fn)
+{
+    if (!c) {
+        set_error("%s: null context", fn);
+        return false;
+    }
+    if (need_scene && c->num_spheres < 0) {
+        set_error("%s: no scene uploaded", fn);
+        return false;
+    }
+    return hipSetDevice(c->device) == hipSuccess;
+}
+
+// Default traversal for frame rendering (wave-uniform walk, scalar loads).
+constexpr bool kUniform = true;
+
+int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_acc, hipStream_t s, bool timed,
+                  mirt_counts* d_counts)
+{
+    const int tiles = ((f.width + 7) / 8) * ((f.num_rows + 7) / 8);
+    const int blocks = (tiles + 3) / 4;
+    if (blocks == 0) return MIRT_OK;
+    if (timed) HIP_TRY(hipEventRecord(c->ev0, s));
+    if (d_counts)
+        render_kernel<kUniform, true><<<blocks, 256, 0, s>>>(dev_scene(c), f, d_out, d_acc, d_counts);
+    else
+        render_kernel<kUniform, false><<<blocks, 256, 0, s>>>(dev_scene(c), f, d_out, d_acc, nullptr);
+    HIP_TRY(hipGetLastError());
+    if (timed) HIP_TRY(hipEventRecord(c->ev1, s));
+    return MIRT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mirt_create(int device, mirt_ctx** out)
+{
+    if (!out) return MIRT_E_INVALID;
+    *out = nullptr;
+    int n = 0;
+    HIP_TRY(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) {
+        set_error("mirt_create: device %d not present (%d visible)", device, n);
+        return MIRT_E_INVALID;
+    }
+    HIP_TRY(hipSetDevice(device));
+    mirt_ctx* c = new mirt_ctx();
+    c->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev0);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+    if (e == hipSuccess) e = hipMalloc((void**)&c->d_counts, sizeof(mirt_counts));
+    if (e != hipSuccess) {
+        mirt_destroy(c);
+        return hip_fail(e, "mirt_create");
+    }
+    *out = c;
+    return MIRT_OK;
+}
+
+void mirt_destroy(mirt_ctx* c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (void* p : {(void*)c->d_nodes, (void*)c->d_geo, (void*)c->d_color, (void*)c->d_out, (void*)c->d_acc,
+                    c->d_in, c->d_res, (void*)c->d_counts})
+        if (p) (void)hipFree(p);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int mirt_scene_upload_flat(mirt_ctx* c, const mirt_sphere* spheres, int ns, const mirt_node* nodes, int nn)
+{
+    if (!ctx_ok(c, false, "mirt_scene_upload_flat")) return MIRT_E_INVALID;
+    if (ns < 0 || nn < 0 || (ns > 0 && !spheres) || (nn > 0 && !nodes)) {
+        set_error("mirt_scene_upload_flat: invalid arguments");
+        return MIRT_E_INVALID;
+    }
+    // validate the tree so a malformed one cannot send the kernel out of bounds
+    for (int i = 0; i < nn; i++) {
+        const uint32_t skip = nodes[i].skip & MIRT_SKIP_MASK;
+        const bool leaf = nodes[i].sphere >= 0;
+        if (skip <= (uint32_t)i || skip > (uint32_t)nn || nodes[i].sphere > ns || nodes[i].sphere < -1 ||
+            (leaf && skip != (uint32_t)i + 1) || (!leaf && i + 1 >= nn)) {
+            set_error("mirt_scene_upload_flat: malformed node %d", i);
+            return MIRT_E_INVALID;
+        }
+    }
+    if (nn > 0 && (nodes[0].skip & MIRT_SKIP_MASK) != (uint32_t)nn) {
+        set_error("mirt_scene_upload_flat: root skip %u != node count %d", nodes[0].skip & MIRT_SKIP_MASK, nn);
+        return MIRT_E_INVALID;
+    }
+    std::vector<float4> geo((size_t)ns + 1);
+    std::vector<uint32_t> col((size_t)ns + 1);
+    for (int i = 0; i < ns; i++) {
+        geo[i] = make_float4(spheres[i].center.x, spheres[i].center.y, spheres[i].center.z, spheres[i].radius);
+        std::memcpy(&col[i], &spheres[i].color, 4);
+    }
+    geo[ns] = make_float4(NAN, NAN, NAN, NAN);  // &spheres[N] sentinel: never hits
+    col[ns] = 0xff000000u;
+    for (void* p : {(void*)c->d_nodes, (void*)c->d_geo, (void*)c->d_color})
+        if (p) (void)hipFree(p);
+    c->d_nodes = nullptr;
+    c->d_geo = nullptr;
+    c->d_color = nullptr;
+    c->num_spheres = -1;
+    HIP_TRY(hipMalloc((void**)&c->d_nodes, sizeof(mirt_node) * (size_t)(nn > 0 ? nn : 1)));
+    HIP_TRY(hipMalloc((void**)&c->d_geo, sizeof(float4) * geo.size()));
+    HIP_TRY(hipMalloc((void**)&c->d_color, sizeof(uint32_t) * col.size()));
+    if (nn > 0) HIP_TRY(hipMemcpy(c->d_nodes, nodes, sizeof(mirt_node) * (size_t)nn, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->d_geo, geo.data(), sizeof(float4) * geo.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->d_color, col.data(), sizeof(uint32_t) * col.size(), hipMemcpyHostToDevice));
+    c->num_nodes = nn;
+    c->num_spheres = ns;
+    return MIRT_OK;
+}
+
+int mirt_scene_upload(mirt_ctx* c, const mirt_sphere* spheres, int ns, const mirt_bvh_node* root)
+{
+    if (!root) return mirt_scene_upload_flat(c, spheres, ns, nullptr, 0);
+    const int nn = mirt_bvh_count(root);
+    std::vector<mirt_node> flat((size_t)nn);
+    if (mirt_bvh_flatten(root, spheres, flat.data(), nn) != nn) {
+        set_error("mirt_scene_upload: flatten failed");
+        return MIRT_E_INVALID;
+    }
+    return mirt_scene_upload_flat(c, spheres, ns, flat.data(), nn);
+}
+
+int mirt_render_frame_device(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, uint32_t* d_out,
+                             float* d_acc, void* stream)
+{
+    if (!ctx_ok(c, true, "mirt_render_frame_device")) return MIRT_E_NOSCENE;
+    if (!cam || !frame_desc_valid(fd) || !d_out || (fd->accumulate && !d_acc)) {
+        set_error("mirt_render_frame_device: invalid arguments");
+        return MIRT_E_INVALID;
+    }
+    if (fd->use_bvh && c->num_nodes == 0) {
+        set_error("mirt_render_frame_device: use_bvh set but no tree uploaded");
+        return MIRT_E_NOSCENE;
+    }
+    const FrameConst f = make_frame_const(cam, fd);
+    return launch_render(c, f, d_out, d_acc, stream ? (hipStream_t)stream : c->stream, false, nullptr);
+}
+
+int mirt_render_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, mirt_rgba8* out)
+{
+    if (!ctx_ok(c, true, "mirt_render_frame")) return MIRT_E_NOSCENE;
+    if (!cam || !frame_desc_valid(fd) || !out) {
+        set_error("mirt_render_frame: invalid arguments");
+        return MIRT_E_INVALID;
+    }
+    if (fd->use_bvh && c->num_nodes == 0) {
+        set_error("mirt_render_frame: use_bvh set but no tree uploaded");
+        return MIRT_E_NOSCENE;
+    }
+    const FrameConst f = make_frame_const(cam, fd);
+    const size_t pixels = (size_t)f.num_rows * f.width;
+    int rc = ensure((void**)&c->d_out, &c->out_cap, pixels * 4 + 4);
+    if (rc) return rc;
+    rc = ensure((void**)&c->d_acc, &c->acc_cap, pixels * 12 + 4);
+    if (rc) return rc;
+    if (c->acc_pixels != pixels) {  // a new frame geometry starts a fresh accumulation buffer
+        HIP_TRY(hipMemsetAsync(c->d_acc, 0, pixels * 12, c->stream));
+        c->acc_pixels = pixels;
+    }
+    rc = launch_render(c, f, c->d_out, c->d_acc, c->stream, true, nullptr);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(out, c->d_out, pixels * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+    return MIRT_OK;
+}
+
+int mirt_accum_download(mirt_ctx* c, float* out, size_t count)
+{
+    if (!ctx_ok(c, false, "mirt_accum_download") || !out) return MIRT_E_INVALID;
+    if (count > c->acc_pixels * 3) {
+        set_error("mirt_accum_download: %zu floats requested, %zu held", count, c->acc_pixels * 3);
+        return MIRT_E_INVALID;
+    }
+    HIP_TRY(hipMemcpy(out, c->d_acc, count * sizeof(float), hipMemcpyDeviceToHost));
+    return MIRT_OK;
+}
+
+int mirt_count_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, mirt_counts* out)
+{
+    if (!ctx_ok(c, true, "mirt_count_frame")) return MIRT_E_NOSCENE;
+    if (!cam || !frame_desc_valid(fd) || !out) {
+        set_error("mirt_count_frame: invalid arguments");
+        return MIRT_E_INVALID;
+    }
+    const FrameConst f = make_frame_const(cam, fd);
+    const size_t pixels = (size_t)f.num_rows * f.width;
+    int rc = ensure((void**)&c->d_out, &c->out_cap, pixels * 4 + 4);
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(c->d_counts, 0, sizeof(mirt_counts), c->stream));
+    FrameConst f2 = f;
+    f2.accumulate = 0;
+    rc = launch_render(c, f2, c->d_out, nullptr, c->stream, false, c->d_counts);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(out, c->d_counts, sizeof(mirt_counts), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return MIRT_OK;
+}
+
+int mirt_camera_rays(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, mirt_ray* out)
+{
+    if (!ctx_ok(c, false, "mirt_camera_rays")) return MIRT_E_INVALID;
+    if (!cam || !frame_desc_valid(fd) || !out) {
+        set_error("mirt_camera_rays: invalid arguments");
+        return MIRT_E_INVALID;
+    }
+    const FrameConst f = make_frame_const(cam, fd);
+    const size_t bytes = (size_t)f.num_rows * f.width * sizeof(mirt_ray);
+    int rc = ensure(&c->d_res, &c->res_cap, bytes + 4);
+    if (rc) return rc;
+    if (f.num_rows > 0) {
+        camera_rays_kernel<<<dim3((f.width + 255) / 256, f.num_rows), 256, 0, c->stream>>>(f, (mirt_ray*)c->d_res);
+        HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipMemcpyAsync(out, c->d_res, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return MIRT_OK;
+}
+
+int mirt_trace_rays(mirt_ctx* c, const mirt_ray* rays, int n, int depth, int use_bvh, uint64_t seed,
+                    uint32_t sample, mirt_rgba8* out)
+{
+    if (!ctx_ok(c, true, "mirt_trace_rays")) return MIRT_E_NOSCENE;
+    if (n < 0 || (n > 0 && (!rays || !out)) || depth < 0 || depth > kMaxDepth) {
+        set_error("mirt_trace_rays: invalid arguments");
+        return MIRT_E_INVALID;
+    }
+    if (n == 0) return MIRT_OK;
+    int rc = ensure(&c->d_in, &c->in_cap, sizeof(mirt_ray) * (size_t)n);
+    if (!rc) rc = ensure(&c->d_res, &c->res_cap, 4 * (size_t)n);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(c->d_in, rays, sizeof(mirt_ray) * (size_t)n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipEventRecord(c->ev0, c->stream));
+    trace_rays_kernel<kUniform><<<(n + 255) / 256, 256, 0, c->stream>>>(dev_scene(c), (const mirt_ray*)c->d_in, n,
+                                                                        depth, use_bvh, seed, sample,
+                                                                        (uint32_t*)c->d_res);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev1, c->stream));
+    HIP_TRY(hipMemcpyAsync(out, c->d_res, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+    return MIRT_OK;
+}
+
+int mirt_intersect_rays(mirt_ctx* c, const mirt_ray* rays, int n, int use_bvh, mirt_hit* out)
+{
+    if (!ctx_ok(c, true, "mirt_intersect_rays")) return MIRT_E_NOSCENE;
+    if (n < 0 || (n > 0 && (!rays || !out))) {
+        set_error("mirt_intersect_rays: invalid arguments");
+        return MIRT_E_INVALID;
+    }
+    if (n == 0) return MIRT_OK;
+    int rc = ensure(&c->d_in, &c->in_cap, sizeof(mirt_ray) * (size_t)n);
+    if (!rc) rc = ensure(&c->d_res, &c->res_cap, sizeof(mirt_hit) * (size_t)n);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(c->d_in, rays, sizeof(mirt_ray) * (size_t)n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipEventRecord(c->ev0, c->stream));
+    intersect_kernel<<<(n + 255) / 256, 256, 0, c->stream>>>(dev_scene(c), (const mirt_ray*)c->d_in, n, use_bvh,
+                                                            (mirt_hit*)c->d_res);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev1, c->stream));
+    HIP_TRY(hipMemcpyAsync(out, c->d_res, sizeof(mirt_hit) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+    return MIRT_OK;
+}
+
+int mirt_sphere_pairs(mirt_ctx* c, const mirt_ray* rays, const mirt_sphere* spheres, int n, mirt_hit* out)
+{
+    if (!ctx_ok(c, false, "mirt_sphere_pairs")) return MIRT_E_INVALID;
+    if (n < 0 || (n > 0 && (!rays || !spheres || !out))) {
+        set_error("mirt_sphere_pairs: invalid arguments");
+        return MIRT_E_INVALID;
+    }
+    if (n == 0) return MIRT_OK;
+    const size_t rb = sizeof(mirt_ray) * (size_t)n, sb = sizeof(mirt_sphere) * (size_t)n;
+    int rc = ensure(&c->d_in, &c->in_cap, rb + sb + 16);
+    if (!rc) rc = ensure(&c->d_res, &c->res_cap, sizeof(mirt_hit) * (size_t)n);
+    if (rc) return rc;
+    char* din = (char*)c->d_in;
+    HIP_TRY(hipMemcpyAsync(din, rays, rb, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(din + rb, spheres, sb, hipMemcpyHostToDevice, c->stream));
+    sphere_pairs_kernel<<<(n + 255) / 256, 256, 0, c->stream>>>((const mirt_ray*)din, (const mirt_sphere*)(din + rb),
+                                                               n, (mirt_hit*)c->d_res);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(out, c->d_res, sizeof(mirt_hit) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return MIRT_OK;
+}
+
+int mirt_aabb_pairs(mirt_ctx* c, const mirt_ray* rays, const mirt_aabb* boxes, int n, int32_t* out)
+{
+    if (!ctx_ok(c, false, "mirt_aabb_pairs")) return MIRT_E_INVALID;
+    if (n < 0 || (n > 0 && (!rays || !boxes || !out))) {
+        set_error("mirt_aabb_pairs: invalid arguments");
+        return MIRT_E_INVALID;
+    }
+    if (n == 0) return MIRT_OK;
+    const size_t rb = sizeof(mirt_ray) * (size_t)n, bb = sizeof(mirt_aabb) * (size_t)n;
+    int rc = ensure(&c->d_in, &c->in_cap, rb + bb + 16);
+    if (!rc) rc = ensure(&c->d_res, &c->res_cap, 4 * (size_t)n);
+    if (rc) return rc;
+    char* din = (char*)c->d_in;
+    HIP_TRY(hipMemcpyAsync(din, rays, rb, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(din + rb, boxes, bb, hipMemcpyHostToDevice, c->stream));
+    aabb_pairs_kernel<<<(n + 255) / 256, 256, 0, c->stream>>>((const mirt_ray*)din, (const mirt_aabb*)(din + rb), n,
+                                                             (int32_t*)c->d_res);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(out, c->d_res, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return MIRT_OK;
+}
+
+float mirt_last_kernel_ms(mirt_ctx* c) { return c ? c->last_ms : 0.0f; }
+
+}  // extern "C"

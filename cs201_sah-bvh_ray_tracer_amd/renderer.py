@@ -1,0 +1,252 @@
+"""Python host side of the render path, mirroring the reference's interface.
+
+Reference call surface -> here (all compute goes through libmirt.so):
+
+  srand / rand (glibc, main.c:90)             RandState
+  create_random_sphere x N (sphere.c:52-59,   create_random_spheres(n, seed)
+    main.c:218-221)
+  create_benchmark_sphere (sphere.c:34-41,    create_benchmark_spheres(n, seed)
+    benchmark.c:307-314)
+  camera init (main.c:203-211) / camera_update default_camera() / camera_update(cam)
+    (camera.c:10-18)
+  build_bvh_node (bvh.c:117-209)               build_bvh(spheres, start, end, depth) -> Bvh
+                                               build_bvh_node(...) -> pointer tree (drop-in)
+  get_camera_ray (ray.c:17-32) per pixel       Renderer.get_camera_rays(cam, W, H)
+  trace_ray (renderer.c:21-77) per ray         Renderer.trace_ray(rays, depth, ...)
+  pixel loop main.c:356-374 / 379-408          Renderer.render_frame(cam, W, H, ...)
+  ray_bvh_intersect (hit.c:91-109)             Renderer.ray_bvh_intersect(rays)
+  ray_sphere_intersect (hit.c:19-39)           Renderer.ray_sphere_intersect(rays, spheres)
+  ray_aabb_intersect (hit.c:49-82)             Renderer.ray_aabb_intersect(rays, boxes)
+
+Errors raise MirtError (the reference only printf's); there is no CPU path.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+from .lib import MirtError, check, load
+
+ptr = abi.ptr
+
+
+class RandState:
+    """glibc srand()/rand() (TYPE_3), restated in libmirt."""
+
+    def __init__(self, seed=1):
+        self.st = abi.RandState()
+        load().mirt_srand(C.byref(self.st), seed)
+
+    def rand(self):
+        return load().mirt_rand(C.byref(self.st))
+
+
+def create_random_spheres(n, seed=1, state=None):
+    """srand(seed) then n x create_random_sphere() (main.c:218-221)."""
+    st = state or RandState(seed)
+    out = np.zeros(n, abi.SPHERE)
+    check(load().mirt_scene_random(C.byref(st.st), ptr(out), n), "mirt_scene_random")
+    return out
+
+
+def create_benchmark_spheres(n, seed=1, world_size=1000.0, state=None):
+    """srand(seed) then the benchmark.c:307-314 sphere loop."""
+    st = state or RandState(seed)
+    out = np.zeros(n, abi.SPHERE)
+    check(load().mirt_scene_benchmark(C.byref(st.st), ptr(out), n, world_size), "mirt_scene_benchmark")
+    return out
+
+
+def default_camera():
+    cam = abi.Camera()
+    load().mirt_camera_default(C.byref(cam))
+    return cam
+
+
+def camera_update(cam):
+    load().mirt_camera_update(C.byref(cam))
+    return cam
+
+
+class Bvh:
+    """A flattened tree (abi.NODE array) plus the leaf sphere counts it came from."""
+
+    def __init__(self, nodes):
+        self.nodes = nodes
+
+    def __len__(self):
+        return len(self.nodes)
+
+
+def build_bvh(spheres, start=0, end=None, depth=0):
+    """build_bvh_node (bvh.c:117) straight into the flat layout; reorders
+    `spheres` in place exactly like the reference."""
+    assert spheres.dtype == abi.SPHERE and spheres.flags["C_CONTIGUOUS"]
+    end = len(spheres) if end is None else end
+    out = C.c_void_p()
+    cnt = C.c_int()
+    L = load()
+    check(L.mirt_bvh_build_flat(ptr(spheres), start, end, depth, C.byref(out), C.byref(cnt)), "mirt_bvh_build_flat")
+    try:
+        buf = (C.c_char * (cnt.value * abi.NODE.itemsize)).from_address(out.value)
+        nodes = np.frombuffer(bytes(buf), dtype=abi.NODE).copy()
+    finally:
+        L.mirt_bvh_free_flat(out)
+    return Bvh(nodes)
+
+
+def build_bvh_node(spheres, start=0, end=None, depth=0):
+    """Drop-in build_bvh_node: returns the reference-layout pointer tree
+    (free with free_bvh)."""
+    end = len(spheres) if end is None else end
+    root = load().mirt_build_bvh_node(ptr(spheres), start, end, depth)
+    if not root:
+        raise MirtError(load().mirt_last_error().decode())
+    return root
+
+
+def free_bvh(root):
+    load().mirt_free_bvh(root)
+
+
+def flatten_bvh(root, spheres):
+    """Flatten a pointer tree (ours or the reference's) into a Bvh."""
+    L = load()
+    n = L.mirt_bvh_count(root)
+    nodes = np.zeros(n, abi.NODE)
+    check(L.mirt_bvh_flatten(root, ptr(spheres), ptr(nodes), n), "mirt_bvh_flatten")
+    return Bvh(nodes)
+
+
+def frame_desc(width, height, depth=5, use_bvh=True, seed=1, sample=0, accumulate=False, frames=1,
+               row_block=8, shard=0, num_shards=1):
+    fd = abi.FrameDesc()
+    fd.width, fd.height, fd.max_depth, fd.use_bvh = width, height, depth, int(use_bvh)
+    fd.seed, fd.sample, fd.accumulate, fd.frames = seed, sample, int(accumulate), frames
+    fd.row_block, fd.shard, fd.num_shards = row_block, shard, num_shards
+    return fd
+
+
+def shard_rows(fd):
+    """Image rows a shard renders, in its compacted order."""
+    L = load()
+    n = check(L.mirt_shard_rows(C.byref(fd), None), "mirt_shard_rows")
+    rows = np.zeros(n, np.int32)
+    L.mirt_shard_rows(C.byref(fd), ptr(rows))
+    return rows
+
+
+class Renderer:
+    """One device context (mirt_ctx) with a resident scene."""
+
+    def __init__(self, device=0):
+        self.L = load()
+        h = C.c_void_p()
+        check(self.L.mirt_create(device, C.byref(h)), "mirt_create")
+        self.h = h
+        self.device = device
+        self.num_spheres = -1
+
+    def close(self):
+        if self.h:
+            self.L.mirt_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- scene
+    def upload(self, spheres, bvh=None):
+        """Upload the (post-build) spheres and a Bvh, a pointer tree, or None."""
+        spheres = np.ascontiguousarray(spheres, abi.SPHERE)
+        if bvh is None:
+            check(self.L.mirt_scene_upload_flat(self.h, ptr(spheres), len(spheres), None, 0), "upload")
+        elif isinstance(bvh, Bvh):
+            check(self.L.mirt_scene_upload_flat(self.h, ptr(spheres), len(spheres), ptr(bvh.nodes), len(bvh.nodes)),
+                  "mirt_scene_upload_flat")
+        else:
+            check(self.L.mirt_scene_upload(self.h, ptr(spheres), len(spheres), bvh), "mirt_scene_upload")
+        self.num_spheres = len(spheres)
+
+    # ---- frames
+    def render_frame(self, cam, width, height, depth=5, use_bvh=True, seed=1, sample=0, accumulate=False,
+                     frames=1, row_block=8, shard=0, num_shards=1):
+        """main.c:356-374 (fresh) or main.c:379-408 (accumulate) for one shard;
+        returns (rows, width, 4) uint8 in the shard's row order."""
+        fd = frame_desc(width, height, depth, use_bvh, seed, sample, accumulate, frames, row_block, shard,
+                        num_shards)
+        n = check(self.L.mirt_shard_rows(C.byref(fd), None), "mirt_shard_rows")
+        out = np.zeros((n, width, 4), np.uint8)
+        check(self.L.mirt_render_frame(self.h, C.byref(cam), C.byref(fd), ptr(out)), "mirt_render_frame")
+        return out
+
+    def render_frame_device(self, cam, fd, d_out, d_acc=None, stream=None):
+        """Enqueue a frame into device memory (integer device pointers)."""
+        check(self.L.mirt_render_frame_device(self.h, C.byref(cam), C.byref(fd), C.c_void_p(d_out),
+                                              C.c_void_p(d_acc) if d_acc else None,
+                                              C.c_void_p(stream) if stream else None), "mirt_render_frame_device")
+
+    def accum(self, count):
+        out = np.zeros(count, np.float32)
+        check(self.L.mirt_accum_download(self.h, ptr(out), count), "mirt_accum_download")
+        return out
+
+    def count_frame(self, cam, width, height, depth=5, use_bvh=True, seed=1, sample=0, row_block=8, shard=0,
+                    num_shards=1):
+        """Reference-DFS work of one frame: rays, node tests, sphere tests, hits."""
+        fd = frame_desc(width, height, depth, use_bvh, seed, sample, False, 1, row_block, shard, num_shards)
+        c = abi.Counts()
+        check(self.L.mirt_count_frame(self.h, C.byref(cam), C.byref(fd), C.byref(c)), "mirt_count_frame")
+        return {"rays": c.rays, "nodes": c.nodes, "spheres": c.spheres, "hits": c.hits}
+
+    @property
+    def last_kernel_ms(self):
+        return self.L.mirt_last_kernel_ms(self.h)
+
+    # ---- per-ray surface (batched)
+    def get_camera_rays(self, cam, width, height, row_block=8, shard=0, num_shards=1):
+        fd = frame_desc(width, height, 1, True, 1, 0, False, 1, row_block, shard, num_shards)
+        n = check(self.L.mirt_shard_rows(C.byref(fd), None), "mirt_shard_rows")
+        out = np.zeros((n, width), abi.RAY)
+        check(self.L.mirt_camera_rays(self.h, C.byref(cam), C.byref(fd), ptr(out)), "mirt_camera_rays")
+        return out
+
+    def trace_ray(self, rays, depth=5, use_bvh=True, seed=1, sample=0):
+        rays = np.ascontiguousarray(rays, abi.RAY)
+        out = np.zeros((len(rays), 4), np.uint8)
+        check(self.L.mirt_trace_rays(self.h, ptr(rays), len(rays), depth, int(use_bvh), seed, sample, ptr(out)),
+              "mirt_trace_rays")
+        return out
+
+    def closest_hit(self, rays, use_bvh=True):
+        rays = np.ascontiguousarray(rays, abi.RAY)
+        out = np.zeros(len(rays), abi.HIT)
+        check(self.L.mirt_intersect_rays(self.h, ptr(rays), len(rays), int(use_bvh), ptr(out)),
+              "mirt_intersect_rays")
+        return out
+
+    def ray_bvh_intersect(self, rays):
+        return self.closest_hit(rays, True)
+
+    def ray_sphere_intersect(self, rays, spheres):
+        rays = np.ascontiguousarray(rays, abi.RAY)
+        spheres = np.ascontiguousarray(spheres, abi.SPHERE)
+        out = np.zeros(len(rays), abi.HIT)
+        check(self.L.mirt_sphere_pairs(self.h, ptr(rays), ptr(spheres), len(rays), ptr(out)), "mirt_sphere_pairs")
+        return out
+
+    def ray_aabb_intersect(self, rays, boxes):
+        rays = np.ascontiguousarray(rays, abi.RAY)
+        boxes = np.ascontiguousarray(boxes, abi.AABB)
+        out = np.zeros(len(rays), np.int32)
+        check(self.L.mirt_aabb_pairs(self.h, ptr(rays), ptr(boxes), len(rays), ptr(out)), "mirt_aabb_pairs")
+        return out

@@ -1,0 +1,99 @@
+"""Row-block sharding of one frame across ranks (one process per GPU) and the
+RCCL gather of the per-rank RGBA8 slabs to rank 0.
+
+A frame's rows are cut into blocks of `row_block` rows; block b belongs to
+rank b % world (interleaved, so the expensive dense middle of the image is
+spread over all ranks). Each rank renders its blocks, compacted in row order,
+into a slab of slab_rows(...) rows (shard 0 has the most rows; the others
+are padded to that), then `dist.gather` brings the slabs to rank 0, which
+de-interleaves them on the device. The scene is replicated per rank, so the
+gather is the only exchange. Pixels do not depend on the sharding (the RNG
+contract keys on the full-frame pixel index), so any world size produces the
+same bytes as one GPU.
+"""
+import torch
+import torch.distributed as dist
+
+
+def shard_row_count(height, row_block, world, shard):
+    """Rows of shard `shard` (matches mirt_shard_rows in csrc/host_scene.cpp)."""
+    blocks = (height + row_block - 1) // row_block
+    rows = 0
+    for b in range(shard, blocks, world):
+        rows += min(row_block, height - b * row_block)
+    return rows
+
+
+def slab_rows(height, row_block, world):
+    """Padded slab height: shard 0 always holds the most rows."""
+    return shard_row_count(height, row_block, world, 0)
+
+
+def row_sources(height, row_block, world, device=None):
+    """For every image row y: (shard, row inside that shard's slab)."""
+    y = torch.arange(height, device=device)
+    blk = y // row_block
+    shard = blk % world
+    pos = (blk // world) * row_block + (y % row_block)
+    return shard, pos
+
+
+def assemble(stacked, height, row_block):
+    """stacked: (world, slab_rows, W) int32 slabs -> (height, W) int32 frame."""
+    world = stacked.shape[0]
+    shard, pos = row_sources(height, row_block, world, stacked.device)
+    return stacked[shard, pos]
+
+
+def gather_frame(slab, height, row_block, group=None, dst=0):
+    """Gather every rank's (slab_rows, W) int32 slab to `dst` and assemble the
+    frame there. Returns the (height, W) int32 frame on dst, None elsewhere."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if world == 1:
+        return assemble(slab.unsqueeze(0), height, row_block)
+    bufs = [torch.empty_like(slab) for _ in range(world)] if rank == dst else None
+    dist.gather(slab, bufs, dst=dst, group=group)
+    if rank != dst:
+        return None
+    return assemble(torch.stack(bufs), height, row_block)
+
+
+def as_rgba(frame_i32):
+    """(H, W) int32 packed RGBA8 -> (H, W, 4) uint8 view."""
+    return frame_i32.contiguous().view(torch.uint8).reshape(frame_i32.shape[0], frame_i32.shape[1], 4)
+
+
+class ShardedFrame:
+    """Renders one frame with this rank's mirt Renderer and gathers it.
+
+    renderer: a renderer.Renderer bound to this rank's GPU with the scene
+    uploaded. Uses torch's current stream for both the kernel and RCCL.
+    """
+
+    def __init__(self, renderer, width, height, row_block=8, group=None):
+        self.r = renderer
+        self.width, self.height, self.row_block = width, height, row_block
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        dev = torch.device("cuda", torch.cuda.current_device())
+        self.rows = slab_rows(height, row_block, self.world)
+        self.slab = torch.zeros((self.rows, width), dtype=torch.int32, device=dev)
+
+    def desc(self, depth=5, use_bvh=True, seed=1, sample=0):
+        from .renderer import frame_desc
+        return frame_desc(self.width, self.height, depth, use_bvh, seed, sample, False, 1, self.row_block,
+                          self.rank, self.world)
+
+    def render_local(self, cam, fd):
+        stream = torch.cuda.current_stream().cuda_stream
+        self.r.render_frame_device(cam, fd, self.slab.data_ptr(), None, stream)
+        return self.slab
+
+    def render(self, cam, fd):
+        """Render this rank's rows and gather; the (H, W) int32 frame on rank 0."""
+        self.render_local(cam, fd)
+        if self.world == 1:
+            return assemble(self.slab.unsqueeze(0), self.height, self.row_block)
+        return gather_frame(self.slab, self.height, self.row_block, self.group)

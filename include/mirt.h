@@ -1,0 +1,224 @@
+/*
+ * include/mirt.h -- C ABI of the MI355X-native primary-ray render path
+ * (camera rays -> BVH traversal + ray/sphere intersection -> closest-hit
+ * diffuse shading -> RGBA framebuffer) of ShivangNagta/CS201_SAH-BVH_Ray_Tracer.
+ *
+ * Every entry point is plain C: POD structs, pointers and sizes, int status.
+ * Structs are layout-compatible with the reference's own types (sizes are
+ * asserted in csrc/host_scene.cpp), so a caller can pass its arrays through
+ * unchanged. The reference interface each entry point replaces is cited as
+ * file:line under /root/reference/ (see also INTEGRATION.md).
+ *
+ * Threading: one host thread per mirt_ctx. Blocking calls return with the
+ * result in host memory; *_device calls enqueue on the given HIP stream.
+ * Errors: negative status, message in mirt_last_error(); the library never
+ * aborts and never falls back to a CPU path.
+ */
+#ifndef MIRT_H
+#define MIRT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ types */
+
+typedef struct mirt_vec3 { float x, y, z; } mirt_vec3;            /* vec3.h:3-7 (12 B)   */
+typedef struct mirt_rgba8 { uint8_t r, g, b, a; } mirt_rgba8;     /* SDL_Color (4 B)     */
+typedef struct mirt_sphere {                                      /* sphere.h:7-11 (20 B) */
+    mirt_vec3 center;
+    float radius;
+    mirt_rgba8 color;
+} mirt_sphere;
+typedef struct mirt_ray { mirt_vec3 origin, direction; } mirt_ray; /* ray.h:5-8 (24 B)   */
+typedef struct mirt_camera {                                      /* camera.h:5-14 (64 B) */
+    mirt_vec3 position, forward, right, up;
+    float yaw, pitch, fov;
+    int move;
+} mirt_camera;
+typedef struct mirt_aabb { mirt_vec3 min, max; } mirt_aabb;       /* bvh.h:7-10 (24 B)   */
+typedef struct mirt_bvh_node {                                    /* bvh.h:12-18 (56 B)  */
+    mirt_aabb bounds;
+    struct mirt_bvh_node *left, *right;
+    mirt_sphere *sphere;
+    int sphere_count;
+} mirt_bvh_node;
+typedef struct mirt_hit_record {                                  /* hit.h:8-14 (40 B)   */
+    float t;
+    mirt_vec3 point, normal;
+    int hit_something;
+    mirt_sphere *object;
+} mirt_hit_record;
+
+/* HitRecord for batch calls: the object pointer becomes an index into the
+   uploaded sphere array (-1: no hit). 40 B. */
+typedef struct mirt_hit {
+    float t;
+    mirt_vec3 point, normal;
+    int32_t hit;
+    int32_t sphere;
+    int32_t pad;
+} mirt_hit;
+
+/* Flattened BVH node, the layout the kernel walks (32 B, 32-B aligned).
+   Depth-first pre-order of the reference tree (bvh.c:203-204: left subtree,
+   then right): the left child of inner node i is i+1 and `skip` is the index
+   that follows i's subtree, so the reference DFS order (hit.c:102-103) is a
+   forward scan that jumps to `skip` when a box is missed or a leaf is done.
+   sphere  >= 0: leaf testing spheres[sphere] (bvh.c:133; == num_spheres is the
+            never-hit sentinel of SURVEY §8.H7); -1: inner node.
+   skip bit 31 (MIRT_NODE_EMPTY): the leaf holds 0 spheres; its box is the
+            inverted create_empty_aabb() box (bvh.c:19-24), which always passes
+            ray_aabb_intersect (hit.c:49-82). */
+typedef struct mirt_node {
+    float bmin[3];
+    float bmax[3];
+    int32_t sphere;
+    uint32_t skip;
+} mirt_node;
+#define MIRT_NODE_EMPTY 0x80000000u
+#define MIRT_SKIP_MASK 0x7fffffffu
+
+/* glibc TYPE_3 rand() state (the reference seeds glibc with srand(),
+   main.c:90, benchmark.c:287). */
+typedef struct mirt_rand_state {
+    int32_t r[34];
+    int32_t f, b;
+} mirt_rand_state;
+
+/* One frame (or one shard of one frame). */
+typedef struct mirt_frame_desc {
+    int32_t width, height;   /* the reference's compile-time WIDTH/HEIGHT (constants.h:7-8) */
+    int32_t max_depth;       /* trace_ray depth argument (main.c:366, MAX_DEPTH = 5) */
+    int32_t use_bvh;         /* main.c:366 `use_bvh ? root : NULL`; 0 = brute force */
+    uint64_t seed;           /* RNG contract seed */
+    uint32_t sample;         /* RNG contract sample index (frame number) */
+    int32_t accumulate;      /* 0: fresh frame main.c:358-374; 1: accumulate main.c:379-408 */
+    int32_t frames;          /* accumulate: divisor accumulated_frames (main.c:380) */
+    int32_t row_block;       /* rows per interleave block (default 8) */
+    int32_t shard;           /* this shard renders row blocks b with b % num_shards == shard */
+    int32_t num_shards;
+} mirt_frame_desc;
+
+/* Work counters of the reference DFS (hit.c:91-109, no pruning). */
+typedef struct mirt_counts {
+    uint64_t rays;       /* rays traced (primary + bounces) */
+    uint64_t nodes;      /* ray_aabb_intersect calls */
+    uint64_t spheres;    /* ray_sphere_intersect calls from leaves (or brute force) */
+    uint64_t hits;       /* rays that found a closest hit */
+} mirt_counts;
+
+enum {
+    MIRT_OK = 0,
+    MIRT_E_INVALID = -1,
+    MIRT_E_NOMEM = -2,
+    MIRT_E_NOSCENE = -3,
+    MIRT_E_DEVICE = -4   /* HIP runtime error; see mirt_last_error() */
+};
+
+typedef struct mirt_ctx mirt_ctx;
+
+const char *mirt_version(void);
+const char *mirt_last_error(void);
+
+/* ------------------------------------------------- host: scene inputs */
+
+/* glibc srand()/rand() restated (TYPE_3 additive feedback), so scenes are
+   reproducible from a seed on any host. */
+void mirt_srand(mirt_rand_state *st, unsigned int seed);
+int mirt_rand(mirt_rand_state *st);
+
+/* n x create_random_sphere() (sphere.c:52-59) as main.c:218-221. */
+int mirt_scene_random(mirt_rand_state *st, mirt_sphere *out, int n);
+/* n x benchmark centre + create_benchmark_sphere() (benchmark.c:307-314, sphere.c:34-41). */
+int mirt_scene_benchmark(mirt_rand_state *st, mirt_sphere *out, int n, float world_size);
+/* The default camera of main.c:203-211. */
+void mirt_camera_default(mirt_camera *cam);
+/* camera_update (camera.c:10-18): basis from yaw/pitch. */
+void mirt_camera_update(mirt_camera *cam);
+
+/* --------------------------------------------- host: BVH (bit-identical) */
+
+/* build_bvh_node (bvh.c:117-209): same signature, same pointer tree, same
+   in-place reordering of `spheres`. Free with mirt_free_bvh. */
+mirt_bvh_node *mirt_build_bvh_node(mirt_sphere *spheres, int start, int end, int depth);
+/* free_bvh (benchmark.c:81-88) */
+void mirt_free_bvh(mirt_bvh_node *node);
+/* Number of nodes in a pointer tree. */
+int mirt_bvh_count(const mirt_bvh_node *root);
+/* Flatten a pointer tree (built by the reference's build_bvh_node or by
+   mirt_build_bvh_node) whose leaf pointers index `base`. Returns the node
+   count, or -needed if cap is too small. */
+int mirt_bvh_flatten(const mirt_bvh_node *root, const mirt_sphere *base, mirt_node *out, int cap);
+/* Build straight into the flat layout: same tree as
+   mirt_bvh_flatten(build_bvh_node(spheres, start, end, depth)) bit for bit,
+   with the SAH planes of bvh.c:143-170 evaluated by one binned pass per axis.
+   *out_nodes is malloc'd; release with mirt_bvh_free_flat. */
+int mirt_bvh_build_flat(mirt_sphere *spheres, int start, int end, int depth,
+                        mirt_node **out_nodes, int *out_count);
+void mirt_bvh_free_flat(mirt_node *nodes);
+
+/* ------------------------------------------------------ device context */
+
+int mirt_create(int device, mirt_ctx **out);
+void mirt_destroy(mirt_ctx *ctx);
+
+/* Copy the (already built, hence reordered) spheres and the caller's tree to
+   the device. The library keeps no pointer into caller memory. */
+int mirt_scene_upload(mirt_ctx *ctx, const mirt_sphere *spheres, int num_spheres, const mirt_bvh_node *root);
+int mirt_scene_upload_flat(mirt_ctx *ctx, const mirt_sphere *spheres, int num_spheres,
+                           const mirt_node *nodes, int num_nodes);
+
+/* ---------------------------------------------------------- rendering */
+
+/* Number of rows (and the row indices, if rows != NULL) a shard renders. */
+int mirt_shard_rows(const mirt_frame_desc *fd, int32_t *rows);
+
+/* The pixel loop of main.c:356-374 (fresh) / main.c:382-407 (accumulate) for
+   the shard described by fd: writes the displayed RGBA8 colour of every pixel
+   of the shard's rows, compacted in shard row order, to host memory `out`
+   (num_rows * width). Accumulation state lives on the device (per ctx). */
+int mirt_render_frame(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_desc *fd, mirt_rgba8 *out);
+
+/* Same, asynchronously on `stream` (a hipStream_t, NULL = the ctx stream),
+   into device memory: d_out = num_rows * width packed RGBA8. d_accum is a
+   device float buffer of num_rows * width * 3 (may be NULL when
+   fd->accumulate == 0). Inputs are already resident in HBM. */
+int mirt_render_frame_device(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_desc *fd,
+                             uint32_t *d_out, float *d_accum, void *stream);
+
+/* Download the ctx's accumulation buffer (row-major float3 of the shard). */
+int mirt_accum_download(mirt_ctx *ctx, float *out, size_t count);
+
+/* trace_ray (renderer.c:21-77) on n arbitrary rays; ray i uses RNG contract
+   pixel index i. */
+int mirt_trace_rays(mirt_ctx *ctx, const mirt_ray *rays, int n, int depth, int use_bvh,
+                    uint64_t seed, uint32_t sample, mirt_rgba8 *out);
+
+/* Closest hit: ray_bvh_intersect (hit.c:91-109) when use_bvh, else the brute
+   force loop of renderer.c:36-43. */
+int mirt_intersect_rays(mirt_ctx *ctx, const mirt_ray *rays, int n, int use_bvh, mirt_hit *out);
+
+/* Element-wise ray_sphere_intersect (hit.c:19-39) / ray_aabb_intersect
+   (hit.c:49-82) on pairs; need no scene. */
+int mirt_sphere_pairs(mirt_ctx *ctx, const mirt_ray *rays, const mirt_sphere *spheres, int n, mirt_hit *out);
+int mirt_aabb_pairs(mirt_ctx *ctx, const mirt_ray *rays, const mirt_aabb *boxes, int n, int32_t *out);
+
+/* The camera ray of every pixel of the shard (ray.c:17-32 with the pixel
+   mapping of main.c:356-365). */
+int mirt_camera_rays(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_desc *fd, mirt_ray *out);
+
+/* Reference-DFS work counters of one frame (instrumented kernel build,
+   untimed): the algorithmic-bytes numerator of SURVEY §8(d). */
+int mirt_count_frame(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_desc *fd, mirt_counts *out);
+
+/* Device time (ms) of the last render kernel launched by a blocking call. */
+float mirt_last_kernel_ms(mirt_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MIRT_H */
