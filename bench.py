@@ -1,0 +1,226 @@
+"""Headline benchmark: Mrays/s of the primary-ray render path at 1920x1080 with
+10,000 random spheres (BASELINE.json configs[1]): camera rays -> BVH
+traversal + ray/sphere tests -> diffuse shading (depth 5, the reference's
+MAX_DEPTH, main.c:19/366) -> RGBA8 framebuffer.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...     (N > 1)
+
+One step = one frame: every rank renders its interleaved 8-row blocks of the
+frame into its HBM slab (scene resident, uploaded once), and for N > 1 the
+slabs are gathered to rank 0 over RCCL and de-interleaved there. value =
+W*H primary rays per step * K / (max over ranks of the timed region).
+Rank 0 prints one JSON line.
+"""
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+mirt = importlib.import_module("cs201_sah-bvh_ray_tracer_amd")
+shard = importlib.import_module("cs201_sah-bvh_ray_tracer_amd.shard")
+
+W, H, NSPH, DEPTH, SEED, ROW_BLOCK = 1920, 1080, 10000, 5, 1, 8
+PEAK_HBM_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+NODE_B, SPHERE_B, COLOR_B, PIXEL_B = 32, 16, 4, 4
+KERNEL = "render_kernel<4, true, false>"   # default schedule: hybrid walk without prefetch, fast slab
+
+
+def algorithmic_bytes(c, pixels):
+    """per frame, sum over traced rays of 32 B per reference-DFS
+    node test + 16 B per sphere test, 4 B per hit colour, 4 B per pixel written."""
+    return NODE_B * c["nodes"] + SPHERE_B * c["spheres"] + COLOR_B * c["hits"] + PIXEL_B * pixels
+
+
+def cpu_baseline(target_s=12.0):
+    """The reference render path on this host's cores: oracle/_ref (the
+    unmodified reference sources compiled in-tree) if present, else the
+    oracle restatement. Bounded sample: evenly spaced rows of the same
+    frame, stride chosen so the run takes ~target_s."""
+    from oracle.lib import Oracle, Reference
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    try:
+        ref = Reference(W, H)
+        kind = "reference"
+    except (FileNotFoundError, OSError):
+        ref, kind = None, "port"
+    o = Oracle()
+    s = o.render_scene(SEED, NSPH)                 # same scene (bit-identical generator)
+    cam = mirt.default_camera()
+    if ref is not None:
+        s_ref = s.copy()
+        tree = ref.build(s_ref)
+
+        def run(step, nthreads):
+            t0 = time.perf_counter()
+            img = ref.render(cam, s_ref, tree, depth=DEPTH, mode=1, seed=SEED, row0=0, step=step,
+                             threads=nthreads)
+            return time.perf_counter() - t0, img.shape[0]
+    else:
+        tree = o.build(s)
+
+        def run(step, nthreads):
+            rows = np.arange(0, H, step, dtype=np.int32)
+            t0 = time.perf_counter()
+            o.render(cam, W, H, s, tree, depth=DEPTH, mode=1, seed=SEED, rows=rows, threads=nthreads)
+            return time.perf_counter() - t0, len(rows)
+
+    probe_t, probe_rows = run(max(1, H // (2 * threads)), threads)   # ~2 rows per thread
+    per_row = probe_t / max(probe_rows, 1)
+    step = max(1, int(np.ceil(H * per_row / target_s)))
+    t, rows = run(step, threads)
+    value = rows * W / t / 1e6
+    t1, rows1 = run(max(step * threads, 1), 1)     # single core, same row density / threads
+    value1 = rows1 * W / t1 / 1e6
+    if ref is not None:
+        ref.free(tree)
+    else:
+        o.free(tree)
+    return {"value": round(value, 5), "unit": "Mrays/s", "cores": threads, "kind": kind,
+            "sample": f"every {step}th row of the 1920x1080 frame ({rows} rows, {rows * W} primary rays, "
+                      f"depth {DEPTH}, {threads} OpenMP threads, row-dynamic schedule) in {t:.1f} s",
+            "single_core_value": round(value1, 5),
+            "single_core_sample": f"every {max(step * threads, 1)}th row ({rows1} rows) in {t1:.1f} s"}
+
+
+def load_traffic(kernel):
+    """Per-launch HBM bytes of the render kernel from the committed PMC
+    profile (profiles/pmc_render.json, written by scripts/collect_profiles.py
+    from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this bench), if
+    it was taken on this workload and kernel."""
+    p = os.path.join(ROOT, "profiles", "pmc_render.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        d = json.load(f)
+    if d.get("workload") != [W, H, NSPH, DEPTH] or d.get("kernel") != kernel:
+        return None
+    return d.get("hbm_bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-host", action="store_true", help="skip the host-inclusive (D2H) leg")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
+
+    spheres = mirt.create_random_spheres(NSPH, SEED)
+    t0 = time.perf_counter()
+    bvh = mirt.build_bvh(spheres)
+    build_s = time.perf_counter() - t0
+    r = mirt.Renderer(local if world > 1 else 0)
+    r.upload(spheres, bvh)
+    cam = mirt.default_camera()
+    sf = shard.ShardedFrame(r, W, H, ROW_BLOCK)
+    fd = sf.desc(depth=DEPTH, seed=SEED)
+    my_rows = shard.shard_row_count(H, ROW_BLOCK, world, rank)
+
+    # algorithmic work of this rank's launch (instrumented build, untimed)
+    counts = r.count_frame(cam, W, H, depth=DEPTH, seed=SEED, row_block=ROW_BLOCK, shard=rank, num_shards=world)
+    alg_bytes = algorithmic_bytes(counts, my_rows * W)
+
+    # one non-default stream for the kernel, the RCCL gather and the timing
+    # events (torch.cuda.Event records on it)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    for _ in range(args.warmup):
+        sf.render(cam, fd)
+    torch.cuda.synchronize()
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        evs[k][0].record(stream)
+        sf.render_local(cam, fd)
+        evs[k][1].record(stream)
+        if world > 1:
+            shard.gather_frame(sf.slab, H, ROW_BLOCK)   # N = 1: the slab is the frame
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+
+    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kernel_ms_max = float(t[0]), float(t[1])
+
+    if rank == 0:
+        value = W * H * args.steps / elapsed / 1e6
+        achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
+        traffic = load_traffic(KERNEL) if world == 1 else None
+        # the same frame through the blocking host API (kernel + D2H over PCIe)
+        host = None
+        if world == 1 and not args.no_host:
+            img = r.render_frame(cam, W, H, depth=DEPTH, seed=SEED)
+            t1 = time.perf_counter()
+            for _ in range(5):
+                img = r.render_frame(cam, W, H, depth=DEPTH, seed=SEED)
+            host = W * H * 5 / (time.perf_counter() - t1) / 1e6
+        line = {
+            "metric": "Mrays/s at 1080p, 10k spheres; 1/2/4/8 GPU + CPU baseline",
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (create_random_sphere scene, srand(1); default camera main.c:203-211)",
+            "config": {"workload": "1920x1080, 10000 random spheres, 1 primary ray/pixel, diffuse shading "
+                                   "depth 5 (BASELINE configs[1])",
+                       "width": W, "height": H, "spheres": NSPH, "max_depth": DEPTH, "spp": 1,
+                       "bvh_nodes": len(bvh), "row_block": ROW_BLOCK,
+                       "parallelism": f"row-block shard x{world}" + (" + RCCL gather" if world > 1 else "")},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
+                         "kernel": KERNEL, "kernel_ms": round(kernel_ms, 4),
+                         "algorithmic_bytes_per_launch": int(alg_bytes),
+                         "note": "effective bandwidth of reference-DFS node/sphere reads; the working set is "
+                                 "L2/MALL-resident, so frac can exceed what HBM alone would allow"},
+            "work": {k: int(v) for k, v in counts.items()},
+            "traced_rays_per_s_M": round(counts["rays"] * world / (kernel_ms_max / 1e3) / 1e6, 3),
+            "host_inclusive_mrays_s": None if host is None else round(host, 3),
+            "bvh_build_s": round(build_s, 4),
+        }
+        if world == 1 and not args.no_cpu:
+            cb = cpu_baseline()
+            line["cpu_baseline"] = cb
+            line["speedup_vs_cpu"] = round(value / cb["value"], 1)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    r.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -59,7 +59,8 @@ class FrameDesc(C.Structure):
 
 class Counts(C.Structure):
     """mirt_counts"""
-    _fields_ = [("rays", C.c_uint64), ("nodes", C.c_uint64), ("spheres", C.c_uint64), ("hits", C.c_uint64)]
+    _fields_ = [("rays", C.c_uint64), ("nodes", C.c_uint64), ("spheres", C.c_uint64), ("hits", C.c_uint64),
+                ("lane_steps", C.c_uint64)]
 
 
 def default_camera():
@@ -116,5 +117,11 @@ SIGNATURES = [
     ("mirt_aabb_pairs", I, [P, P, P, I, P]),
     ("mirt_camera_rays", I, [P, P, P, P]),
     ("mirt_count_frame", I, [P, P, P, P]),
+    ("mirt_wave_stats", I, [P, P, P, P, I]),
     ("mirt_last_kernel_ms", C.c_float, [P]),
+    ("mirt_set_option", I, [P, I, I]),
+    ("mirt_get_option", I, [P, I]),
 ]
+
+OPT_TRAVERSAL, OPT_FAST_SLAB, OPT_BLOCK_WAVES = 1, 2, 3
+TRAV_UNIFORM, TRAV_LANE, TRAV_HYBRID, TRAV_LANE_NP, TRAV_HYBRID_NP = 0, 1, 2, 3, 4

@@ -101,22 +101,38 @@ __device__ __forceinline__ void add_counts(mirt_counts* out, const Counters& c)
     atomicAdd((unsigned long long*)&out->nodes, (unsigned long long)c.nodes);
     atomicAdd((unsigned long long*)&out->spheres, (unsigned long long)c.spheres);
     atomicAdd((unsigned long long*)&out->hits, (unsigned long long)c.hits);
+    atomicAdd((unsigned long long*)&out->lane_steps, (unsigned long long)c.steps);
 }
 
 // The pixel loop of main.c:358-374 (fresh) / main.c:382-407 (accumulate).
-template <bool UNIFORM, bool COUNT>
-__global__ __launch_bounds__(256) void render_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
-                                                      float* __restrict__ acc, mirt_counts* counts)
+template <int TRAV, bool FAST, bool COUNT>
+__global__ __launch_bounds__(512) void render_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
+                                                      float* __restrict__ acc, mirt_counts* counts,
+                                                      uint32_t* wave_stats)
 {
+    uint64_t t0 = 0;
+    if (COUNT) t0 = __builtin_amdgcn_s_memrealtime();
     int x, r;
     tile_pixel(f, x, r);
     const bool alive = x < f.width && r < f.num_rows;
     const int y = alive ? shard_row_to_y(f, r) : 0;
     const Ray ray = camera_ray(f, alive ? x : 0, y);
     const uint64_t key = pixel_key(f.seed, (uint32_t)(y * f.width + x), f.sample);
-    Counters cnt{0, 0, 0, 0};
-    const uint32_t c = trace_path<UNIFORM, COUNT>(sc, ray, alive, f.depth, f.use_bvh != 0, key, cnt);
-    if (COUNT) add_counts(counts, cnt);
+    Counters cnt{0, 0, 0, 0, 0};
+    const uint32_t c = trace_path<TRAV, FAST, COUNT>(sc, ray, alive, f.depth, f.use_bvh != 0, key, cnt);
+    if (COUNT) {
+        add_counts(counts, cnt);
+        if (wave_stats && (threadIdx.x & 63) == 0) {
+            // diagnostic: {tile, traversal steps of this wave, start, end} (100 MHz clock)
+            const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+            const uint32_t tile = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+            uint32_t* w = wave_stats + 4 * (size_t)tile;
+            w[0] = tile;
+            w[1] = cnt.steps;
+            w[2] = (uint32_t)t0;
+            w[3] = (uint32_t)t1;
+        }
+    }
     if (!alive) return;
     const size_t i = (size_t)r * f.width + x;
     uint32_t shown = c;
@@ -138,7 +154,7 @@ __global__ __launch_bounds__(256) void render_kernel(DevScene sc, FrameConst f, 
 }
 
 // trace_ray on explicit rays (renderer.c:21); ray i uses contract pixel i.
-template <bool UNIFORM>
+template <int TRAV, bool FAST>
 __global__ __launch_bounds__(256) void trace_rays_kernel(DevScene sc, const mirt_ray* __restrict__ rays, int n,
                                                          int depth, int use_bvh, uint64_t seed, uint32_t sample,
                                                          uint32_t* __restrict__ out)
@@ -147,8 +163,8 @@ __global__ __launch_bounds__(256) void trace_rays_kernel(DevScene sc, const mirt
     const bool alive = i < n;
     const mirt_ray& rr = rays[alive ? i : 0];
     const Ray ray{rr.origin.x, rr.origin.y, rr.origin.z, rr.direction.x, rr.direction.y, rr.direction.z};
-    Counters cnt{0, 0, 0, 0};
-    const uint32_t c = trace_path<UNIFORM, false>(sc, ray, alive, depth, use_bvh != 0,
+    Counters cnt{0, 0, 0, 0, 0};
+    const uint32_t c = trace_path<TRAV, FAST, false>(sc, ray, alive, depth, use_bvh != 0,
                                                   pixel_key(seed, (uint32_t)i, sample), cnt);
     if (alive) out[i] = c;
 }
@@ -171,6 +187,7 @@ __device__ __forceinline__ void store_hit(const Ray& ray, float t, int s, const 
 }
 
 // ray_bvh_intersect (hit.c:91) / brute-force closest hit (renderer.c:36-43)
+template <bool FAST>
 __global__ __launch_bounds__(256) void intersect_kernel(DevScene sc, const mirt_ray* __restrict__ rays, int n,
                                                         int use_bvh, mirt_hit* __restrict__ out)
 {
@@ -178,13 +195,13 @@ __global__ __launch_bounds__(256) void intersect_kernel(DevScene sc, const mirt_
     const bool alive = i < n;
     const mirt_ray& rr = rays[alive ? i : 0];
     const Ray ray{rr.origin.x, rr.origin.y, rr.origin.z, rr.direction.x, rr.direction.y, rr.direction.z};
-    Counters cnt{0, 0, 0, 0};
+    Counters cnt{0, 0, 0, 0, 0};
     float t;
     int s;
     if (use_bvh)
-        closest_bvh<true, false>(sc, ray, alive, t, s, cnt);
+        closest_hit<true, FAST, false>(sc, ray, alive, t, s, cnt);
     else
-        closest_brute<false>(sc, ray, alive, t, s, cnt);
+        closest_brute<FAST, false>(sc, ray, alive, t, s, cnt);
     if (alive) store_hit(ray, t, s, sc, &out[i]);
 }
 
@@ -197,7 +214,7 @@ __global__ void sphere_pairs_kernel(const mirt_ray* __restrict__ rays, const mir
     const mirt_ray rr = rays[i];
     const Ray ray{rr.origin.x, rr.origin.y, rr.origin.z, rr.direction.x, rr.direction.y, rr.direction.z};
     const float4 g = make_float4(sph[i].center.x, sph[i].center.y, sph[i].center.z, sph[i].radius);
-    const float t = sphere_t(sph_ray(ray), g);
+    const float t = sphere_t<false>(sph_ray(ray), g, INFINITY);
     mirt_hit h;
     memset(&h, 0, sizeof h);
     h.sphere = -1;
@@ -244,7 +261,7 @@ struct mirt_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     float last_ms = 0.0f;
     // scene (replicated per device, uploaded once)
-    mirt_node* d_nodes = nullptr;
+    DNode* d_nodes = nullptr;
     float4* d_geo = nullptr;
     uint32_t* d_color = nullptr;
     int num_nodes = 0, num_spheres = -1;
@@ -257,6 +274,10 @@ struct mirt_ctx {
     void* d_res = nullptr;
     size_t in_cap = 0, res_cap = 0;
     mirt_counts* d_counts = nullptr;
+    // kernel schedule (mirt_set_option)
+    int trav = kTravHybridNP;
+    int fast_slab = 1;
+    int block_waves = 4;  // waves (8x8 tiles) per workgroup
 };
 
 namespace {
@@ -302,20 +323,49 @@ bool ctx_ok(mirt_ctx* c, bool need_scene, const char* fn)
     return hipSetDevice(c->device) == hipSuccess;
 }
 
-// Default traversal for frame rendering (wave-uniform walk, scalar loads).
-constexpr bool kUniform = true;
+template <int TRAV, bool FAST>
+void launch_render_t(const DevScene& sc, const FrameConst& f, uint32_t* d_out, float* d_acc, hipStream_t s,
+                     int blocks, int bw)
+{
+    render_kernel<TRAV, FAST, false><<<blocks, 64 * bw, 0, s>>>(sc, f, d_out, d_acc, nullptr, nullptr);
+}
 
 int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_acc, hipStream_t s, bool timed,
-                  mirt_counts* d_counts)
+                  mirt_counts* d_counts, uint32_t* d_wave_stats = nullptr)
 {
     const int tiles = ((f.width + 7) / 8) * ((f.num_rows + 7) / 8);
-    const int blocks = (tiles + 3) / 4;
+    const int bw = c->block_waves;
+    const int blocks = (tiles + bw - 1) / bw;
     if (blocks == 0) return MIRT_OK;
     if (timed) HIP_TRY(hipEventRecord(c->ev0, s));
-    if (d_counts)
-        render_kernel<kUniform, true><<<blocks, 256, 0, s>>>(dev_scene(c), f, d_out, d_acc, d_counts);
-    else
-        render_kernel<kUniform, false><<<blocks, 256, 0, s>>>(dev_scene(c), f, d_out, d_acc, nullptr);
+    const DevScene sc = dev_scene(c);
+    if (d_counts) {
+        // the work counters are schedule independent except lane_steps
+        if (c->trav == kTravUniform)
+            render_kernel<kTravUniform, true, true><<<blocks, 64 * bw, 0, s>>>(sc, f, d_out, d_acc, d_counts, d_wave_stats);
+        else if (c->trav == kTravLane)
+            render_kernel<kTravLane, true, true><<<blocks, 64 * bw, 0, s>>>(sc, f, d_out, d_acc, d_counts, d_wave_stats);
+        else
+            render_kernel<kTravHybrid, true, true><<<blocks, 64 * bw, 0, s>>>(sc, f, d_out, d_acc, d_counts, d_wave_stats);
+    } else {
+        const bool fast = c->fast_slab != 0;
+#define MIRT_LAUNCH_TRAV(T)                                                          \
+    case T:                                                                        \
+        fast ? launch_render_t<T, true>(sc, f, d_out, d_acc, s, blocks, bw)         \
+             : launch_render_t<T, false>(sc, f, d_out, d_acc, s, blocks, bw);       \
+        break;
+        switch (c->trav) {
+            MIRT_LAUNCH_TRAV(kTravUniform)
+            MIRT_LAUNCH_TRAV(kTravLane)
+            MIRT_LAUNCH_TRAV(kTravLaneNP)
+            MIRT_LAUNCH_TRAV(kTravHybridNP)
+        default:
+            fast ? launch_render_t<kTravHybrid, true>(sc, f, d_out, d_acc, s, blocks, bw)
+                 : launch_render_t<kTravHybrid, false>(sc, f, d_out, d_acc, s, blocks, bw);
+            break;
+        }
+#undef MIRT_LAUNCH_TRAV
+    }
     HIP_TRY(hipGetLastError());
     if (timed) HIP_TRY(hipEventRecord(c->ev1, s));
     return MIRT_OK;
@@ -399,10 +449,21 @@ int mirt_scene_upload_flat(mirt_ctx* c, const mirt_sphere* spheres, int ns, cons
     c->d_geo = nullptr;
     c->d_color = nullptr;
     c->num_spheres = -1;
-    HIP_TRY(hipMalloc((void**)&c->d_nodes, sizeof(mirt_node) * (size_t)(nn > 0 ? nn : 1)));
+    // device layout: 64-B nodes with each leaf's sphere inline (trace.h DNode)
+    std::vector<DNode> dn((size_t)nn);
+    for (int i = 0; i < nn; i++) {
+        DNode& d = dn[i];
+        std::memset(&d, 0, sizeof d);
+        std::memcpy(d.bmin, nodes[i].bmin, sizeof d.bmin);
+        std::memcpy(d.bmax, nodes[i].bmax, sizeof d.bmax);
+        d.sphere = nodes[i].sphere;
+        d.skip = nodes[i].skip;
+        d.geo = nodes[i].sphere >= 0 ? geo[nodes[i].sphere] : geo[ns];
+    }
+    HIP_TRY(hipMalloc((void**)&c->d_nodes, sizeof(DNode) * (size_t)(nn > 0 ? nn : 1)));
     HIP_TRY(hipMalloc((void**)&c->d_geo, sizeof(float4) * geo.size()));
     HIP_TRY(hipMalloc((void**)&c->d_color, sizeof(uint32_t) * col.size()));
-    if (nn > 0) HIP_TRY(hipMemcpy(c->d_nodes, nodes, sizeof(mirt_node) * (size_t)nn, hipMemcpyHostToDevice));
+    if (nn > 0) HIP_TRY(hipMemcpy(c->d_nodes, dn.data(), sizeof(DNode) * (size_t)nn, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_geo, geo.data(), sizeof(float4) * geo.size(), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_color, col.data(), sizeof(uint32_t) * col.size(), hipMemcpyHostToDevice));
     c->num_nodes = nn;
@@ -435,7 +496,7 @@ int mirt_render_frame_device(mirt_ctx* c, const mirt_camera* cam, const mirt_fra
         return MIRT_E_NOSCENE;
     }
     const FrameConst f = make_frame_const(cam, fd);
-    return launch_render(c, f, d_out, d_acc, stream ? (hipStream_t)stream : c->stream, false, nullptr);
+    return launch_render(c, f, d_out, d_acc, (hipStream_t)stream, false, nullptr);
 }
 
 int mirt_render_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, mirt_rgba8* out)
@@ -499,6 +560,29 @@ int mirt_count_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc*
     return MIRT_OK;
 }
 
+int mirt_wave_stats(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, uint32_t* out, int cap)
+{
+    if (!ctx_ok(c, true, "mirt_wave_stats")) return MIRT_E_NOSCENE;
+    if (!cam || !frame_desc_valid(fd)) {
+        set_error("mirt_wave_stats: invalid arguments");
+        return MIRT_E_INVALID;
+    }
+    FrameConst f = make_frame_const(cam, fd);
+    f.accumulate = 0;
+    const int waves = ((f.width + 7) / 8) * ((f.num_rows + 7) / 8);
+    if (!out || cap < waves) return -waves;
+    const size_t pixels = (size_t)f.num_rows * f.width;
+    int rc = ensure((void**)&c->d_out, &c->out_cap, pixels * 4 + 4);
+    if (!rc) rc = ensure(&c->d_res, &c->res_cap, 16 * (size_t)waves + 64);
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(c->d_counts, 0, sizeof(mirt_counts), c->stream));
+    rc = launch_render(c, f, c->d_out, nullptr, c->stream, false, c->d_counts, (uint32_t*)c->d_res);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(out, c->d_res, 16 * (size_t)waves, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return waves;
+}
+
 int mirt_camera_rays(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, mirt_ray* out)
 {
     if (!ctx_ok(c, false, "mirt_camera_rays")) return MIRT_E_INVALID;
@@ -527,15 +611,32 @@ int mirt_trace_rays(mirt_ctx* c, const mirt_ray* rays, int n, int depth, int use
         set_error("mirt_trace_rays: invalid arguments");
         return MIRT_E_INVALID;
     }
+    if (use_bvh && c->num_nodes == 0) {
+        set_error("mirt_trace_rays: use_bvh set but no tree uploaded");
+        return MIRT_E_NOSCENE;
+    }
     if (n == 0) return MIRT_OK;
     int rc = ensure(&c->d_in, &c->in_cap, sizeof(mirt_ray) * (size_t)n);
     if (!rc) rc = ensure(&c->d_res, &c->res_cap, 4 * (size_t)n);
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(c->d_in, rays, sizeof(mirt_ray) * (size_t)n, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
-    trace_rays_kernel<kUniform><<<(n + 255) / 256, 256, 0, c->stream>>>(dev_scene(c), (const mirt_ray*)c->d_in, n,
-                                                                        depth, use_bvh, seed, sample,
-                                                                        (uint32_t*)c->d_res);
+    {
+        const dim3 g((n + 255) / 256), b(256);
+        const DevScene sc = dev_scene(c);
+        const mirt_ray* in = (const mirt_ray*)c->d_in;
+        uint32_t* res = (uint32_t*)c->d_res;
+        const bool fast = c->fast_slab != 0;
+        if (c->trav == kTravUniform)
+            fast ? trace_rays_kernel<kTravUniform, true><<<g, b, 0, c->stream>>>(sc, in, n, depth, use_bvh, seed, sample, res)
+                 : trace_rays_kernel<kTravUniform, false><<<g, b, 0, c->stream>>>(sc, in, n, depth, use_bvh, seed, sample, res);
+        else if (c->trav == kTravLane)
+            fast ? trace_rays_kernel<kTravLane, true><<<g, b, 0, c->stream>>>(sc, in, n, depth, use_bvh, seed, sample, res)
+                 : trace_rays_kernel<kTravLane, false><<<g, b, 0, c->stream>>>(sc, in, n, depth, use_bvh, seed, sample, res);
+        else
+            fast ? trace_rays_kernel<kTravHybrid, true><<<g, b, 0, c->stream>>>(sc, in, n, depth, use_bvh, seed, sample, res)
+                 : trace_rays_kernel<kTravHybrid, false><<<g, b, 0, c->stream>>>(sc, in, n, depth, use_bvh, seed, sample, res);
+    }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev1, c->stream));
     HIP_TRY(hipMemcpyAsync(out, c->d_res, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
@@ -551,14 +652,22 @@ int mirt_intersect_rays(mirt_ctx* c, const mirt_ray* rays, int n, int use_bvh, m
         set_error("mirt_intersect_rays: invalid arguments");
         return MIRT_E_INVALID;
     }
+    if (use_bvh && c->num_nodes == 0) {
+        set_error("mirt_intersect_rays: use_bvh set but no tree uploaded");
+        return MIRT_E_NOSCENE;
+    }
     if (n == 0) return MIRT_OK;
     int rc = ensure(&c->d_in, &c->in_cap, sizeof(mirt_ray) * (size_t)n);
     if (!rc) rc = ensure(&c->d_res, &c->res_cap, sizeof(mirt_hit) * (size_t)n);
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(c->d_in, rays, sizeof(mirt_ray) * (size_t)n, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
-    intersect_kernel<<<(n + 255) / 256, 256, 0, c->stream>>>(dev_scene(c), (const mirt_ray*)c->d_in, n, use_bvh,
-                                                            (mirt_hit*)c->d_res);
+    if (c->fast_slab)
+        intersect_kernel<true><<<(n + 255) / 256, 256, 0, c->stream>>>(dev_scene(c), (const mirt_ray*)c->d_in, n,
+                                                                      use_bvh, (mirt_hit*)c->d_res);
+    else
+        intersect_kernel<false><<<(n + 255) / 256, 256, 0, c->stream>>>(dev_scene(c), (const mirt_ray*)c->d_in, n,
+                                                                       use_bvh, (mirt_hit*)c->d_res);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev1, c->stream));
     HIP_TRY(hipMemcpyAsync(out, c->d_res, sizeof(mirt_hit) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
@@ -614,5 +723,37 @@ int mirt_aabb_pairs(mirt_ctx* c, const mirt_ray* rays, const mirt_aabb* boxes, i
 }
 
 float mirt_last_kernel_ms(mirt_ctx* c) { return c ? c->last_ms : 0.0f; }
+
+int mirt_set_option(mirt_ctx* c, int option, int value)
+{
+    if (!c) return MIRT_E_INVALID;
+    switch (option) {
+    case MIRT_OPT_TRAVERSAL:
+        if (value < MIRT_TRAV_UNIFORM || value > MIRT_TRAV_HYBRID_NP) break;
+        c->trav = value;
+        return MIRT_OK;
+    case MIRT_OPT_FAST_SLAB:
+        c->fast_slab = value != 0;
+        return MIRT_OK;
+    case MIRT_OPT_BLOCK_WAVES:
+        if (value != 1 && value != 2 && value != 4 && value != 8) break;
+        c->block_waves = value;
+        return MIRT_OK;
+    default:
+        break;
+    }
+    set_error("mirt_set_option: bad option %d / value %d", option, value);
+    return MIRT_E_INVALID;
+}
+
+int mirt_get_option(mirt_ctx* c, int option)
+{
+    if (!c) return MIRT_E_INVALID;
+    if (option == MIRT_OPT_TRAVERSAL) return c->trav;
+    if (option == MIRT_OPT_FAST_SLAB) return c->fast_slab;
+    if (option == MIRT_OPT_BLOCK_WAVES) return c->block_waves;
+    set_error("mirt_get_option: bad option %d", option);
+    return MIRT_E_INVALID;
+}
 
 }  // extern "C"

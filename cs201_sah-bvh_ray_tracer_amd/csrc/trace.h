@@ -4,8 +4,10 @@
 // Floating point follows the reference operation by operation (the .hip is
 // compiled with -ffp-contract=off; divisions and square roots are the IEEE
 // correctly rounded HIP defaults; the double-precision segments of
-// hit.c:28 and vec3.c:22 are computed in double). Anything else would move
-// the framebuffer away from the reference's bytes.
+// hit.c:28 and vec3.c:22 are computed in double). Where a cheaper estimate
+// is used (slab_fast, sphere_t), it only ever DECIDES an outcome when a
+// proven error bound shows the reference computation would decide the same
+// way, and falls back to the reference arithmetic otherwise.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -19,11 +21,24 @@ namespace mirt {
 constexpr float kEps = 0.000001f;  // constants.h:6
 constexpr int kMaxDepth = 8;       // bounce levels kept in registers
 
-// Read-only scene in HBM. Loads whose index is wave-uniform go through the
-// constant address space so they become scalar (s_load) loads.
+// Device copy of a flattened node (mirt_node, include/mirt.h) padded to 64 B,
+// with the leaf's sphere (centre, radius) inline so a leaf step needs no
+// second, dependent load. Inner nodes and the &spheres[N] sentinel carry NaN
+// geometry (never hits).
+struct __attribute__((aligned(64))) DNode {
+    float bmin[3];
+    float bmax[3];
+    int32_t sphere;   // leaf: sphere index; inner: -1
+    uint32_t skip;    // next node after this subtree | MIRT_NODE_EMPTY
+    float4 geo;       // leaf sphere centre.xyz, radius
+    uint32_t pad[4];
+};
+static_assert(sizeof(DNode) == 64, "device node is 64 B");
+
+// Read-only scene in HBM (L2 / Infinity-Cache resident at the BASELINE sizes).
 struct DevScene {
-    const mirt_node* nodes;
-    const float4* geo;      // centre.xyz, radius; [num_spheres] = NaN sentinel (never hits)
+    const DNode* nodes;
+    const float4* geo;      // centre.xyz, radius per sphere; [num_spheres] = NaN sentinel
     const uint32_t* color;  // packed RGBA8
     uint32_t num_nodes;
     int num_spheres;
@@ -35,47 +50,59 @@ struct Ray {
 
 struct Counters {
     uint32_t rays, nodes, spheres, hits;
+    uint32_t steps;  // traversal loop iterations executed (every lane counts; /64 = wave steps)
+};
+
+// A node in registers (12 dwords).
+struct NodeV {
+    float b0, b1, b2, b3, b4, b5;
+    int32_t sphere;
+    uint32_t skip;
+    float4 g;
 };
 
 typedef const __attribute__((address_space(4))) uint32_t cu32_t;
 typedef const __attribute__((address_space(4))) float cf32_t;
 
 // Wave-uniform index -> read through the constant address space, which the
-// backend lowers to scalar loads (s_load_dwordx8 for a node, x4 for a sphere).
-__device__ __forceinline__ mirt_node load_node_uniform(const mirt_node* base, uint32_t i)
+// backend lowers to scalar loads (s_load_dwordx8 + x4 for a node).
+__device__ __forceinline__ NodeV load_node_uniform(const DNode* base, uint32_t i)
 {
-    const cu32_t* p = (const cu32_t*)base + 8u * i;
-    mirt_node n;
-    n.bmin[0] = __uint_as_float(p[0]);
-    n.bmin[1] = __uint_as_float(p[1]);
-    n.bmin[2] = __uint_as_float(p[2]);
-    n.bmax[0] = __uint_as_float(p[3]);
-    n.bmax[1] = __uint_as_float(p[4]);
-    n.bmax[2] = __uint_as_float(p[5]);
+    const cu32_t* p = (const cu32_t*)base + 16u * i;
+    NodeV n;
+    n.b0 = __uint_as_float(p[0]);
+    n.b1 = __uint_as_float(p[1]);
+    n.b2 = __uint_as_float(p[2]);
+    n.b3 = __uint_as_float(p[3]);
+    n.b4 = __uint_as_float(p[4]);
+    n.b5 = __uint_as_float(p[5]);
     n.sphere = (int32_t)p[6];
     n.skip = p[7];
+    n.g = make_float4(__uint_as_float(p[8]), __uint_as_float(p[9]), __uint_as_float(p[10]), __uint_as_float(p[11]));
     return n;
 }
+
 __device__ __forceinline__ float4 load_geo_uniform(const float4* base, int i)
 {
     const cf32_t* p = (const cf32_t*)base + 4 * i;
     return make_float4(p[0], p[1], p[2], p[3]);
 }
 
-// Divergent index -> two 16-B vector loads per node.
-__device__ __forceinline__ mirt_node load_node_lane(const mirt_node* base, uint32_t i)
+// Divergent index -> three 16-B vector loads per node.
+__device__ __forceinline__ NodeV load_node_lane(const DNode* base, uint32_t i)
 {
     const float4* p = (const float4*)(base + i);
-    const float4 a = p[0], b = p[1];
-    mirt_node n;
-    n.bmin[0] = a.x;
-    n.bmin[1] = a.y;
-    n.bmin[2] = a.z;
-    n.bmax[0] = a.w;
-    n.bmax[1] = b.x;
-    n.bmax[2] = b.y;
+    const float4 a = p[0], b = p[1], g = p[2];
+    NodeV n;
+    n.b0 = a.x;
+    n.b1 = a.y;
+    n.b2 = a.z;
+    n.b3 = a.w;
+    n.b4 = b.x;
+    n.b5 = b.y;
     n.sphere = __float_as_int(b.z);
     n.skip = __float_as_uint(b.w);
+    n.g = g;
     return n;
 }
 
@@ -103,15 +130,32 @@ __device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, fl
 }
 
 // Per-ray constants of the slab test (hit.c:54-76): the per-axis d == 0
-// branch does not depend on the box.
+// branch does not depend on the box, nor do the reciprocals of slab_fast.
 struct SlabRay {
     float ox, oy, oz, dx, dy, dz;
+    float ix, iy, iz;  // correctly rounded 1/d
     bool zx, zy, zz;
+    bool generic;      // a zero or tiny (< 2^-40) direction component: exact test only
 };
 
 __device__ __forceinline__ SlabRay slab_ray(const Ray& r)
 {
-    return {r.ox, r.oy, r.oz, r.dx, r.dy, r.dz, r.dx == 0.0f, r.dy == 0.0f, r.dz == 0.0f};
+    SlabRay s;
+    s.ox = r.ox;
+    s.oy = r.oy;
+    s.oz = r.oz;
+    s.dx = r.dx;
+    s.dy = r.dy;
+    s.dz = r.dz;
+    s.zx = r.dx == 0.0f;
+    s.zy = r.dy == 0.0f;
+    s.zz = r.dz == 0.0f;
+    const float tiny = 0x1p-40f;
+    s.generic = !(fabsf(r.dx) >= tiny && fabsf(r.dy) >= tiny && fabsf(r.dz) >= tiny);
+    s.ix = 1.0f / r.dx;
+    s.iy = 1.0f / r.dy;
+    s.iz = 1.0f / r.dz;
+    return s;
 }
 
 // hit.c:49-82: true IEEE division per axis (no reciprocal: SURVEY §8.H3),
@@ -137,34 +181,86 @@ __device__ __forceinline__ bool slab_test(const SlabRay& r, float x0, float y0, 
     return tmax >= tmin && tmax > kEps;
 }
 
+// The same predicate, decided from reciprocal-multiply estimates whenever
+// that is provably safe, else by slab_test (same result, bit for bit).
+//
+// For a = RN(b - o) (computed identically in both), Q = RN(a / d) is the
+// reference's slab value and q = RN(a * RN(1/d)) ours: |q - Q| <= 3u|a/d|,
+// u = 2^-24 (one rounding in 1/d, one in the product, Q's own half ulp), so
+// every t value moves by < 2^-22 |t|; max/min select from values that moved
+// that little, so |tmin' - tmin| and |tmax' - tmax| stay < 2^-22 of their
+// magnitudes, and the two subtractions below add < 2^-24 (|tmin|+|tmax|).
+// m = 2^-20 (|tmin'| + |tmax'|) therefore bounds every perturbation with a
+// 2x margin: when a comparison clears m it has the reference's outcome;
+// otherwise (near-tangent boxes) the exact division path decides.
+// Requires finite, normal-range reciprocals: rays with a zero or tiny
+// component take slab_test (`generic`), whose +-inf handling is exact.
+__device__ __forceinline__ bool slab_fast(const SlabRay& r, float x0, float y0, float z0, float x1, float y1,
+                                          float z1)
+{
+    const float tx1 = (x0 - r.ox) * r.ix, tx2 = (x1 - r.ox) * r.ix;
+    const float ty1 = (y0 - r.oy) * r.iy, ty2 = (y1 - r.oy) * r.iy;
+    const float tz1 = (z0 - r.oz) * r.iz, tz2 = (z1 - r.oz) * r.iz;
+    const float tmin = fmaxf(fminf(tx1, tx2), fmaxf(fminf(ty1, ty2), fminf(tz1, tz2)));
+    const float tmax = fminf(fmaxf(tx1, tx2), fminf(fmaxf(ty1, ty2), fmaxf(tz1, tz2)));
+    const float m = (fabsf(tmin) + fabsf(tmax)) * 0x1p-20f;
+    const float gap = tmax - tmin, above = tmax - kEps;
+    if (gap > m && above > m) return true;
+    if (gap < -m || above < -m) return false;
+    return slab_test(r, x0, y0, z0, x1, y1, z1);
+}
+
+template <bool FAST>
+__device__ __forceinline__ bool slab(const SlabRay& r, const NodeV& n)
+{
+    if (FAST && !r.generic) return slab_fast(r, n.b0, n.b1, n.b2, n.b3, n.b4, n.b5);
+    return slab_test(r, n.b0, n.b1, n.b2, n.b3, n.b4, n.b5);
+}
+
 // Per-ray constants of ray_sphere_intersect: a = d.d, 4a and 2a (hit.c:22-28).
 struct SphRay {
     float ox, oy, oz, dx, dy, dz;
     float a4;     // 4 * a  (hit.c:25: 4 * a * c evaluates (4 * a) * c)
+    float inv2a;  // ~1 / (2a), for the estimate only
     double a2;    // (double)(2.0f * a)
 };
 
 __device__ __forceinline__ SphRay sph_ray(const Ray& r)
 {
     const float a = dot3(r.dx, r.dy, r.dz, r.dx, r.dy, r.dz);
-    return {r.ox, r.oy, r.oz, r.dx, r.dy, r.dz, 4.0f * a, (double)(2.0f * a)};
+    return {r.ox, r.oy, r.oz, r.dx, r.dy, r.dz, 4.0f * a, 1.0f / (2.0f * a), (double)(2.0f * a)};
 }
 
-// hit.c:19-39 without the point/normal (computed once for the winner).
-// Returns t > EPS on a hit, else -1.
-__device__ __forceinline__ float sphere_t(const SphRay& r, float4 s)
+// hit.c:19-39 without point/normal (computed once for the winner): the t a
+// hit would record if it could still become the closest (t <= best, the
+// later-DFS-leaf-wins tie rule), else -1.
+//
+// The discriminant is the reference's float expression (it alone decides
+// hit vs miss). t itself is hit.c:28 in double, rounded to float, which costs
+// a chain of f64 sqrt/div; it is only evaluated when a float estimate cannot
+// rule the hit out. Estimate: s' = sqrt(disc) to ~1 ulp, t' = RN(-b - s') *
+// RN(1/(2a)); every step is within a few u = 2^-24 relative of its operands,
+// so |t' - t| < 8u (|b| + s') / 2a, and M = 2^-18 (|b| + s') |1/(2a)| bounds
+// that 8x over. If t' - M > best the recorded t would exceed best (cannot
+// win); if t' + M <= EPS it would fail t > EPS. Otherwise the exact path runs.
+template <bool FAST>
+__device__ __forceinline__ float sphere_t(const SphRay& r, float4 s, float best)
 {
     const float ocx = r.ox - s.x, ocy = r.oy - s.y, ocz = r.oz - s.z;
     const float b = 2.0f * dot3(ocx, ocy, ocz, r.dx, r.dy, r.dz);
     const float c = dot3(ocx, ocy, ocz, ocx, ocy, ocz) - s.w * s.w;
     const float disc = b * b - r.a4 * c;
-    if (disc > 0.0f) {
-        // hit.c:28 in double: (-b - sqrt(disc)) / (2a), rounded to float
-        const double num = (double)(-b) - __dsqrt_rn((double)disc);
-        const float t = (float)__ddiv_rn(num, r.a2);
-        if (t > kEps) return t;
+    if (!(disc > 0.0f)) return -1.0f;
+    if (FAST) {
+        const float sq = __builtin_amdgcn_sqrtf(disc);
+        const float te = (-b - sq) * r.inv2a;
+        const float m = (fabsf(b) + sq) * fabsf(r.inv2a) * 0x1p-18f;
+        if (te - m > best || te + m <= kEps) return -1.0f;
     }
-    return -1.0f;
+    // hit.c:28 in double: (-b - sqrt(disc)) / (2a), rounded to float
+    const double num = (double)(-b) - __dsqrt_rn((double)disc);
+    const float t = (float)__ddiv_rn(num, r.a2);
+    return (t > kEps && t <= best) ? t : -1.0f;
 }
 
 // Closest hit over the flattened tree in the reference's DFS order
@@ -178,89 +274,269 @@ __device__ __forceinline__ float sphere_t(const SphRay& r, float4 s)
 // that did not reach i have next >= skip(i) (no walk can enter a subtree
 // without visiting its root), so the cursor advances to i + 1 if any lane
 // descended and to skip(i) otherwise -- no stack, no reduction, and every
-// node / sphere load is a scalar load.
+// node load is a scalar load.
 // Otherwise (LANE): every lane walks its own sequence with vector loads.
-template <bool UNIFORM, bool COUNT>
+//
+// Both walks are latency-bound chains (load -> test -> next index), so each
+// step issues the loads of BOTH possible successors (i + 1 and skip(i))
+// before testing node i; the test then overlaps the load latency.
+template <bool UNIFORM, bool FAST, bool COUNT, bool LPF = true>
 __device__ __forceinline__ void closest_bvh(const DevScene& sc, const Ray& ray, bool active, float& best_t,
                                             int& best_s, Counters& cnt)
 {
     const SlabRay sr = slab_ray(ray);
     const SphRay sp = sph_ray(ray);
     const uint32_t end = sc.num_nodes;
+    const uint32_t last = end - 1;
     uint32_t next = active ? 0u : end;
     best_t = INFINITY;
     best_s = -1;
     if constexpr (UNIFORM) {
         uint32_t cur = __builtin_amdgcn_readfirstlane(__ballot(active) ? 0u : end);
+        if (cur >= end) return;
+        NodeV nd = load_node_uniform(sc.nodes, cur);
         while (cur < end) {
-            const mirt_node nd = load_node_uniform(sc.nodes, cur);
+            if (COUNT) cnt.steps++;
             const uint32_t skip = nd.skip & MIRT_SKIP_MASK;
+            const bool inner = nd.sphere < 0;
+            // both loads always issue (a leaf's skip is i + 1: the second is a
+            // scalar-cache hit); nothing reads them until the step is decided
+            const NodeV na = load_node_uniform(sc.nodes, min(cur + 1, last));
+            const NodeV nb = load_node_uniform(sc.nodes, min(skip, last));
             bool descend = false;
             if (next == cur) {
-                const bool pass = (nd.skip & MIRT_NODE_EMPTY) ||
-                                  slab_test(sr, nd.bmin[0], nd.bmin[1], nd.bmin[2], nd.bmax[0], nd.bmax[1], nd.bmax[2]);
+                const bool pass = (nd.skip & MIRT_NODE_EMPTY) || slab<FAST>(sr, nd);
                 if (COUNT) cnt.nodes++;
-                if (pass && nd.sphere < 0) {
+                if (pass && inner) {
                     next = cur + 1;
                     descend = true;
                 } else {
                     next = skip;
                     if (pass) {
                         if (COUNT) cnt.spheres++;
-                        const float t = sphere_t(sp, load_geo_uniform(sc.geo, nd.sphere));
-                        if (t > 0.0f && t <= best_t) {
+                        const float t = sphere_t<FAST>(sp, nd.g, best_t);
+                        if (t > 0.0f) {
                             best_t = t;
                             best_s = nd.sphere;
                         }
                     }
                 }
             }
-            cur = __builtin_amdgcn_readfirstlane(__ballot(descend) ? cur + 1 : skip);
+            if (__builtin_amdgcn_readfirstlane(__ballot(descend) != 0)) {  // wave-uniform branch
+                cur = cur + 1;
+                nd = na;
+            } else {
+                cur = skip;
+                nd = nb;
+            }
         }
     } else {
+      if constexpr (!LPF) {
+        // no prefetch: 32 B of box/links per step, the leaf sphere only when
+        // the leaf's box passes
         while (__ballot(next < end)) {
+            if (COUNT) cnt.steps++;
             if (next < end) {
-                const mirt_node nd = load_node_lane(sc.nodes, next);
-                const bool pass = (nd.skip & MIRT_NODE_EMPTY) ||
-                                  slab_test(sr, nd.bmin[0], nd.bmin[1], nd.bmin[2], nd.bmax[0], nd.bmax[1], nd.bmax[2]);
+                const float4* p = (const float4*)(sc.nodes + next);
+                const float4 a = p[0], b = p[1];
+                NodeV nd;
+                nd.b0 = a.x; nd.b1 = a.y; nd.b2 = a.z; nd.b3 = a.w; nd.b4 = b.x; nd.b5 = b.y;
+                nd.sphere = __float_as_int(b.z);
+                nd.skip = __float_as_uint(b.w);
+                const bool inner = nd.sphere < 0;
+                const bool pass = (nd.skip & MIRT_NODE_EMPTY) || slab<FAST>(sr, nd);
                 if (COUNT) cnt.nodes++;
-                if (pass && nd.sphere < 0) {
+                if (pass && inner) {
                     next = next + 1;
                 } else {
-                    next = nd.skip & MIRT_SKIP_MASK;
                     if (pass) {
                         if (COUNT) cnt.spheres++;
-                        const float t = sphere_t(sp, sc.geo[nd.sphere]);
-                        if (t > 0.0f && t <= best_t) {
+                        const float t = sphere_t<FAST>(sp, p[2], best_t);
+                        if (t > 0.0f) {
                             best_t = t;
                             best_s = nd.sphere;
                         }
                     }
+                    next = nd.skip & MIRT_SKIP_MASK;
+                }
+            }
+        }
+        return;
+      }
+        NodeV nd;
+        if (next < end) nd = load_node_lane(sc.nodes, next);
+        while (__ballot(next < end)) {
+            if (COUNT) cnt.steps++;
+            if (next < end) {
+                const uint32_t skip = nd.skip & MIRT_SKIP_MASK;
+                const bool inner = nd.sphere < 0;
+                const NodeV na = load_node_lane(sc.nodes, min(next + 1, last));
+                NodeV nb = na;
+                if (inner) nb = load_node_lane(sc.nodes, min(skip, last));
+                const bool pass = (nd.skip & MIRT_NODE_EMPTY) || slab<FAST>(sr, nd);
+                if (COUNT) cnt.nodes++;
+                if (pass && inner) {
+                    next = next + 1;
+                    nd = na;
+                } else {
+                    if (pass) {
+                        if (COUNT) cnt.spheres++;
+                        const float t = sphere_t<FAST>(sp, nd.g, best_t);
+                        if (t > 0.0f) {
+                            best_t = t;
+                            best_s = nd.sphere;
+                        }
+                    }
+                    next = skip;
+                    nd = nb;
                 }
             }
         }
     }
 }
 
-// renderer.c:36-43: every sphere in array order, the first wins a tie.
-template <bool COUNT>
+__device__ __forceinline__ float wave_min(float v)
+{
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = fminf(v, __shfl_xor(v, off));
+    return v;
+}
+
+// Node-parallel walk of ONE (wave-uniform) ray by the whole wave. Rays with
+// an exactly zero direction component (the image's centre row and column
+// under an axis-aligned camera) ignore that slab entirely (hit.c:54-57), so
+// they pass most boxes and walk a large part of the tree -- the centre
+// pixel of the default camera visits all 29,399 nodes at 10k spheres. Walked
+// one node per step they set the frame time; here every step tests the 64
+// consecutive pre-order nodes [cur, cur + 64) in parallel (coalesced loads,
+// sphere tests for every passing leaf), then replays the DFS over the
+// chunk's pass/leaf masks on the scalar unit: a run of passed inner nodes
+// advances one by one, any other node jumps to its skip. Hit candidates are
+// the visited passing leaves; the chunk's winner (min t, later DFS index on
+// a tie) replaces the running best when t <= best -- the sequential rule of
+// hit.c:105-108 applied chunk by chunk.
+template <bool FAST, bool COUNT>
+__device__ __forceinline__ void closest_bvh_chunked(const DevScene& sc, const Ray& ray, float& best_t, int& best_s,
+                                                    Counters& cnt)
+{
+    const SlabRay sr = slab_ray(ray);
+    const SphRay sp = sph_ray(ray);
+    const uint32_t end = sc.num_nodes;
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t cur = 0;
+    float bt = INFINITY;
+    int bs = -1;
+    while (cur < end) {
+        if (COUNT) cnt.steps++;
+        const uint32_t base = cur;
+        const uint32_t i = base + lane;
+        bool pass = false, leaf = false;
+        uint32_t skip = end;
+        int sph = -1;
+        float t = -1.0f;
+        if (i < end) {
+            const NodeV nd = load_node_lane(sc.nodes, i);
+            skip = nd.skip & MIRT_SKIP_MASK;
+            leaf = nd.sphere >= 0;
+            sph = nd.sphere;
+            pass = (nd.skip & MIRT_NODE_EMPTY) || slab<FAST>(sr, nd);
+            if (pass && leaf) t = sphere_t<FAST>(sp, nd.g, bt);
+        }
+        const uint64_t descend = __ballot(pass && !leaf);
+        uint64_t visited = 0;
+        uint32_t c = cur;
+        const uint32_t lim = min(base + 64, end);
+        while (c < lim) {
+            uint32_t k = c - base;
+            // consume the run of passed inner nodes starting at k
+            const uint64_t run = ~(descend >> k);
+            const uint32_t n = run ? (uint32_t)__builtin_ctzll(run) : 64u - k;
+            const uint32_t stop = min(k + n, lim - base);
+            if (stop > k) visited |= (stop - k >= 64 ? ~0ull : ((1ull << (stop - k)) - 1)) << k;
+            c = base + stop;
+            if (c >= lim) break;
+            k = stop;
+            visited |= 1ull << k;  // a leaf or a failed node: jump past its subtree
+            c = __builtin_amdgcn_readlane(skip, k);
+        }
+        cur = c;
+        const bool cand = ((visited >> lane) & 1) && t > 0.0f;
+        const float tmin = wave_min(cand ? t : INFINITY);
+        if (tmin <= bt && tmin < INFINITY) {
+            const uint64_t eq = __ballot(cand && t == tmin);
+            const int last = 63 - __builtin_clzll(eq);
+            bt = tmin;
+            bs = __builtin_amdgcn_readlane(sph, last);
+        }
+        const uint64_t passed_leaves = __ballot(pass && leaf);
+        if (COUNT) {  // uniform values: every lane holds the ray's totals
+            cnt.nodes += __popcll(visited);
+            cnt.spheres += __popcll(visited & passed_leaves);
+        }
+    }
+    best_t = bt;
+    best_s = bs;
+}
+
+__device__ __forceinline__ float readlane_f(float v, int l)
+{
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// Closest hit for every active lane: degenerate rays (a zero or tiny
+// direction component, `SlabRay::generic`) one at a time with the whole
+// wave (closest_bvh_chunked), the rest with the lane-parallel walk.
+template <bool UNIFORM, bool FAST, bool COUNT, bool LPF = true>
+__device__ __forceinline__ void closest_hit(const DevScene& sc, const Ray& ray, bool active, float& best_t,
+                                            int& best_s, Counters& cnt)
+{
+    const bool gen = active && slab_ray(ray).generic;
+    closest_bvh<UNIFORM, FAST, COUNT, LPF>(sc, ray, active && !gen, best_t, best_s, cnt);
+    uint64_t gm = __ballot(gen);
+    const int lane = threadIdx.x & 63;
+    while (gm) {
+        const int l = __builtin_ctzll(gm);
+        gm &= gm - 1;
+        const Ray rr{readlane_f(ray.ox, l), readlane_f(ray.oy, l), readlane_f(ray.oz, l),
+                     readlane_f(ray.dx, l), readlane_f(ray.dy, l), readlane_f(ray.dz, l)};
+        float t;
+        int s;
+        Counters c2{0, 0, 0, 0, 0};
+        closest_bvh_chunked<FAST, COUNT>(sc, rr, t, s, c2);
+        if (COUNT) cnt.steps += c2.steps;
+        if (lane == l) {
+            best_t = t;
+            best_s = s;
+            if (COUNT) {
+                cnt.nodes += c2.nodes;
+                cnt.spheres += c2.spheres;
+            }
+        }
+    }
+}
+
+// renderer.c:36-43: every sphere in array order, the first wins a tie (so
+// the estimate may discard t >= best, not just t > best).
+template <bool FAST, bool COUNT>
 __device__ __forceinline__ void closest_brute(const DevScene& sc, const Ray& ray, bool active, float& best_t,
                                               int& best_s, Counters& cnt)
 {
     const SphRay sp = sph_ray(ray);
     best_t = INFINITY;
     best_s = -1;
-    if (!__ballot(active)) return;
+    if (!__ballot(active) || sc.num_spheres == 0) return;
+    float4 g = load_geo_uniform(sc.geo, 0);
     for (int i = 0; i < sc.num_spheres; i++) {
-        const float4 g = load_geo_uniform(sc.geo, i);
+        const float4 gn = load_geo_uniform(sc.geo, i + 1);  // [num_spheres] is the sentinel: in bounds
         if (active) {
             if (COUNT) cnt.spheres++;
-            const float t = sphere_t(sp, g);
+            const float t = sphere_t<FAST>(sp, g, best_t);
             if (t > 0.0f && t < best_t) {
                 best_t = t;
                 best_s = i;
             }
         }
+        g = gn;
     }
 }
 
@@ -323,10 +599,14 @@ __device__ __forceinline__ uint32_t blend_rgba(uint32_t base, uint32_t refl)
     return out;
 }
 
+// Traversal schedules (mirt_set_option MIRT_OPT_TRAVERSAL).
+// LANE / HYBRID prefetch both successors; the *_NP forms load on demand.
+enum Trav { kTravUniform = 0, kTravLane = 1, kTravHybrid = 2, kTravLaneNP = 3, kTravHybridNP = 4 };
+
 // trace_ray (renderer.c:21-77) with the recursion turned into a loop over
 // bounce levels that the whole wave executes together (the traversal needs
 // convergent lanes). Returns packed RGBA8. `key` is the pixel's RNG stream.
-template <bool UNIFORM, bool COUNT>
+template <int TRAV, bool FAST, bool COUNT>
 __device__ __forceinline__ uint32_t trace_path(const DevScene& sc, Ray ray, bool alive, int depth, bool use_bvh,
                                                uint64_t key, Counters& cnt)
 {
@@ -338,10 +618,17 @@ __device__ __forceinline__ uint32_t trace_path(const DevScene& sc, Ray ray, bool
         if (!__ballot(alive)) break;
         float t;
         int s;
-        if (use_bvh)
-            closest_bvh<UNIFORM, COUNT>(sc, ray, alive, t, s, cnt);
-        else
-            closest_brute<COUNT>(sc, ray, alive, t, s, cnt);
+        if (use_bvh) {
+            // primary rays of an 8x8 tile are coherent: walk them as one
+            // packet; bounce rays scatter: each lane walks alone (hybrid)
+            constexpr bool lpf = TRAV == kTravLane || TRAV == kTravHybrid;
+            if (TRAV == kTravUniform || ((TRAV == kTravHybrid || TRAV == kTravHybridNP) && level == 0))
+                closest_hit<true, FAST, COUNT>(sc, ray, alive, t, s, cnt);
+            else
+                closest_hit<false, FAST, COUNT, lpf>(sc, ray, alive, t, s, cnt);
+        } else {
+            closest_brute<FAST, COUNT>(sc, ray, alive, t, s, cnt);
+        }
         if (alive) {
             if (COUNT) cnt.rays++;
             if (s < 0) {

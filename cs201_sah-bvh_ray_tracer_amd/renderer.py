@@ -193,7 +193,7 @@ class Renderer:
         """Enqueue a frame into device memory (integer device pointers)."""
         check(self.L.mirt_render_frame_device(self.h, C.byref(cam), C.byref(fd), C.c_void_p(d_out),
                                               C.c_void_p(d_acc) if d_acc else None,
-                                              C.c_void_p(stream) if stream else None), "mirt_render_frame_device")
+                                              C.c_void_p(stream or 0)), "mirt_render_frame_device")
 
     def accum(self, count):
         out = np.zeros(count, np.float32)
@@ -206,7 +206,24 @@ class Renderer:
         fd = frame_desc(width, height, depth, use_bvh, seed, sample, False, 1, row_block, shard, num_shards)
         c = abi.Counts()
         check(self.L.mirt_count_frame(self.h, C.byref(cam), C.byref(fd), C.byref(c)), "mirt_count_frame")
-        return {"rays": c.rays, "nodes": c.nodes, "spheres": c.spheres, "hits": c.hits}
+        return {"rays": c.rays, "nodes": c.nodes, "spheres": c.spheres, "hits": c.hits, "lane_steps": c.lane_steps}
+
+    def set_option(self, option, value):
+        """abi.OPT_TRAVERSAL (abi.TRAV_*) / abi.OPT_FAST_SLAB (0/1): speed only."""
+        check(self.L.mirt_set_option(self.h, option, value), "mirt_set_option")
+
+    def get_option(self, option):
+        return check(self.L.mirt_get_option(self.h, option), "mirt_get_option")
+
+    def wave_stats(self, cam, width, height, depth=5, use_bvh=True, seed=1, sample=0, row_block=8, shard=0,
+                   num_shards=1):
+        """Per-wave (8x8 tile) diagnostic: array of (tile, steps, start, end),
+        start/end in 10 ns ticks of the device's constant clock."""
+        fd = frame_desc(width, height, depth, use_bvh, seed, sample, False, 1, row_block, shard, num_shards)
+        n = -self.L.mirt_wave_stats(self.h, C.byref(cam), C.byref(fd), None, 0)
+        out = np.zeros((n, 4), np.uint32)
+        check(self.L.mirt_wave_stats(self.h, C.byref(cam), C.byref(fd), ptr(out), n), "mirt_wave_stats")
+        return out
 
     @property
     def last_kernel_ms(self):

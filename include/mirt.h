@@ -109,6 +109,8 @@ typedef struct mirt_counts {
     uint64_t nodes;      /* ray_aabb_intersect calls */
     uint64_t spheres;    /* ray_sphere_intersect calls from leaves (or brute force) */
     uint64_t hits;       /* rays that found a closest hit */
+    uint64_t lane_steps; /* traversal loop iterations x 64 lanes executed by the
+                            default schedule; nodes / lane_steps = SIMD efficiency */
 } mirt_counts;
 
 enum {
@@ -183,7 +185,7 @@ int mirt_shard_rows(const mirt_frame_desc *fd, int32_t *rows);
    (num_rows * width). Accumulation state lives on the device (per ctx). */
 int mirt_render_frame(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_desc *fd, mirt_rgba8 *out);
 
-/* Same, asynchronously on `stream` (a hipStream_t, NULL = the ctx stream),
+/* Same, asynchronously on `stream` (a hipStream_t; NULL = the default stream),
    into device memory: d_out = num_rows * width packed RGBA8. d_accum is a
    device float buffer of num_rows * width * 3 (may be NULL when
    fd->accumulate == 0). Inputs are already resident in HBM. */
@@ -215,8 +217,30 @@ int mirt_camera_rays(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_des
    untimed): the algorithmic-bytes numerator of SURVEY §8(d). */
 int mirt_count_frame(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_desc *fd, mirt_counts *out);
 
+/* Diagnostic: renders the frame with the instrumented kernel and writes, per
+   8x8 tile (= wave), {tile, traversal loop steps, start, end} with start/end
+   read from the 100 MHz s_memrealtime clock. Returns the number of waves
+   (or -waves if cap is too small). */
+int mirt_wave_stats(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_desc *fd, uint32_t *out, int cap);
+
 /* Device time (ms) of the last render kernel launched by a blocking call. */
 float mirt_last_kernel_ms(mirt_ctx *ctx);
+
+/* Kernel schedule knobs (results are identical under every setting; only
+   speed changes). MIRT_OPT_TRAVERSAL: how a wave walks the tree --
+   MIRT_TRAV_UNIFORM (the wave walks the union of its lanes' walks with one
+   cursor, scalar node loads), MIRT_TRAV_LANE (each lane walks alone, vector
+   node loads), MIRT_TRAV_HYBRID (uniform for camera rays, per-lane for
+   bounces), MIRT_TRAV_HYBRID_NP (the same without successor prefetch in the
+   per-lane walk; default). MIRT_OPT_FAST_SLAB: 1 (default) = reciprocal-multiply
+   slab test with an exact-division fallback for undecidable boxes; 0 = the
+   division-only slab test of hit.c:49-82. MIRT_OPT_BLOCK_WAVES: 8x8 pixel
+   tiles (waves) per workgroup of the frame kernel: 1, 2, 4 (default) or 8. */
+enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3 };
+enum { MIRT_TRAV_UNIFORM = 0, MIRT_TRAV_LANE = 1, MIRT_TRAV_HYBRID = 2, MIRT_TRAV_LANE_NP = 3,
+       MIRT_TRAV_HYBRID_NP = 4 };  /* *_NP: per-lane walk without successor prefetch */
+int mirt_set_option(mirt_ctx *ctx, int option, int value);
+int mirt_get_option(mirt_ctx *ctx, int option);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,67 @@
+"""Copy the rocprofv3 summaries of a GPU session (gpurun_out/<tag>/) into the
+tracked profiles/ directory and derive the per-launch HBM traffic of the
+render kernel that bench.py reports as roofline.traffic.
+
+    python scripts/collect_profiles.py r01g
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE come
+from separate --pmc passes (they do not fit one pass), both in KiB; on
+gfx950 FETCH_SIZE counts half of the bytes of a wide read, so it is doubled
+(an upper bound for this kernel's narrower reads); WRITE_SIZE is taken as is.
+"""
+import csv
+import json
+import os
+import shutil
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+KERNEL = "render_kernel<4, true, false>"
+WORKLOAD = [1920, 1080, 10000, 5]
+
+
+def per_launch(path, counter):
+    vals = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                vals.append(float(r["Counter_Value"]))
+    return vals
+
+
+def main():
+    tag = sys.argv[1]
+    src = os.path.join(ROOT, "gpurun_out", tag)
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    stats = os.path.join(src, "prof", "run_kernel_stats.csv")
+    if os.path.exists(stats):
+        shutil.copy(stats, os.path.join(dst, f"{tag}_kernel_stats.csv"))
+        with open(stats) as f:
+            rows = list(csv.DictReader(f))
+        for r in rows:
+            if KERNEL in r["Name"]:
+                print("kernel stats:", r["Name"][:60], "calls", r["Calls"], "avg ms", float(r["AverageNs"]) / 1e6)
+    fetch = per_launch(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = per_launch(os.path.join(src, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
+    # the first launch is the warm-up (cold caches); the rest are the timed frames
+    f_kb = statistics.median(fetch[1:] or fetch)
+    w_kb = statistics.median(write[1:] or write)
+    out = {"workload": WORKLOAD, "kernel": KERNEL, "source": f"gpurun_out/{tag} (bench.py --no-cpu --no-host)",
+           "launches": {"fetch": len(fetch), "write": len(write)},
+           "fetch_size_kib_per_launch": f_kb, "write_size_kib_per_launch": w_kb,
+           "correction": "FETCH_SIZE x2 (gfx950 counts half of a wide read), WRITE_SIZE x1; KiB -> bytes",
+           "hbm_bytes_per_launch": int((2 * f_kb + w_kb) * 1024)}
+    with open(os.path.join(dst, "pmc_render.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    for name in ("pmc_fetch", "pmc_write"):
+        p = os.path.join(src, name, "run_counter_collection.csv")
+        if os.path.exists(p):
+            shutil.copy(p, os.path.join(dst, f"{tag}_{name}.csv"))
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,31 @@
+#!/bin/bash
+# One GPU-box session: smoke, GPU parity tests, bench, rocprofv3 kernel stats
+# and (separate passes) HBM counters. Every GPU step has its own time limit;
+# a fault / abort / timeout (rc not in {0,1}) ends the script.
+# usage: scripts/gpu_round.sh [tag] [steps...]   steps default: smoke tests bench prof pmc
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${1:-r01}; shift || true
+STEPS=${*:-smoke tests bench prof pmc}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+step() {
+    local name=$1 lim=$2; shift 2
+    echo "== $name ($(date +%T))"
+    timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "$name rc=$rc"; tail -n 4 "$OUT/$name.log"
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+}
+for s in $STEPS; do
+  case $s in
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()";;
+    tests) step pytest_gpu 1200 python -m pytest tests -m gpu -x -q;;
+    bench) step bench 600 python bench.py;;
+    prof)  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu;;
+    pmc)   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --no-cpu --no-host --steps 5 --warmup 1
+           step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --no-cpu --no-host --steps 5 --warmup 1;;
+  esac
+done
+echo "done"
