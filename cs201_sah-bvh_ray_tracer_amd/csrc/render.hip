@@ -9,6 +9,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -85,16 +86,6 @@ __device__ __forceinline__ Ray camera_ray(const FrameConst& f, int x, int y)
     return {f.px, f.py, f.pz, dx, dy, dz};
 }
 
-// Wave w of a block covers an 8x8 tile; tiles run along x, then shard rows.
-__device__ __forceinline__ void tile_pixel(const FrameConst& f, int& x, int& r)
-{
-    const int lane = threadIdx.x & 63;
-    const int tile = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const int tiles_x = (f.width + 7) >> 3;
-    x = (tile % tiles_x) * 8 + (lane & 7);
-    r = (tile / tiles_x) * 8 + (lane >> 3);
-}
-
 __device__ __forceinline__ void add_counts(mirt_counts* out, const Counters& c)
 {
     atomicAdd((unsigned long long*)&out->rays, (unsigned long long)c.rays);
@@ -104,35 +95,32 @@ __device__ __forceinline__ void add_counts(mirt_counts* out, const Counters& c)
     atomicAdd((unsigned long long*)&out->lane_steps, (unsigned long long)c.steps);
 }
 
-// The pixel loop of main.c:358-374 (fresh) / main.c:382-407 (accumulate).
+// Pixels whose camera ray has a zero or tiny direction component (the image
+// centre row / column under an axis-aligned camera) ignore a slab
+// (hit.c:54-57) and walk a large part of the tree. A pre-pass lists them
+// (mark_deferred_kernel); the first `blocks` workgroups of the frame kernel
+// trace them one pixel per wave (the node-parallel walk of trace.h) while
+// the other workgroups trace the 8x8 tiles and skip them, so the long walks
+// start first and overlap the bulk instead of trailing it.
+struct Deferred {
+    const uint32_t* list;   // r * width + x
+    const uint32_t* count;
+    int blocks;
+};
+
+// One pixel of the pixel loop: main.c:362-366 ray, trace_ray, then the
+// display/accumulation of main.c:368-372 (fresh) or main.c:394-405.
 template <int TRAV, bool FAST, bool COUNT>
-__global__ __launch_bounds__(512) void render_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
-                                                      float* __restrict__ acc, mirt_counts* counts,
-                                                      uint32_t* wave_stats)
+__device__ __forceinline__ void render_pixel(const DevScene& sc, const FrameConst& f, int x, int r, bool alive,
+                                             bool skip_generic, uint32_t* __restrict__ out, float* __restrict__ acc,
+                                             Counters& cnt, uint32_t* cstack, int cstride)
 {
-    uint64_t t0 = 0;
-    if (COUNT) t0 = __builtin_amdgcn_s_memrealtime();
-    int x, r;
-    tile_pixel(f, x, r);
-    const bool alive = x < f.width && r < f.num_rows;
     const int y = alive ? shard_row_to_y(f, r) : 0;
     const Ray ray = camera_ray(f, alive ? x : 0, y);
+    if (skip_generic && alive && slab_ray(ray).generic) alive = false;  // a deferred wave traces it
     const uint64_t key = pixel_key(f.seed, (uint32_t)(y * f.width + x), f.sample);
-    Counters cnt{0, 0, 0, 0, 0};
-    const uint32_t c = trace_path<TRAV, FAST, COUNT>(sc, ray, alive, f.depth, f.use_bvh != 0, key, cnt);
-    if (COUNT) {
-        add_counts(counts, cnt);
-        if (wave_stats && (threadIdx.x & 63) == 0) {
-            // diagnostic: {tile, traversal steps of this wave, start, end} (100 MHz clock)
-            const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
-            const uint32_t tile = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-            uint32_t* w = wave_stats + 4 * (size_t)tile;
-            w[0] = tile;
-            w[1] = cnt.steps;
-            w[2] = (uint32_t)t0;
-            w[3] = (uint32_t)t1;
-        }
-    }
+    const uint32_t c = trace_path<TRAV, FAST, COUNT>(sc, ray, alive, f.depth, f.use_bvh != 0, key, cnt, cstack,
+                                                     cstride);
     if (!alive) return;
     const size_t i = (size_t)r * f.width + x;
     uint32_t shown = c;
@@ -153,6 +141,59 @@ __global__ __launch_bounds__(512) void render_kernel(DevScene sc, FrameConst f, 
     out[i] = shown;
 }
 
+// The pixel loop of main.c:358-374 (fresh) / main.c:382-407 (accumulate).
+template <int TRAV, bool FAST, bool COUNT>
+__global__ __launch_bounds__(512) void render_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
+                                                      float* __restrict__ acc, mirt_counts* counts,
+                                                      uint32_t* wave_stats, Deferred dfr)
+{
+    uint64_t t0 = 0;
+    if (COUNT) t0 = __builtin_amdgcn_s_memrealtime();
+    __shared__ uint32_t cstack[kMaxDepth * 512];
+    Counters cnt{0, 0, 0, 0, 0};
+    const int bw = blockDim.x >> 6;
+    const int wave = threadIdx.x >> 6;
+    if ((int)blockIdx.x < dfr.blocks) {
+        const uint32_t n = __builtin_amdgcn_readfirstlane(*dfr.count);
+        const uint32_t stride = (uint32_t)(dfr.blocks * bw);
+        for (uint32_t j = blockIdx.x * bw + wave; j < n; j += stride) {
+            const uint32_t p = __builtin_amdgcn_readfirstlane(dfr.list[j]);
+            render_pixel<TRAV, FAST, COUNT>(sc, f, (int)(p % f.width), (int)(p / f.width), (threadIdx.x & 63) == 0,
+                                            false, out, acc, cnt, cstack + threadIdx.x, blockDim.x);
+        }
+        if (COUNT) add_counts(counts, cnt);
+        return;
+    }
+    const int tile = (blockIdx.x - dfr.blocks) * bw + wave;
+    const int lane = threadIdx.x & 63;
+    const int tiles_x = (f.width + 7) >> 3;
+    const int x = (tile % tiles_x) * 8 + (lane & 7);
+    const int r = (tile / tiles_x) * 8 + (lane >> 3);
+    render_pixel<TRAV, FAST, COUNT>(sc, f, x, r, x < f.width && r < f.num_rows, dfr.blocks > 0, out, acc, cnt,
+                                    cstack + threadIdx.x, blockDim.x);
+    if (COUNT) {
+        add_counts(counts, cnt);
+        if (wave_stats && lane == 0) {
+            // diagnostic: {tile, traversal steps of this wave, start, end} (100 MHz clock)
+            const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+            uint32_t* w = wave_stats + 4 * (size_t)tile;
+            w[0] = tile;
+            w[1] = cnt.steps;
+            w[2] = (uint32_t)t0;
+            w[3] = (uint32_t)t1;
+        }
+    }
+}
+
+__global__ void mark_deferred_kernel(FrameConst f, uint32_t* __restrict__ list, uint32_t* __restrict__ count)
+{
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int r = blockIdx.y;
+    if (x >= f.width || r >= f.num_rows) return;
+    const Ray ray = camera_ray(f, x, shard_row_to_y(f, r));
+    if (slab_ray(ray).generic) list[atomicAdd(count, 1u)] = (uint32_t)(r * f.width + x);
+}
+
 // trace_ray on explicit rays (renderer.c:21); ray i uses contract pixel i.
 template <int TRAV, bool FAST>
 __global__ __launch_bounds__(256) void trace_rays_kernel(DevScene sc, const mirt_ray* __restrict__ rays, int n,
@@ -164,8 +205,9 @@ __global__ __launch_bounds__(256) void trace_rays_kernel(DevScene sc, const mirt
     const mirt_ray& rr = rays[alive ? i : 0];
     const Ray ray{rr.origin.x, rr.origin.y, rr.origin.z, rr.direction.x, rr.direction.y, rr.direction.z};
     Counters cnt{0, 0, 0, 0, 0};
+    __shared__ uint32_t cstack[kMaxDepth * 256];
     const uint32_t c = trace_path<TRAV, FAST, false>(sc, ray, alive, depth, use_bvh != 0,
-                                                  pixel_key(seed, (uint32_t)i, sample), cnt);
+                                                  pixel_key(seed, (uint32_t)i, sample), cnt, cstack + threadIdx.x, 256);
     if (alive) out[i] = c;
 }
 
@@ -262,6 +304,7 @@ struct mirt_ctx {
     float last_ms = 0.0f;
     // scene (replicated per device, uploaded once)
     DNode* d_nodes = nullptr;
+    mirt_node* d_nodes32 = nullptr;
     float4* d_geo = nullptr;
     uint32_t* d_color = nullptr;
     int num_nodes = 0, num_spheres = -1;
@@ -278,6 +321,9 @@ struct mirt_ctx {
     int trav = kTravHybridNP;
     int fast_slab = 1;
     int block_waves = 4;  // waves (8x8 tiles) per workgroup
+    int defer = 1;        // trace zero-component camera rays in leading waves
+    uint32_t* d_defer = nullptr;  // [count, list...]
+    size_t defer_cap = 0;
 };
 
 namespace {
@@ -307,7 +353,7 @@ int ensure(void** p, size_t* cap, size_t bytes)
 
 DevScene dev_scene(const mirt_ctx* c)
 {
-    return DevScene{c->d_nodes, c->d_geo, c->d_color, (uint32_t)c->num_nodes, c->num_spheres};
+    return DevScene{c->d_nodes, c->d_nodes32, c->d_geo, c->d_color, (uint32_t)c->num_nodes, c->num_spheres};
 }
 
 bool ctx_ok(mirt_ctx* c, bool need_scene, const char* fn)
@@ -323,11 +369,31 @@ bool ctx_ok(mirt_ctx* c, bool need_scene, const char* fn)
     return hipSetDevice(c->device) == hipSuccess;
 }
 
-template <int TRAV, bool FAST>
+template <int TRAV, bool FAST, bool COUNT>
 void launch_render_t(const DevScene& sc, const FrameConst& f, uint32_t* d_out, float* d_acc, hipStream_t s,
-                     int blocks, int bw)
+                     int blocks, int bw, mirt_counts* d_counts, uint32_t* d_ws, Deferred dfr)
 {
-    render_kernel<TRAV, FAST, false><<<blocks, 64 * bw, 0, s>>>(sc, f, d_out, d_acc, nullptr, nullptr);
+    render_kernel<TRAV, FAST, COUNT><<<blocks + dfr.blocks, 64 * bw, 0, s>>>(sc, f, d_out, d_acc, d_counts, d_ws, dfr);
+}
+
+template <bool COUNT>
+void dispatch_render(int trav, bool fast, const DevScene& sc, const FrameConst& f, uint32_t* d_out, float* d_acc,
+                     hipStream_t s, int blocks, int bw, mirt_counts* d_counts, uint32_t* d_ws, Deferred dfr)
+{
+#define MIRT_LAUNCH_TRAV(T)                                                                              \
+    case T:                                                                                            \
+        fast ? launch_render_t<T, true, COUNT>(sc, f, d_out, d_acc, s, blocks, bw, d_counts, d_ws, dfr)   \
+             : launch_render_t<T, false, COUNT>(sc, f, d_out, d_acc, s, blocks, bw, d_counts, d_ws, dfr); \
+        break;
+    switch (trav) {
+        MIRT_LAUNCH_TRAV(kTravUniform)
+        MIRT_LAUNCH_TRAV(kTravLane)
+        MIRT_LAUNCH_TRAV(kTravHybrid)
+        MIRT_LAUNCH_TRAV(kTravLaneNP)
+    default:
+        MIRT_LAUNCH_TRAV(kTravHybridNP)
+    }
+#undef MIRT_LAUNCH_TRAV
 }
 
 int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_acc, hipStream_t s, bool timed,
@@ -338,34 +404,24 @@ int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_ac
     const int blocks = (tiles + bw - 1) / bw;
     if (blocks == 0) return MIRT_OK;
     if (timed) HIP_TRY(hipEventRecord(c->ev0, s));
-    const DevScene sc = dev_scene(c);
-    if (d_counts) {
-        // the work counters are schedule independent except lane_steps
-        if (c->trav == kTravUniform)
-            render_kernel<kTravUniform, true, true><<<blocks, 64 * bw, 0, s>>>(sc, f, d_out, d_acc, d_counts, d_wave_stats);
-        else if (c->trav == kTravLane)
-            render_kernel<kTravLane, true, true><<<blocks, 64 * bw, 0, s>>>(sc, f, d_out, d_acc, d_counts, d_wave_stats);
-        else
-            render_kernel<kTravHybrid, true, true><<<blocks, 64 * bw, 0, s>>>(sc, f, d_out, d_acc, d_counts, d_wave_stats);
-    } else {
-        const bool fast = c->fast_slab != 0;
-#define MIRT_LAUNCH_TRAV(T)                                                          \
-    case T:                                                                        \
-        fast ? launch_render_t<T, true>(sc, f, d_out, d_acc, s, blocks, bw)         \
-             : launch_render_t<T, false>(sc, f, d_out, d_acc, s, blocks, bw);       \
-        break;
-        switch (c->trav) {
-            MIRT_LAUNCH_TRAV(kTravUniform)
-            MIRT_LAUNCH_TRAV(kTravLane)
-            MIRT_LAUNCH_TRAV(kTravLaneNP)
-            MIRT_LAUNCH_TRAV(kTravHybridNP)
-        default:
-            fast ? launch_render_t<kTravHybrid, true>(sc, f, d_out, d_acc, s, blocks, bw)
-                 : launch_render_t<kTravHybrid, false>(sc, f, d_out, d_acc, s, blocks, bw);
-            break;
-        }
-#undef MIRT_LAUNCH_TRAV
+    Deferred dfr{nullptr, nullptr, 0};
+    if (f.use_bvh && c->defer) {
+        const size_t pixels = (size_t)f.num_rows * f.width;
+        int rc = ensure((void**)&c->d_defer, &c->defer_cap, 4 * (pixels + 1));
+        if (rc) return rc;
+        HIP_TRY(hipMemsetAsync(c->d_defer, 0, 4, s));
+        mark_deferred_kernel<<<dim3((f.width + 255) / 256, f.num_rows), 256, 0, s>>>(f, c->d_defer + 1, c->d_defer);
+        HIP_TRY(hipGetLastError());
+        // enough waves for the centre row and column of an axis-aligned
+        // camera; a longer list is strided over the same waves
+        const size_t want = std::min(pixels, (size_t)(f.width + f.num_rows + 64));
+        dfr = Deferred{c->d_defer + 1, c->d_defer, (int)((want + bw - 1) / bw)};
     }
+    const DevScene sc = dev_scene(c);
+    if (d_counts)
+        dispatch_render<true>(c->trav, true, sc, f, d_out, d_acc, s, blocks, bw, d_counts, d_wave_stats, dfr);
+    else
+        dispatch_render<false>(c->trav, c->fast_slab != 0, sc, f, d_out, d_acc, s, blocks, bw, nullptr, nullptr, dfr);
     HIP_TRY(hipGetLastError());
     if (timed) HIP_TRY(hipEventRecord(c->ev1, s));
     return MIRT_OK;
@@ -405,8 +461,8 @@ void mirt_destroy(mirt_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (void* p : {(void*)c->d_nodes, (void*)c->d_geo, (void*)c->d_color, (void*)c->d_out, (void*)c->d_acc,
-                    c->d_in, c->d_res, (void*)c->d_counts})
+    for (void* p : {(void*)c->d_nodes, (void*)c->d_nodes32, (void*)c->d_geo, (void*)c->d_color, (void*)c->d_out, (void*)c->d_acc,
+                    c->d_in, c->d_res, (void*)c->d_counts, (void*)c->d_defer})
         if (p) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -443,9 +499,10 @@ int mirt_scene_upload_flat(mirt_ctx* c, const mirt_sphere* spheres, int ns, cons
     }
     geo[ns] = make_float4(NAN, NAN, NAN, NAN);  // &spheres[N] sentinel: never hits
     col[ns] = 0xff000000u;
-    for (void* p : {(void*)c->d_nodes, (void*)c->d_geo, (void*)c->d_color})
+    for (void* p : {(void*)c->d_nodes, (void*)c->d_nodes32, (void*)c->d_geo, (void*)c->d_color})
         if (p) (void)hipFree(p);
     c->d_nodes = nullptr;
+    c->d_nodes32 = nullptr;
     c->d_geo = nullptr;
     c->d_color = nullptr;
     c->num_spheres = -1;
@@ -463,7 +520,9 @@ int mirt_scene_upload_flat(mirt_ctx* c, const mirt_sphere* spheres, int ns, cons
     HIP_TRY(hipMalloc((void**)&c->d_nodes, sizeof(DNode) * (size_t)(nn > 0 ? nn : 1)));
     HIP_TRY(hipMalloc((void**)&c->d_geo, sizeof(float4) * geo.size()));
     HIP_TRY(hipMalloc((void**)&c->d_color, sizeof(uint32_t) * col.size()));
+    HIP_TRY(hipMalloc((void**)&c->d_nodes32, sizeof(mirt_node) * (size_t)(nn > 0 ? nn : 1)));
     if (nn > 0) HIP_TRY(hipMemcpy(c->d_nodes, dn.data(), sizeof(DNode) * (size_t)nn, hipMemcpyHostToDevice));
+    if (nn > 0) HIP_TRY(hipMemcpy(c->d_nodes32, nodes, sizeof(mirt_node) * (size_t)nn, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_geo, geo.data(), sizeof(float4) * geo.size(), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_color, col.data(), sizeof(uint32_t) * col.size(), hipMemcpyHostToDevice));
     c->num_nodes = nn;
@@ -735,6 +794,9 @@ int mirt_set_option(mirt_ctx* c, int option, int value)
     case MIRT_OPT_FAST_SLAB:
         c->fast_slab = value != 0;
         return MIRT_OK;
+    case MIRT_OPT_DEFER:
+        c->defer = value != 0;
+        return MIRT_OK;
     case MIRT_OPT_BLOCK_WAVES:
         if (value != 1 && value != 2 && value != 4 && value != 8) break;
         c->block_waves = value;
@@ -752,6 +814,7 @@ int mirt_get_option(mirt_ctx* c, int option)
     if (option == MIRT_OPT_TRAVERSAL) return c->trav;
     if (option == MIRT_OPT_FAST_SLAB) return c->fast_slab;
     if (option == MIRT_OPT_BLOCK_WAVES) return c->block_waves;
+    if (option == MIRT_OPT_DEFER) return c->defer;
     set_error("mirt_get_option: bad option %d", option);
     return MIRT_E_INVALID;
 }

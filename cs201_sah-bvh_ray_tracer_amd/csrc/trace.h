@@ -37,7 +37,8 @@ static_assert(sizeof(DNode) == 64, "device node is 64 B");
 
 // Read-only scene in HBM (L2 / Infinity-Cache resident at the BASELINE sizes).
 struct DevScene {
-    const DNode* nodes;
+    const DNode* nodes;     // 64 B, leaf sphere inline: scalar (wave-uniform) walks
+    const mirt_node* nodes32;  // the same tree in 32 B (mirt_node): per-lane walks (twice the nodes per L1 line)
     const float4* geo;      // centre.xyz, radius per sphere; [num_spheres] = NaN sentinel
     const uint32_t* color;  // packed RGBA8
     uint32_t num_nodes;
@@ -337,7 +338,7 @@ __device__ __forceinline__ void closest_bvh(const DevScene& sc, const Ray& ray, 
         while (__ballot(next < end)) {
             if (COUNT) cnt.steps++;
             if (next < end) {
-                const float4* p = (const float4*)(sc.nodes + next);
+                const float4* p = (const float4*)(sc.nodes32 + next);
                 const float4 a = p[0], b = p[1];
                 NodeV nd;
                 nd.b0 = a.x; nd.b1 = a.y; nd.b2 = a.z; nd.b3 = a.w; nd.b4 = b.x; nd.b5 = b.y;
@@ -351,7 +352,7 @@ __device__ __forceinline__ void closest_bvh(const DevScene& sc, const Ray& ray, 
                 } else {
                     if (pass) {
                         if (COUNT) cnt.spheres++;
-                        const float t = sphere_t<FAST>(sp, p[2], best_t);
+                        const float t = sphere_t<FAST>(sp, sc.geo[nd.sphere], best_t);
                         if (t > 0.0f) {
                             best_t = t;
                             best_s = nd.sphere;
@@ -606,11 +607,13 @@ enum Trav { kTravUniform = 0, kTravLane = 1, kTravHybrid = 2, kTravLaneNP = 3, k
 // trace_ray (renderer.c:21-77) with the recursion turned into a loop over
 // bounce levels that the whole wave executes together (the traversal needs
 // convergent lanes). Returns packed RGBA8. `key` is the pixel's RNG stream.
+// The base colours of the hit levels (folded innermost-first at the end,
+// renderer.c:55-58) live in LDS, `cstack[level * cstride]`, one column per
+// thread, to keep them out of the register budget.
 template <int TRAV, bool FAST, bool COUNT>
 __device__ __forceinline__ uint32_t trace_path(const DevScene& sc, Ray ray, bool alive, int depth, bool use_bvh,
-                                               uint64_t key, Counters& cnt)
+                                               uint64_t key, Counters& cnt, uint32_t* cstack, int cstride)
 {
-    uint32_t base[kMaxDepth];
     int levels = 0;
     uint32_t tail = 255u << 24;  // renderer.c:23-24 depth exhausted -> (0,0,0,255)
     uint32_t k = 0;
@@ -636,9 +639,7 @@ __device__ __forceinline__ uint32_t trace_path(const DevScene& sc, Ray ray, bool
                 alive = false;
             } else {
                 if (COUNT) cnt.hits++;
-#pragma unroll
-                for (int l = 0; l < kMaxDepth; l++)
-                    if (l == levels) base[l] = sc.color[s];
+                cstack[levels * cstride] = sc.color[s];
                 levels++;
                 if (level + 1 < depth) {
                     // the bounce of renderer.c:51-55; at the last level it would
@@ -655,9 +656,7 @@ __device__ __forceinline__ uint32_t trace_path(const DevScene& sc, Ray ray, bool
             }
         }
     }
-#pragma unroll
-    for (int l = kMaxDepth - 1; l >= 0; l--)
-        if (l < levels) tail = blend_rgba(base[l], tail);
+    for (int l = levels - 1; l >= 0; l--) tail = blend_rgba(cstack[l * cstride], tail);
     return tail;
 }
 

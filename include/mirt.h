@@ -235,8 +235,10 @@ float mirt_last_kernel_ms(mirt_ctx *ctx);
    per-lane walk; default). MIRT_OPT_FAST_SLAB: 1 (default) = reciprocal-multiply
    slab test with an exact-division fallback for undecidable boxes; 0 = the
    division-only slab test of hit.c:49-82. MIRT_OPT_BLOCK_WAVES: 8x8 pixel
-   tiles (waves) per workgroup of the frame kernel: 1, 2, 4 (default) or 8. */
-enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3 };
+   tiles (waves) per workgroup of the frame kernel: 1, 2, 4 (default) or 8.
+   MIRT_OPT_DEFER: 1 (default) = camera rays with a zero/tiny direction
+   component are traced first, one per wave (node-parallel walk). */
+enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3, MIRT_OPT_DEFER = 4 };
 enum { MIRT_TRAV_UNIFORM = 0, MIRT_TRAV_LANE = 1, MIRT_TRAV_HYBRID = 2, MIRT_TRAV_LANE_NP = 3,
        MIRT_TRAV_HYBRID_NP = 4 };  /* *_NP: per-lane walk without successor prefetch */
 int mirt_set_option(mirt_ctx *ctx, int option, int value);

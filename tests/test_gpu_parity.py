@@ -194,12 +194,14 @@ def test_sentinel_and_edge_scenes(gpu, mirt, oracle):
 
 @pytest.mark.parametrize("trav", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("fast", [0, 1])
-def test_all_schedules_bit_identical(gpu, mirt, golden, small, scene1000, trav, fast):
+@pytest.mark.parametrize("defer", [0, 1])
+def test_all_schedules_bit_identical(gpu, mirt, golden, small, scene1000, trav, fast, defer):
     """Every traversal schedule x slab-test form gives the reference's bytes:
     per-ray hits and traces, and the 1080p 10k depth-1/depth-5 frames."""
     abi = mirt.abi
     gpu.set_option(abi.OPT_TRAVERSAL, trav)
     gpu.set_option(abi.OPT_FAST_SLAB, fast)
+    gpu.set_option(abi.OPT_DEFER, defer)
     try:
         s, b = scene1000
         gpu.upload(s, b)
@@ -215,6 +217,7 @@ def test_all_schedules_bit_identical(gpu, mirt, golden, small, scene1000, trav, 
     finally:
         gpu.set_option(abi.OPT_TRAVERSAL, abi.TRAV_HYBRID_NP)
         gpu.set_option(abi.OPT_FAST_SLAB, 1)
+        gpu.set_option(abi.OPT_DEFER, 1)
 
 
 def test_errors_are_loud(gpu, mirt):
