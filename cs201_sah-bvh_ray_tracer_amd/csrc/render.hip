@@ -194,6 +194,199 @@ __global__ void mark_deferred_kernel(FrameConst f, uint32_t* __restrict__ list, 
     if (slab_ray(ray).generic) list[atomicAdd(count, 1u)] = (uint32_t)(r * f.width + x);
 }
 
+// main.c:368-372 / 394-405 for one finished pixel i of the shard.
+__device__ __forceinline__ void store_pixel(const FrameConst& f, uint32_t* __restrict__ out, float* __restrict__ acc,
+                                            size_t i, uint32_t c)
+{
+    uint32_t shown = c;
+    if (acc) {
+        float* a = acc + 3 * i;
+        for (int ch = 0; ch < 3; ch++) {
+            const float v = (float)((c >> (8 * ch)) & 0xff) / 255.0f;
+            if (f.accumulate) {
+                a[ch] = a[ch] + v;
+                const float avg = a[ch] / f.frames * 255.0f;
+                const uint32_t q = (uint32_t)(int)fminf(avg, 255.0f);
+                shown = (shown & ~(0xffu << (8 * ch))) | ((q & 0xffu) << (8 * ch));
+            } else {
+                a[ch] = v;
+            }
+        }
+    }
+    out[i] = shown;
+}
+
+__device__ __forceinline__ uint32_t lanes_below(uint64_t mask)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// ------------------------------------------------------------------------
+// Wavefront schedule (depth >= 2): the camera rays of 8x8 tiles are walked
+// as packets (wave-uniform cursor); the bounce chains that follow are
+// scattered, so they go through a queue to persistent waves in which every
+// lane owns one pixel's chain and refills from the queue when it ends.
+
+// First bounce of one pixel, produced by primary_kernel.
+struct BounceRec {
+    float ox, oy, oz, dx, dy, dz;
+    uint32_t pixel;  // r * width + x (shard-compacted row r)
+    uint32_t k;      // RNG contract draws consumed so far
+    uint32_t base0;  // colour of the camera ray's hit (renderer.c:49)
+    uint32_t pad;
+};
+
+template <bool FAST>
+__global__ __launch_bounds__(256) void primary_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
+                                                      float* __restrict__ acc, Deferred dfr,
+                                                      BounceRec* __restrict__ queue, uint32_t* __restrict__ qctl)
+{
+    __shared__ uint32_t cstack[kMaxDepth * 256];
+    Counters cnt{0, 0, 0, 0, 0};
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    if ((int)blockIdx.x < dfr.blocks) {  // zero-component camera rays: whole path in this wave
+        const uint32_t n = __builtin_amdgcn_readfirstlane(*dfr.count);
+        const uint32_t stride = (uint32_t)(dfr.blocks * 4);
+        for (uint32_t j = blockIdx.x * 4 + wave; j < n; j += stride) {
+            const uint32_t p = __builtin_amdgcn_readfirstlane(dfr.list[j]);
+            render_pixel<kTravHybridNP, FAST, false>(sc, f, (int)(p % f.width), (int)(p / f.width), lane == 0, false,
+                                                     out, acc, cnt, cstack + threadIdx.x, 256);
+        }
+        return;
+    }
+    const int tile = (blockIdx.x - dfr.blocks) * 4 + wave;
+    const int tiles_x = (f.width + 7) >> 3;
+    const int x = (tile % tiles_x) * 8 + (lane & 7);
+    const int r = (tile / tiles_x) * 8 + (lane >> 3);
+    bool alive = x < f.width && r < f.num_rows;
+    const int y = alive ? shard_row_to_y(f, r) : 0;
+    const Ray ray = camera_ray(f, alive ? x : 0, y);
+    if (dfr.blocks > 0 && alive && slab_ray(ray).generic) alive = false;  // traced by a deferred wave
+    float t;
+    int s;
+    closest_hit<true, FAST, false>(sc, ray, alive, t, s, cnt);
+    const size_t i = (size_t)r * f.width + x;
+    bool push = false;
+    BounceRec rec;
+    if (alive) {
+        if (s < 0) {
+            store_pixel(f, out, acc, i, sky_rgba(ray.dy));      // renderer.c:65-70
+        } else {
+            // renderer.c:49-55: base colour, then the bounce (depth >= 2 here)
+            const float4 g = sc.geo[s];
+            float p[3], n[3];
+            hit_point_normal(ray, t, g, p, n);
+            uint32_t k = 0;
+            float bx, by, bz;
+            hemisphere(pixel_key(f.seed, (uint32_t)(y * f.width + x), f.sample), k, n, bx, by, bz);
+            rec = BounceRec{p[0], p[1], p[2], bx, by, bz, (uint32_t)i, k, sc.color[s], 0u};
+            push = true;
+        }
+    }
+    const uint64_t pm = __ballot(push);
+    if (pm) {  // one atomic per wave; records stay in tile order
+        const int leader = __builtin_ctzll(pm);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&qctl[0], (uint32_t)__popcll(pm));
+        base = __builtin_amdgcn_readlane(base, leader);
+        if (push) queue[base + lanes_below(pm)] = rec;
+    }
+}
+
+template <bool FAST>
+__global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
+                                                     float* __restrict__ acc, const BounceRec* __restrict__ queue,
+                                                     uint32_t* __restrict__ qctl, int threshold)
+{
+    __shared__ uint32_t cstack[kMaxDepth * 256];
+    uint32_t* cs = cstack + threadIdx.x;
+    Counters cnt{0, 0, 0, 0, 0};
+    const uint32_t n = __builtin_amdgcn_readfirstlane(qctl[0]);
+    const uint32_t end = sc.num_nodes;
+    bool has = false, exhausted = false;
+    Ray ray{0, 0, 0, 0, 0, 0};
+    SlabRay sr = slab_ray(ray);
+    SphRay sp = sph_ray(ray);
+    uint32_t next = end, pixel = 0, k = 0, base0 = 0;
+    int level = 0, best_s = -1;
+    float best_t = INFINITY;
+    uint64_t key = 0;
+    for (;;) {
+        // refill lanes that own no chain (one atomic per wave, tile order kept)
+        const uint64_t need = __ballot(!has);
+        if (need && !exhausted) {
+            const int leader = __builtin_ctzll(need);
+            uint32_t b = 0;
+            if ((threadIdx.x & 63) == leader) b = atomicAdd(&qctl[1], (uint32_t)__popcll(need));
+            b = __builtin_amdgcn_readlane(b, leader);
+            if (b + (uint32_t)__popcll(need) >= n) exhausted = true;
+            if (!has) {
+                const uint32_t idx = b + lanes_below(need);
+                if (idx < n) {
+                    const BounceRec rec = queue[idx];
+                    ray = Ray{rec.ox, rec.oy, rec.oz, rec.dx, rec.dy, rec.dz};
+                    sr = slab_ray(ray);
+                    sp = sph_ray(ray);
+                    pixel = rec.pixel;
+                    k = rec.k;
+                    base0 = rec.base0;
+                    level = 1;
+                    const int r = (int)(pixel / f.width), x = (int)(pixel - r * f.width);
+                    key = pixel_key(f.seed, (uint32_t)(shard_row_to_y(f, r) * f.width + x), f.sample);
+                    next = 0;
+                    best_t = INFINITY;
+                    best_s = -1;
+                    has = true;
+                }
+            }
+        }
+        if (!__ballot(has)) break;
+        // walk until few lanes are still walking and the others can make progress
+        for (;;) {
+            const uint64_t walking = __ballot(has && next < end);
+            if (!walking) break;
+            if (__popcll(walking) < threshold &&
+                (__ballot(has && next >= end) || (!exhausted && __ballot(!has))))
+                break;
+            if (has && next < end) lane_step<FAST, false>(sc, sr, sp, next, best_t, best_s, cnt);
+        }
+        // shade every lane whose ray is done (renderer.c:46-77 for that level)
+        if (has && next >= end) {
+            bool finish = true;
+            uint32_t tail = 255u << 24;          // depth exhausted: black (renderer.c:23-24)
+            int stored = level - 1;
+            if (best_s < 0) {
+                tail = sky_rgba(ray.dy);
+            } else {
+                cs[(level - 1) * 256] = sc.color[best_s];
+                stored = level;
+                if (level + 1 < f.depth) {       // trace_ray(bounce, depth - 1) still has depth
+                    const float4 g = sc.geo[best_s];
+                    float p[3], nn[3];
+                    hit_point_normal(ray, best_t, g, p, nn);
+                    float bx, by, bz;
+                    hemisphere(key, k, nn, bx, by, bz);
+                    ray = Ray{p[0], p[1], p[2], bx, by, bz};
+                    sr = slab_ray(ray);
+                    sp = sph_ray(ray);
+                    next = 0;
+                    best_t = INFINITY;
+                    best_s = -1;
+                    level++;
+                    finish = false;
+                }
+            }
+            if (finish) {
+                uint32_t c = tail;
+                for (int l = stored - 1; l >= 0; l--) c = blend_rgba(cs[l * 256], c);
+                store_pixel(f, out, acc, pixel, blend_rgba(base0, c));
+                has = false;
+            }
+        }
+    }
+}
+
 // trace_ray on explicit rays (renderer.c:21); ray i uses contract pixel i.
 template <int TRAV, bool FAST>
 __global__ __launch_bounds__(256) void trace_rays_kernel(DevScene sc, const mirt_ray* __restrict__ rays, int n,
@@ -318,10 +511,14 @@ struct mirt_ctx {
     size_t in_cap = 0, res_cap = 0;
     mirt_counts* d_counts = nullptr;
     // kernel schedule (mirt_set_option)
-    int trav = kTravHybridNP;
+    int trav = kTravWavefront;
     int fast_slab = 1;
     int block_waves = 4;  // waves (8x8 tiles) per workgroup
     int defer = 1;        // trace zero-component camera rays in leading waves
+    int bounce_threshold = 40;  // wavefront: shade finished rays once fewer lanes walk
+    int bounce_blocks = 0;      // wavefront: persistent workgroups (set in mirt_create)
+    void* d_queue = nullptr;    // wavefront: {count, head} + bounce records
+    size_t queue_cap = 0;
     uint32_t* d_defer = nullptr;  // [count, list...]
     size_t defer_cap = 0;
 };
@@ -404,6 +601,8 @@ int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_ac
     const int blocks = (tiles + bw - 1) / bw;
     if (blocks == 0) return MIRT_OK;
     if (timed) HIP_TRY(hipEventRecord(c->ev0, s));
+    const bool wavefront = c->trav == kTravWavefront && f.use_bvh && f.depth >= 2 && !d_counts;
+    const int dbw = wavefront ? 4 : bw;  // the wavefront kernels use 256-thread workgroups
     Deferred dfr{nullptr, nullptr, 0};
     if (f.use_bvh && c->defer) {
         const size_t pixels = (size_t)f.num_rows * f.width;
@@ -415,9 +614,28 @@ int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_ac
         // enough waves for the centre row and column of an axis-aligned
         // camera; a longer list is strided over the same waves
         const size_t want = std::min(pixels, (size_t)(f.width + f.num_rows + 64));
-        dfr = Deferred{c->d_defer + 1, c->d_defer, (int)((want + bw - 1) / bw)};
+        dfr = Deferred{c->d_defer + 1, c->d_defer, (int)((want + dbw - 1) / dbw)};
     }
     const DevScene sc = dev_scene(c);
+    if (wavefront) {
+        const size_t pixels = (size_t)f.num_rows * f.width;
+        int rc = ensure(&c->d_queue, &c->queue_cap, sizeof(BounceRec) * pixels + 64);
+        if (rc) return rc;
+        uint32_t* qctl = (uint32_t*)c->d_queue;                          // {count, head}
+        BounceRec* queue = (BounceRec*)((char*)c->d_queue + 64);
+        HIP_TRY(hipMemsetAsync(qctl, 0, 8, s));
+        const int pblocks = (tiles + 3) / 4 + dfr.blocks;
+        if (c->fast_slab) {
+            primary_kernel<true><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
+            bounce_kernel<true><<<c->bounce_blocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold);
+        } else {
+            primary_kernel<false><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
+            bounce_kernel<false><<<c->bounce_blocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold);
+        }
+        HIP_TRY(hipGetLastError());
+        if (timed) HIP_TRY(hipEventRecord(c->ev1, s));
+        return MIRT_OK;
+    }
     if (d_counts)
         dispatch_render<true>(c->trav, true, sc, f, d_out, d_acc, s, blocks, bw, d_counts, d_wave_stats, dfr);
     else
@@ -448,6 +666,13 @@ int mirt_create(int device, mirt_ctx** out)
     if (e == hipSuccess) e = hipEventCreate(&c->ev0);
     if (e == hipSuccess) e = hipEventCreate(&c->ev1);
     if (e == hipSuccess) e = hipMalloc((void**)&c->d_counts, sizeof(mirt_counts));
+    if (e == hipSuccess) {
+        int cus = 0, per_cu = 0;
+        e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+        if (e == hipSuccess)
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bounce_kernel<true>, 256, 0);
+        c->bounce_blocks = std::max(1, cus) * std::max(1, per_cu);
+    }
     if (e != hipSuccess) {
         mirt_destroy(c);
         return hip_fail(e, "mirt_create");
@@ -462,7 +687,7 @@ void mirt_destroy(mirt_ctx* c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : {(void*)c->d_nodes, (void*)c->d_nodes32, (void*)c->d_geo, (void*)c->d_color, (void*)c->d_out, (void*)c->d_acc,
-                    c->d_in, c->d_res, (void*)c->d_counts, (void*)c->d_defer})
+                    c->d_in, c->d_res, (void*)c->d_counts, (void*)c->d_defer, c->d_queue})
         if (p) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -788,11 +1013,15 @@ int mirt_set_option(mirt_ctx* c, int option, int value)
     if (!c) return MIRT_E_INVALID;
     switch (option) {
     case MIRT_OPT_TRAVERSAL:
-        if (value < MIRT_TRAV_UNIFORM || value > MIRT_TRAV_HYBRID_NP) break;
+        if (value < MIRT_TRAV_UNIFORM || value > MIRT_TRAV_WAVEFRONT) break;
         c->trav = value;
         return MIRT_OK;
     case MIRT_OPT_FAST_SLAB:
         c->fast_slab = value != 0;
+        return MIRT_OK;
+    case MIRT_OPT_BOUNCE_THRESHOLD:
+        if (value < 0 || value > 64) break;
+        c->bounce_threshold = value;
         return MIRT_OK;
     case MIRT_OPT_DEFER:
         c->defer = value != 0;
@@ -815,6 +1044,7 @@ int mirt_get_option(mirt_ctx* c, int option)
     if (option == MIRT_OPT_FAST_SLAB) return c->fast_slab;
     if (option == MIRT_OPT_BLOCK_WAVES) return c->block_waves;
     if (option == MIRT_OPT_DEFER) return c->defer;
+    if (option == MIRT_OPT_BOUNCE_THRESHOLD) return c->bounce_threshold;
     set_error("mirt_get_option: bad option %d", option);
     return MIRT_E_INVALID;
 }

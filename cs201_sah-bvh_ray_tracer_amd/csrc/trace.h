@@ -396,6 +396,37 @@ __device__ __forceinline__ void closest_bvh(const DevScene& sc, const Ray& ray, 
     }
 }
 
+// One step of the per-lane walk with on-demand loads (the body of
+// closest_bvh's LANE_NP loop), for kernels that interleave walking with
+// other per-lane work.
+template <bool FAST, bool COUNT>
+__device__ __forceinline__ void lane_step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, uint32_t& next,
+                                          float& best_t, int& best_s, Counters& cnt)
+{
+    const float4* p = (const float4*)(sc.nodes32 + next);
+    const float4 a = p[0], b = p[1];
+    NodeV nd;
+    nd.b0 = a.x; nd.b1 = a.y; nd.b2 = a.z; nd.b3 = a.w; nd.b4 = b.x; nd.b5 = b.y;
+    nd.sphere = __float_as_int(b.z);
+    nd.skip = __float_as_uint(b.w);
+    const bool inner = nd.sphere < 0;
+    const bool pass = (nd.skip & MIRT_NODE_EMPTY) || slab<FAST>(sr, nd);
+    if (COUNT) cnt.nodes++;
+    if (pass && inner) {
+        next = next + 1;
+    } else {
+        if (pass) {
+            if (COUNT) cnt.spheres++;
+            const float t = sphere_t<FAST>(sp, sc.geo[nd.sphere], best_t);
+            if (t > 0.0f) {
+                best_t = t;
+                best_s = nd.sphere;
+            }
+        }
+        next = nd.skip & MIRT_SKIP_MASK;
+    }
+}
+
 __device__ __forceinline__ float wave_min(float v)
 {
 #pragma unroll
@@ -602,7 +633,9 @@ __device__ __forceinline__ uint32_t blend_rgba(uint32_t base, uint32_t refl)
 
 // Traversal schedules (mirt_set_option MIRT_OPT_TRAVERSAL).
 // LANE / HYBRID prefetch both successors; the *_NP forms load on demand.
-enum Trav { kTravUniform = 0, kTravLane = 1, kTravHybrid = 2, kTravLaneNP = 3, kTravHybridNP = 4 };
+// WAVEFRONT: camera rays as packets, then persistent per-lane bounce chains
+// fed by a queue (render.hip primary_kernel / bounce_kernel), depth >= 2.
+enum Trav { kTravUniform = 0, kTravLane = 1, kTravHybrid = 2, kTravLaneNP = 3, kTravHybridNP = 4, kTravWavefront = 5 };
 
 // trace_ray (renderer.c:21-77) with the recursion turned into a loop over
 // bounce levels that the whole wave executes together (the traversal needs

@@ -232,15 +232,19 @@ float mirt_last_kernel_ms(mirt_ctx *ctx);
    cursor, scalar node loads), MIRT_TRAV_LANE (each lane walks alone, vector
    node loads), MIRT_TRAV_HYBRID (uniform for camera rays, per-lane for
    bounces), MIRT_TRAV_HYBRID_NP (the same without successor prefetch in the
-   per-lane walk; default). MIRT_OPT_FAST_SLAB: 1 (default) = reciprocal-multiply
+   per-lane walk). MIRT_OPT_FAST_SLAB: 1 (default) = reciprocal-multiply
    slab test with an exact-division fallback for undecidable boxes; 0 = the
    division-only slab test of hit.c:49-82. MIRT_OPT_BLOCK_WAVES: 8x8 pixel
    tiles (waves) per workgroup of the frame kernel: 1, 2, 4 (default) or 8.
    MIRT_OPT_DEFER: 1 (default) = camera rays with a zero/tiny direction
    component are traced first, one per wave (node-parallel walk). */
-enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3, MIRT_OPT_DEFER = 4 };
+enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3, MIRT_OPT_DEFER = 4,
+       MIRT_OPT_BOUNCE_THRESHOLD = 5 /* wavefront: shade finished bounce rays once fewer than
+                                        this many lanes of a wave still walk (0..64, default 32) */ };
 enum { MIRT_TRAV_UNIFORM = 0, MIRT_TRAV_LANE = 1, MIRT_TRAV_HYBRID = 2, MIRT_TRAV_LANE_NP = 3,
-       MIRT_TRAV_HYBRID_NP = 4 };  /* *_NP: per-lane walk without successor prefetch */
+       MIRT_TRAV_HYBRID_NP = 4,  /* *_NP: per-lane walk without successor prefetch */
+       MIRT_TRAV_WAVEFRONT = 5   /* default: camera-ray packets, then persistent per-lane
+                                    bounce chains fed by a queue (depth >= 2) */ };
 int mirt_set_option(mirt_ctx *ctx, int option, int value);
 int mirt_get_option(mirt_ctx *ctx, int option);
 

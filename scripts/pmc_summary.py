@@ -18,10 +18,13 @@ for d in sorted(glob.glob(os.path.join(root, "t*_f*_d*.*"))):
         continue
     acc = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
-        if "render_kernel" in r["Kernel_Name"] and "true, true" not in r["Kernel_Name"]:
-            acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    for k, v in acc.items():
-        cfgs[cfg][k] = statistics.median(v)
+        name = r["Kernel_Name"]
+        kern = ("bounce" if "bounce_kernel" in name else "primary" if "primary_kernel" in name else
+                "render" if "render_kernel" in name and "true, true" not in name else None)
+        if kern:
+            acc[(kern, r["Counter_Name"])].append(float(r["Counter_Value"]))
+    for (kern, k), v in acc.items():
+        cfgs[cfg + "/" + kern][k] = statistics.median(v)
 for cfg, c in cfgs.items():
     g = c.get("GRBM_GUI_ACTIVE", 0) / 8
     print(cfg, "kernel_cycles(per XCD)", int(g))
@@ -34,4 +37,7 @@ for cfg, c in cfgs.items():
         print("   derived: VALU busy per SIMD %.3f" % (c["SQ_INSTS_VALU"] * 2 / (g * 1024)))
     if "TCC_HIT_sum" in c:
         print("   derived: L2 hit %.3f  TA busy frac %.3f" % (
-            c["TCC_HIT_sum"] / max(1, c["TCC_HIT_sum"] + c["TCC_MISS_sum"]), c["TA_TA_BUSY_sum"] / max(1, g * 256)))
+            c["TCC_HIT_sum"] / max(1, c["TCC_HIT_sum"] + c["TCC_MISS_sum"]), c.get("TA_TA_BUSY_sum", 0) / max(1, g * 256)))
+    if "TCP_TOTAL_CACHE_ACCESSES_sum" in c:
+        print("   derived: L1 miss->L2 requests / accesses %.3f" % (
+            c["TCP_TCC_READ_REQ_sum"] / max(1, c["TCP_TOTAL_CACHE_ACCESSES_sum"])))

@@ -22,6 +22,7 @@ VARIANTS = {
     "lane_exact": (abi.TRAV_LANE, 0), "lane_fast": (abi.TRAV_LANE, 1),
     "hybrid_exact": (abi.TRAV_HYBRID, 0), "hybrid_fast": (abi.TRAV_HYBRID, 1),
     "lanenp_fast": (abi.TRAV_LANE_NP, 1), "hybridnp_fast": (abi.TRAV_HYBRID_NP, 1),
+    "wavefront_fast": (abi.TRAV_WAVEFRONT, 1), "wavefront_exact": (abi.TRAV_WAVEFRONT, 0),
 }
 
 

@@ -192,7 +192,7 @@ def test_sentinel_and_edge_scenes(gpu, mirt, oracle):
     assert (img == ref).all()
 
 
-@pytest.mark.parametrize("trav", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("trav", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("fast", [0, 1])
 @pytest.mark.parametrize("defer", [0, 1])
 def test_all_schedules_bit_identical(gpu, mirt, golden, small, scene1000, trav, fast, defer):
@@ -215,7 +215,7 @@ def test_all_schedules_bit_identical(gpu, mirt, golden, small, scene1000, trav, 
             img = gpu.render_frame(cam, 1920, 1080, depth=depth, seed=1)
             assert sha(img) == golden["frames"][key]["sha"], key
     finally:
-        gpu.set_option(abi.OPT_TRAVERSAL, abi.TRAV_HYBRID_NP)
+        gpu.set_option(abi.OPT_TRAVERSAL, abi.TRAV_WAVEFRONT)
         gpu.set_option(abi.OPT_FAST_SLAB, 1)
         gpu.set_option(abi.OPT_DEFER, 1)
 
