@@ -60,7 +60,8 @@ class FrameDesc(C.Structure):
 class Counts(C.Structure):
     """mirt_counts"""
     _fields_ = [("rays", C.c_uint64), ("nodes", C.c_uint64), ("spheres", C.c_uint64), ("hits", C.c_uint64),
-                ("lane_steps", C.c_uint64)]
+                ("lane_steps", C.c_uint64), ("nodes_primary", C.c_uint64), ("spheres_primary", C.c_uint64),
+                ("hits_primary", C.c_uint64)]
 
 
 def default_camera():
@@ -119,6 +120,7 @@ SIGNATURES = [
     ("mirt_count_frame", I, [P, P, P, P]),
     ("mirt_wave_stats", I, [P, P, P, P, I]),
     ("mirt_last_kernel_ms", C.c_float, [P]),
+    ("mirt_last_phase_ms", I, [P, C.POINTER(C.c_float)]),
     ("mirt_set_option", I, [P, I, I]),
     ("mirt_get_option", I, [P, I]),
 ]

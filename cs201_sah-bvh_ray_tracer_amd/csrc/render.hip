@@ -93,6 +93,9 @@ __device__ __forceinline__ void add_counts(mirt_counts* out, const Counters& c)
     atomicAdd((unsigned long long*)&out->spheres, (unsigned long long)c.spheres);
     atomicAdd((unsigned long long*)&out->hits, (unsigned long long)c.hits);
     atomicAdd((unsigned long long*)&out->lane_steps, (unsigned long long)c.steps);
+    atomicAdd((unsigned long long*)&out->nodes_primary, (unsigned long long)c.nodes0);
+    atomicAdd((unsigned long long*)&out->spheres_primary, (unsigned long long)c.spheres0);
+    atomicAdd((unsigned long long*)&out->hits_primary, (unsigned long long)c.hits0);
 }
 
 // Pixels whose camera ray has a zero or tiny direction component (the image
@@ -495,6 +498,9 @@ struct mirt_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     float last_ms = 0.0f;
+    // wavefront phase boundaries of the last frame (any API)
+    hipEvent_t ph0 = nullptr, ph1 = nullptr, ph2 = nullptr;
+    bool phases_valid = false;
     // scene (replicated per device, uploaded once)
     DNode* d_nodes = nullptr;
     mirt_node* d_nodes32 = nullptr;
@@ -604,6 +610,8 @@ int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_ac
     const bool wavefront = c->trav == kTravWavefront && f.use_bvh && f.depth >= 2 && !d_counts;
     const int dbw = wavefront ? 4 : bw;  // the wavefront kernels use 256-thread workgroups
     Deferred dfr{nullptr, nullptr, 0};
+    c->phases_valid = wavefront;
+    if (wavefront) HIP_TRY(hipEventRecord(c->ph0, s));
     if (f.use_bvh && c->defer) {
         const size_t pixels = (size_t)f.num_rows * f.width;
         int rc = ensure((void**)&c->d_defer, &c->defer_cap, 4 * (pixels + 1));
@@ -625,14 +633,18 @@ int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_ac
         BounceRec* queue = (BounceRec*)((char*)c->d_queue + 64);
         HIP_TRY(hipMemsetAsync(qctl, 0, 8, s));
         const int pblocks = (tiles + 3) / 4 + dfr.blocks;
-        if (c->fast_slab) {
+        if (c->fast_slab)
             primary_kernel<true><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
-            bounce_kernel<true><<<c->bounce_blocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold);
-        } else {
+        else
             primary_kernel<false><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
-            bounce_kernel<false><<<c->bounce_blocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold);
-        }
         HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(c->ph1, s));
+        if (c->fast_slab)
+            bounce_kernel<true><<<c->bounce_blocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold);
+        else
+            bounce_kernel<false><<<c->bounce_blocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(c->ph2, s));
         if (timed) HIP_TRY(hipEventRecord(c->ev1, s));
         return MIRT_OK;
     }
@@ -665,6 +677,9 @@ int mirt_create(int device, mirt_ctx** out)
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&c->ev0);
     if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+    if (e == hipSuccess) e = hipEventCreate(&c->ph0);
+    if (e == hipSuccess) e = hipEventCreate(&c->ph1);
+    if (e == hipSuccess) e = hipEventCreate(&c->ph2);
     if (e == hipSuccess) e = hipMalloc((void**)&c->d_counts, sizeof(mirt_counts));
     if (e == hipSuccess) {
         int cus = 0, per_cu = 0;
@@ -691,6 +706,8 @@ void mirt_destroy(mirt_ctx* c)
         if (p) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    for (hipEvent_t ev : {c->ph0, c->ph1, c->ph2})
+        if (ev) (void)hipEventDestroy(ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1007,6 +1024,20 @@ int mirt_aabb_pairs(mirt_ctx* c, const mirt_ray* rays, const mirt_aabb* boxes, i
 }
 
 float mirt_last_kernel_ms(mirt_ctx* c) { return c ? c->last_ms : 0.0f; }
+
+int mirt_last_phase_ms(mirt_ctx* c, float* phase)
+{
+    if (!c || !phase) return MIRT_E_INVALID;
+    if (!c->phases_valid) {
+        set_error("mirt_last_phase_ms: the last frame did not use the wavefront schedule");
+        return MIRT_E_INVALID;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipEventSynchronize(c->ph2));
+    HIP_TRY(hipEventElapsedTime(&phase[0], c->ph0, c->ph1));
+    HIP_TRY(hipEventElapsedTime(&phase[1], c->ph1, c->ph2));
+    return MIRT_OK;
+}
 
 int mirt_set_option(mirt_ctx* c, int option, int value)
 {

@@ -52,6 +52,9 @@ struct Ray {
 struct Counters {
     uint32_t rays, nodes, spheres, hits;
     uint32_t steps;  // traversal loop iterations executed (every lane counts; /64 = wave steps)
+    // the camera-ray level alone (the wavefront schedule's primary pass);
+    // the rest of nodes/spheres/hits is the bounce pass
+    uint32_t nodes0, spheres0, hits0;
 };
 
 // A node in registers (12 dwords).
@@ -687,6 +690,11 @@ __device__ __forceinline__ uint32_t trace_path(const DevScene& sc, Ray ray, bool
                     alive = false;
                 }
             }
+        }
+        if (COUNT && level == 0) {
+            cnt.nodes0 = cnt.nodes;
+            cnt.spheres0 = cnt.spheres;
+            cnt.hits0 = cnt.hits;
         }
     }
     for (int l = levels - 1; l >= 0; l--) tail = blend_rgba(cstack[l * cstride], tail);

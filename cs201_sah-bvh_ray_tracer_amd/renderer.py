@@ -206,7 +206,7 @@ class Renderer:
         fd = frame_desc(width, height, depth, use_bvh, seed, sample, False, 1, row_block, shard, num_shards)
         c = abi.Counts()
         check(self.L.mirt_count_frame(self.h, C.byref(cam), C.byref(fd), C.byref(c)), "mirt_count_frame")
-        return {"rays": c.rays, "nodes": c.nodes, "spheres": c.spheres, "hits": c.hits, "lane_steps": c.lane_steps}
+        return {k: getattr(c, k) for k, _ in abi.Counts._fields_}
 
     def set_option(self, option, value):
         """abi.OPT_TRAVERSAL (abi.TRAV_*) / abi.OPT_FAST_SLAB (0/1): speed only."""
@@ -228,6 +228,12 @@ class Renderer:
     @property
     def last_kernel_ms(self):
         return self.L.mirt_last_kernel_ms(self.h)
+
+    def last_phase_ms(self):
+        """(primary ms, bounce ms) of the last wavefront-schedule frame; waits for it."""
+        out = (C.c_float * 2)()
+        check(self.L.mirt_last_phase_ms(self.h, out), "mirt_last_phase_ms")
+        return float(out[0]), float(out[1])
 
     # ---- per-ray surface (batched)
     def get_camera_rays(self, cam, width, height, row_block=8, shard=0, num_shards=1):

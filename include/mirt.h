@@ -111,6 +111,11 @@ typedef struct mirt_counts {
     uint64_t hits;       /* rays that found a closest hit */
     uint64_t lane_steps; /* traversal loop iterations x 64 lanes executed by the
                             default schedule; nodes / lane_steps = SIMD efficiency */
+    /* the camera-ray level alone (depth level 0 = the wavefront schedule's
+       primary pass); nodes - nodes_primary etc. is the bounce pass */
+    uint64_t nodes_primary;
+    uint64_t spheres_primary;
+    uint64_t hits_primary;
 } mirt_counts;
 
 enum {
@@ -225,6 +230,12 @@ int mirt_wave_stats(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_desc
 
 /* Device time (ms) of the last render kernel launched by a blocking call. */
 float mirt_last_kernel_ms(mirt_ctx *ctx);
+
+/* Device time (ms) of the two passes of the last frame this ctx launched
+   with the wavefront schedule (blocking or _device call; waits for it):
+   phase[0] = deferral mark + primary kernel (camera rays), phase[1] = the
+   bounce kernel. Returns MIRT_E_INVALID if no wavefront frame was launched. */
+int mirt_last_phase_ms(mirt_ctx *ctx, float *phase);
 
 /* Kernel schedule knobs (results are identical under every setting; only
    speed changes). MIRT_OPT_TRAVERSAL: how a wave walks the tree --

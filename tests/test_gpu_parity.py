@@ -163,6 +163,23 @@ def test_counts_match_oracle(gpu, mirt, oracle):
     oracle.free(t)
     got = gpu.count_frame(cam, 320, 180, depth=5, seed=1)
     assert (got["rays"], got["nodes"], got["spheres"]) == tuple(int(x) for x in cnt)
+    # the camera-ray level of a depth-5 frame is the whole of a depth-1 frame
+    d1 = gpu.count_frame(cam, 320, 180, depth=1, seed=1)
+    assert (got["nodes_primary"], got["spheres_primary"], got["hits_primary"]) == \
+        (d1["nodes"], d1["spheres"], d1["hits"])
+    assert d1["nodes_primary"] == d1["nodes"]
+
+
+def test_phase_timing(gpu, mirt):
+    s, b = _scene(mirt, "render", 10000)
+    gpu.upload(s, b)
+    cam = mirt.default_camera()
+    gpu.render_frame(cam, 320, 180, depth=5, seed=1)
+    primary, bounce = gpu.last_phase_ms()
+    assert primary > 0 and bounce > 0
+    gpu.render_frame(cam, 320, 180, depth=1, seed=1)   # depth 1 has no bounce pass
+    with pytest.raises(mirt.MirtError):
+        gpu.last_phase_ms()
 
 
 def test_sentinel_and_edge_scenes(gpu, mirt, oracle):
