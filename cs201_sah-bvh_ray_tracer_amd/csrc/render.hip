@@ -311,6 +311,7 @@ __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, 
     Ray ray{0, 0, 0, 0, 0, 0};
     SlabRay sr = slab_ray(ray);
     SphRay sp = sph_ray(ray);
+    Prune pr = prune_off();
     uint32_t next = end, pixel = 0, k = 0, base0 = 0;
     int level = 0, best_s = -1;
     float best_t = INFINITY;
@@ -340,6 +341,7 @@ __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, 
                     next = 0;
                     best_t = INFINITY;
                     best_s = -1;
+                    pr = prune_off();
                     has = true;
                 }
             }
@@ -352,7 +354,7 @@ __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, 
             if (__popcll(walking) < threshold &&
                 (__ballot(has && next >= end) || (!exhausted && __ballot(!has))))
                 break;
-            if (has && next < end) lane_step<FAST, false>(sc, sr, sp, next, best_t, best_s, cnt);
+            if (has && next < end) lane_step<FAST, false>(sc, sr, sp, pr, next, best_t, best_s, cnt);
         }
         // shade every lane whose ray is done (renderer.c:46-77 for that level)
         if (has && next >= end) {
@@ -376,6 +378,7 @@ __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, 
                     next = 0;
                     best_t = INFINITY;
                     best_s = -1;
+                    pr = prune_off();
                     level++;
                     finish = false;
                 }
@@ -521,6 +524,9 @@ struct mirt_ctx {
     int fast_slab = 1;
     int block_waves = 4;  // waves (8x8 tiles) per workgroup
     int defer = 1;        // trace zero-component camera rays in leading waves
+    int prune = 1;              // closest-hit pruning (trace.h Prune), FAST slab only
+    bool prune_ok = false;      // the uploaded tree's boxes enclose their subtrees
+    float r_max = 0.0f, c_max = 0.0f;
     int bounce_threshold = 40;  // wavefront: shade finished rays once fewer lanes walk
     int bounce_blocks = 0;      // wavefront: persistent workgroups (set in mirt_create)
     void* d_queue = nullptr;    // wavefront: {count, head} + bounce records
@@ -554,9 +560,52 @@ int ensure(void** p, size_t* cap, size_t bytes)
     return MIRT_OK;
 }
 
+// The pruning bound (trace.h Prune) holds for a tree in which every leaf box
+// holds its sphere's box as bvh.c:26-46 computes it, fl(c -+ r), and every
+// inner box holds both children's boxes; the reference's own trees are built
+// that way. Also returns the scene constants of the bound. A NaN anywhere,
+// a non-finite sphere or a tree that does not nest turns pruning off.
+bool tree_encloses(const mirt_sphere* sp, int ns, const mirt_node* nd, int nn, float* r_max, float* c_max)
+{
+    float rm = 0.0f, cm = 0.0f;
+    for (int i = 0; i < ns; i++) {
+        const float c[3] = {sp[i].center.x, sp[i].center.y, sp[i].center.z};
+        const float r = std::fabs(sp[i].radius);
+        if (!std::isfinite(c[0]) || !std::isfinite(c[1]) || !std::isfinite(c[2]) || !std::isfinite(r)) return false;
+        rm = std::max(rm, r);
+        cm = std::max(cm, std::max(std::fabs(c[0]), std::max(std::fabs(c[1]), std::fabs(c[2]))) + r);
+    }
+    auto holds = [](const mirt_node& outer, const mirt_node& inner) {
+        if (inner.skip & MIRT_NODE_EMPTY) return true;  // +inf/-inf box, no sphere
+        for (int k = 0; k < 3; k++)
+            if (!(outer.bmin[k] <= inner.bmin[k] && outer.bmax[k] >= inner.bmax[k])) return false;
+        return true;
+    };
+    for (int i = 0; i < nn; i++) {
+        const mirt_node& n = nd[i];
+        if (n.skip & MIRT_NODE_EMPTY) continue;
+        if (n.sphere >= 0) {
+            if (n.sphere >= ns) continue;  // the never-hit sentinel
+            const mirt_sphere& s = sp[n.sphere];
+            const float c[3] = {s.center.x, s.center.y, s.center.z};
+            const float r = std::fabs(s.radius);
+            for (int k = 0; k < 3; k++)
+                if (!(n.bmin[k] <= c[k] - r && n.bmax[k] >= c[k] + r)) return false;
+        } else {
+            const uint32_t left = (uint32_t)i + 1, right = nd[left].skip & MIRT_SKIP_MASK;
+            if (!holds(n, nd[left]) || (right < (uint32_t)nn && right < (n.skip & MIRT_SKIP_MASK) && !holds(n, nd[right])))
+                return false;
+        }
+    }
+    *r_max = rm;
+    *c_max = cm;
+    return true;
+}
+
 DevScene dev_scene(const mirt_ctx* c)
 {
-    return DevScene{c->d_nodes, c->d_nodes32, c->d_geo, c->d_color, (uint32_t)c->num_nodes, c->num_spheres};
+    return DevScene{c->d_nodes, c->d_nodes32, c->d_geo, c->d_color, (uint32_t)c->num_nodes, c->num_spheres,
+                    c->prune && c->prune_ok, c->r_max, c->c_max};
 }
 
 bool ctx_ok(mirt_ctx* c, bool need_scene, const char* fn)
@@ -733,6 +782,8 @@ int mirt_scene_upload_flat(mirt_ctx* c, const mirt_sphere* spheres, int ns, cons
         set_error("mirt_scene_upload_flat: root skip %u != node count %d", nodes[0].skip & MIRT_SKIP_MASK, nn);
         return MIRT_E_INVALID;
     }
+    float r_max = 0.0f, c_max = 0.0f;
+    const bool encloses = tree_encloses(spheres, ns, nodes, nn, &r_max, &c_max);
     std::vector<float4> geo((size_t)ns + 1);
     std::vector<uint32_t> col((size_t)ns + 1);
     for (int i = 0; i < ns; i++) {
@@ -769,6 +820,9 @@ int mirt_scene_upload_flat(mirt_ctx* c, const mirt_sphere* spheres, int ns, cons
     HIP_TRY(hipMemcpy(c->d_color, col.data(), sizeof(uint32_t) * col.size(), hipMemcpyHostToDevice));
     c->num_nodes = nn;
     c->num_spheres = ns;
+    c->prune_ok = encloses;
+    c->r_max = r_max;
+    c->c_max = c_max;
     return MIRT_OK;
 }
 
@@ -1057,6 +1111,9 @@ int mirt_set_option(mirt_ctx* c, int option, int value)
     case MIRT_OPT_DEFER:
         c->defer = value != 0;
         return MIRT_OK;
+    case MIRT_OPT_PRUNE:
+        c->prune = value != 0;
+        return MIRT_OK;
     case MIRT_OPT_BLOCK_WAVES:
         if (value != 1 && value != 2 && value != 4 && value != 8) break;
         c->block_waves = value;
@@ -1076,6 +1133,7 @@ int mirt_get_option(mirt_ctx* c, int option)
     if (option == MIRT_OPT_BLOCK_WAVES) return c->block_waves;
     if (option == MIRT_OPT_DEFER) return c->defer;
     if (option == MIRT_OPT_BOUNCE_THRESHOLD) return c->bounce_threshold;
+    if (option == MIRT_OPT_PRUNE) return c->prune;
     set_error("mirt_get_option: bad option %d", option);
     return MIRT_E_INVALID;
 }

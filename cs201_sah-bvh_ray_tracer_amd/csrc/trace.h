@@ -43,6 +43,11 @@ struct DevScene {
     const uint32_t* color;  // packed RGBA8
     uint32_t num_nodes;
     int num_spheres;
+    // closest-hit pruning (Prune below): enabled only for a tree whose boxes
+    // enclose their subtrees (checked at upload)
+    int prune;
+    float r_max;   // largest sphere radius
+    float c_max;   // largest |centre|_inf + radius
 };
 
 struct Ray {
@@ -185,6 +190,45 @@ __device__ __forceinline__ bool slab_test(const SlabRay& r, float x0, float y0, 
     return tmax >= tmin && tmax > kEps;
 }
 
+// Closest-hit pruning: a walk may skip a subtree whose box the ray can only
+// enter beyond the best hit so far, because no sphere inside can then record
+// t <= best (the reference's DFS, hit.c:91-109, tests everything; the result
+// is the same closest hit with the same later-leaf-wins tie rule, since the
+// walk still visits leaves in DFS order and only drops losers).
+//
+// Bound: let sphere S (centre c, radius r) lie in box B and let its
+// hit.c:19-39 arithmetic return t' with t' <= best. The point p = o + t' d
+// (exact) then lies within D of S's surface: with the computed quadratic,
+// |p - c|^2 - r^2 equals the rounding error of the discriminant over 4a plus
+// the a/b roundings times t'^2 / t', all below 35 u M^2 (u = 2^-24,
+// M = max(|o - c|, r)), so D <= sqrt(35 u) M < 2^-9.3 M; and M <= t'|d| + r + D
+// <= best |d| + r_max + D. The reference's leaf boxes fl(c -+ r) and the
+// computed fl(o - c) move S by below 2^-22 (|o|_inf + c_max). Hence p lies in
+// B grown by m = 2^-8 (best |d| + r_max) + 2^-20 (|o|_inf + c_max) (>2x over
+// both terms; a float32 sweep of grazing rays peaks at 2^-10.5 M), so t' is at
+// least the entry t of the grown box, max_k (near_k - m |1/d_k|). slab_fast's
+// near_k is within 2^-21 of the exact (b_k - o_k) / d_k (its 2^-22 plus the
+// rounding of b_k - o_k), so
+// fma(near_k, 1 - 2^-20, -m |1/d_k|), when positive, is at most (1 + u) times
+// the exact grown near plane whatever the cancellation; the box is pruned only
+// when that computed entry exceeds lim = best (1 + 2^-18).
+struct Prune {
+    float m;    // growth of the box (world units)
+    float lim;  // prune when the grown box's entry t exceeds this; +inf = off
+};
+
+__device__ __forceinline__ Prune prune_off() { return {0.0f, INFINITY}; }
+
+// After a hit at t = best (finite). a4 = 4 d.d (SphRay).
+__device__ __forceinline__ void prune_update(Prune& p, const DevScene& sc, float ox, float oy, float oz, float a4,
+                                             float best)
+{
+    const float dl = __builtin_amdgcn_sqrtf(a4) * (0.5f + 0x1p-20f);  // >= |d|
+    const float oi = fmaxf(fabsf(ox), fmaxf(fabsf(oy), fabsf(oz)));
+    p.m = (best * dl + sc.r_max) * 0x1p-8f + (oi + sc.c_max) * 0x1p-20f;
+    p.lim = best + best * 0x1p-18f;
+}
+
 // The same predicate, decided from reciprocal-multiply estimates whenever
 // that is provably safe, else by slab_test (same result, bit for bit).
 //
@@ -199,13 +243,19 @@ __device__ __forceinline__ bool slab_test(const SlabRay& r, float x0, float y0, 
 // otherwise (near-tangent boxes) the exact division path decides.
 // Requires finite, normal-range reciprocals: rays with a zero or tiny
 // component take slab_test (`generic`), whose +-inf handling is exact.
-__device__ __forceinline__ bool slab_fast(const SlabRay& r, float x0, float y0, float z0, float x1, float y1,
-                                          float z1)
+// A box beyond the pruning limit (Prune) fails before any of this.
+__device__ __forceinline__ bool slab_fast(const SlabRay& r, const Prune& p, float x0, float y0, float z0, float x1,
+                                          float y1, float z1)
 {
     const float tx1 = (x0 - r.ox) * r.ix, tx2 = (x1 - r.ox) * r.ix;
     const float ty1 = (y0 - r.oy) * r.iy, ty2 = (y1 - r.oy) * r.iy;
     const float tz1 = (z0 - r.oz) * r.iz, tz2 = (z1 - r.oz) * r.iz;
-    const float tmin = fmaxf(fminf(tx1, tx2), fmaxf(fminf(ty1, ty2), fminf(tz1, tz2)));
+    const float nx = fminf(tx1, tx2), ny = fminf(ty1, ty2), nz = fminf(tz1, tz2);
+    constexpr float c = 1.0f - 0x1p-20f;
+    const float entry = fmaxf(fmaf(nx, c, -(p.m * fabsf(r.ix))),
+                              fmaxf(fmaf(ny, c, -(p.m * fabsf(r.iy))), fmaf(nz, c, -(p.m * fabsf(r.iz)))));
+    if (entry > p.lim) return false;
+    const float tmin = fmaxf(nx, fmaxf(ny, nz));
     const float tmax = fminf(fmaxf(tx1, tx2), fminf(fmaxf(ty1, ty2), fmaxf(tz1, tz2)));
     const float m = (fabsf(tmin) + fabsf(tmax)) * 0x1p-20f;
     const float gap = tmax - tmin, above = tmax - kEps;
@@ -215,9 +265,9 @@ __device__ __forceinline__ bool slab_fast(const SlabRay& r, float x0, float y0, 
 }
 
 template <bool FAST>
-__device__ __forceinline__ bool slab(const SlabRay& r, const NodeV& n)
+__device__ __forceinline__ bool slab(const SlabRay& r, const Prune& p, const NodeV& n)
 {
-    if (FAST && !r.generic) return slab_fast(r, n.b0, n.b1, n.b2, n.b3, n.b4, n.b5);
+    if (FAST && !r.generic) return slab_fast(r, p, n.b0, n.b1, n.b2, n.b3, n.b4, n.b5);
     return slab_test(r, n.b0, n.b1, n.b2, n.b3, n.b4, n.b5);
 }
 
@@ -290,6 +340,7 @@ __device__ __forceinline__ void closest_bvh(const DevScene& sc, const Ray& ray, 
 {
     const SlabRay sr = slab_ray(ray);
     const SphRay sp = sph_ray(ray);
+    Prune pr = prune_off();
     const uint32_t end = sc.num_nodes;
     const uint32_t last = end - 1;
     uint32_t next = active ? 0u : end;
@@ -309,7 +360,7 @@ __device__ __forceinline__ void closest_bvh(const DevScene& sc, const Ray& ray, 
             const NodeV nb = load_node_uniform(sc.nodes, min(skip, last));
             bool descend = false;
             if (next == cur) {
-                const bool pass = (nd.skip & MIRT_NODE_EMPTY) || slab<FAST>(sr, nd);
+                const bool pass = (nd.skip & MIRT_NODE_EMPTY) || slab<FAST>(sr, pr, nd);
                 if (COUNT) cnt.nodes++;
                 if (pass && inner) {
                     next = cur + 1;
@@ -322,6 +373,7 @@ __device__ __forceinline__ void closest_bvh(const DevScene& sc, const Ray& ray, 
                         if (t > 0.0f) {
                             best_t = t;
                             best_s = nd.sphere;
+                            if (sc.prune) prune_update(pr, sc, ray.ox, ray.oy, ray.oz, sp.a4, t);
                         }
                     }
                 }
@@ -348,7 +400,7 @@ __device__ __forceinline__ void closest_bvh(const DevScene& sc, const Ray& ray, 
                 nd.sphere = __float_as_int(b.z);
                 nd.skip = __float_as_uint(b.w);
                 const bool inner = nd.sphere < 0;
-                const bool pass = (nd.skip & MIRT_NODE_EMPTY) || slab<FAST>(sr, nd);
+                const bool pass = (nd.skip & MIRT_NODE_EMPTY) || slab<FAST>(sr, pr, nd);
                 if (COUNT) cnt.nodes++;
                 if (pass && inner) {
                     next = next + 1;
@@ -359,6 +411,7 @@ __device__ __forceinline__ void closest_bvh(const DevScene& sc, const Ray& ray, 
                         if (t > 0.0f) {
                             best_t = t;
                             best_s = nd.sphere;
+                            if (sc.prune) prune_update(pr, sc, ray.ox, ray.oy, ray.oz, sp.a4, t);
                         }
                     }
                     next = nd.skip & MIRT_SKIP_MASK;
@@ -377,7 +430,7 @@ __device__ __forceinline__ void closest_bvh(const DevScene& sc, const Ray& ray, 
                 const NodeV na = load_node_lane(sc.nodes, min(next + 1, last));
                 NodeV nb = na;
                 if (inner) nb = load_node_lane(sc.nodes, min(skip, last));
-                const bool pass = (nd.skip & MIRT_NODE_EMPTY) || slab<FAST>(sr, nd);
+                const bool pass = (nd.skip & MIRT_NODE_EMPTY) || slab<FAST>(sr, pr, nd);
                 if (COUNT) cnt.nodes++;
                 if (pass && inner) {
                     next = next + 1;
@@ -389,6 +442,7 @@ __device__ __forceinline__ void closest_bvh(const DevScene& sc, const Ray& ray, 
                         if (t > 0.0f) {
                             best_t = t;
                             best_s = nd.sphere;
+                            if (sc.prune) prune_update(pr, sc, ray.ox, ray.oy, ray.oz, sp.a4, t);
                         }
                     }
                     next = skip;
@@ -403,8 +457,8 @@ __device__ __forceinline__ void closest_bvh(const DevScene& sc, const Ray& ray, 
 // closest_bvh's LANE_NP loop), for kernels that interleave walking with
 // other per-lane work.
 template <bool FAST, bool COUNT>
-__device__ __forceinline__ void lane_step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, uint32_t& next,
-                                          float& best_t, int& best_s, Counters& cnt)
+__device__ __forceinline__ void lane_step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
+                                          uint32_t& next, float& best_t, int& best_s, Counters& cnt)
 {
     const float4* p = (const float4*)(sc.nodes32 + next);
     const float4 a = p[0], b = p[1];
@@ -413,7 +467,7 @@ __device__ __forceinline__ void lane_step(const DevScene& sc, const SlabRay& sr,
     nd.sphere = __float_as_int(b.z);
     nd.skip = __float_as_uint(b.w);
     const bool inner = nd.sphere < 0;
-    const bool pass = (nd.skip & MIRT_NODE_EMPTY) || slab<FAST>(sr, nd);
+    const bool pass = (nd.skip & MIRT_NODE_EMPTY) || slab<FAST>(sr, pr, nd);
     if (COUNT) cnt.nodes++;
     if (pass && inner) {
         next = next + 1;
@@ -424,6 +478,7 @@ __device__ __forceinline__ void lane_step(const DevScene& sc, const SlabRay& sr,
             if (t > 0.0f) {
                 best_t = t;
                 best_s = nd.sphere;
+                if (sc.prune) prune_update(pr, sc, sr.ox, sr.oy, sr.oz, sp.a4, t);
             }
         }
         next = nd.skip & MIRT_SKIP_MASK;
@@ -474,7 +529,7 @@ __device__ __forceinline__ void closest_bvh_chunked(const DevScene& sc, const Ra
             skip = nd.skip & MIRT_SKIP_MASK;
             leaf = nd.sphere >= 0;
             sph = nd.sphere;
-            pass = (nd.skip & MIRT_NODE_EMPTY) || slab<FAST>(sr, nd);
+            pass = (nd.skip & MIRT_NODE_EMPTY) || slab<FAST>(sr, prune_off(), nd);
             if (pass && leaf) t = sphere_t<FAST>(sp, nd.g, bt);
         }
         const uint64_t descend = __ballot(pass && !leaf);

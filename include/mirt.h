@@ -103,7 +103,8 @@ typedef struct mirt_frame_desc {
     int32_t num_shards;
 } mirt_frame_desc;
 
-/* Work counters of the reference DFS (hit.c:91-109, no pruning). */
+/* Work counters of the walk as configured; with MIRT_OPT_PRUNE = 0 they are
+   exactly the reference DFS (hit.c:91-109) node and sphere tests. */
 typedef struct mirt_counts {
     uint64_t rays;       /* rays traced (primary + bounces) */
     uint64_t nodes;      /* ray_aabb_intersect calls */
@@ -248,10 +249,15 @@ int mirt_last_phase_ms(mirt_ctx *ctx, float *phase);
    division-only slab test of hit.c:49-82. MIRT_OPT_BLOCK_WAVES: 8x8 pixel
    tiles (waves) per workgroup of the frame kernel: 1, 2, 4 (default) or 8.
    MIRT_OPT_DEFER: 1 (default) = camera rays with a zero/tiny direction
-   component are traced first, one per wave (node-parallel walk). */
+   component are traced first, one per wave (node-parallel walk).
+   MIRT_OPT_PRUNE: 1 (default) = with the fast slab test, skip subtrees whose
+   box the ray provably enters beyond the best hit so far (the closest hit and
+   its tie rule are unchanged; active only for a tree whose boxes enclose
+   their subtrees, checked at upload); 0 = the reference's exhaustive DFS. */
 enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3, MIRT_OPT_DEFER = 4,
-       MIRT_OPT_BOUNCE_THRESHOLD = 5 /* wavefront: shade finished bounce rays once fewer than
-                                        this many lanes of a wave still walk (0..64, default 32) */ };
+       MIRT_OPT_BOUNCE_THRESHOLD = 5, /* wavefront: shade finished bounce rays once fewer than
+                                         this many lanes of a wave still walk (0..64, default 40) */
+       MIRT_OPT_PRUNE = 6 };
 enum { MIRT_TRAV_UNIFORM = 0, MIRT_TRAV_LANE = 1, MIRT_TRAV_HYBRID = 2, MIRT_TRAV_LANE_NP = 3,
        MIRT_TRAV_HYBRID_NP = 4,  /* *_NP: per-lane walk without successor prefetch */
        MIRT_TRAV_WAVEFRONT = 5   /* default: camera-ray packets, then persistent per-lane

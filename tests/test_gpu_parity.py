@@ -161,13 +161,83 @@ def test_counts_match_oracle(gpu, mirt, oracle):
     t = oracle.build(s2)
     _, cnt = oracle.render(cam, 320, 180, s2, t, depth=5, mode=1, seed=1, counts=True)
     oracle.free(t)
-    got = gpu.count_frame(cam, 320, 180, depth=5, seed=1)
+    gpu.set_option(mirt.abi.OPT_PRUNE, 0)        # the reference's exhaustive DFS
+    try:
+        got = gpu.count_frame(cam, 320, 180, depth=5, seed=1)
+        d1 = gpu.count_frame(cam, 320, 180, depth=1, seed=1)
+    finally:
+        gpu.set_option(mirt.abi.OPT_PRUNE, 1)
     assert (got["rays"], got["nodes"], got["spheres"]) == tuple(int(x) for x in cnt)
     # the camera-ray level of a depth-5 frame is the whole of a depth-1 frame
-    d1 = gpu.count_frame(cam, 320, 180, depth=1, seed=1)
     assert (got["nodes_primary"], got["spheres_primary"], got["hits_primary"]) == \
         (d1["nodes"], d1["spheres"], d1["hits"])
     assert d1["nodes_primary"] == d1["nodes"]
+    # pruning: same rays and hits, strictly less walking
+    pr = gpu.count_frame(cam, 320, 180, depth=5, seed=1)
+    assert (pr["rays"], pr["hits"], pr["hits_primary"]) == (got["rays"], got["hits"], got["hits_primary"])
+    assert pr["nodes"] < got["nodes"] and pr["spheres"] < got["spheres"]
+
+
+def _hard_rays(rng, spheres, n):
+    """Rays that stress the pruning bound: bounce-like rays leaving sphere
+    surfaces, rays grazing sphere silhouettes, and rays from anywhere."""
+    from importlib import import_module
+    abi = import_module("cs201_sah-bvh_ray_tracer_amd").abi
+    c = spheres["center"].astype(np.float64)
+    r = spheres["radius"].astype(np.float64)
+    k = n // 3
+    rays = np.zeros(3 * k, abi.RAY)
+    # 1) leave a surface point into the outer hemisphere
+    i = rng.integers(0, len(spheres), k)
+    nrm = rng.normal(size=(k, 3))
+    nrm /= np.linalg.norm(nrm, axis=1)[:, None]
+    d = rng.normal(size=(k, 3))
+    d /= np.linalg.norm(d, axis=1)[:, None]
+    d *= np.sign((d * nrm).sum(1))[:, None]
+    rays["origin"][:k] = c[i] + nrm * r[i][:, None]
+    rays["direction"][:k] = d
+    # 2) aim at a point within 0.1% of a sphere's silhouette
+    i = rng.integers(0, len(spheres), k)
+    lo, hi = c.min(0) - 10, c.max(0) + 10
+    o = rng.uniform(lo, hi, (k, 3))
+    u = rng.normal(size=(k, 3))
+    u /= np.linalg.norm(u, axis=1)[:, None]
+    tgt = c[i] + u * (r[i] * rng.uniform(0.999, 1.001, k))[:, None]
+    d = tgt - o
+    d /= np.linalg.norm(d, axis=1)[:, None]
+    rays["origin"][k:2 * k] = o
+    rays["direction"][k:2 * k] = d
+    # 3) anywhere, any direction
+    d = rng.normal(size=(k, 3))
+    d /= np.linalg.norm(d, axis=1)[:, None]
+    rays["origin"][2 * k:] = rng.uniform(lo, hi, (k, 3))
+    rays["direction"][2 * k:] = d
+    return rays
+
+
+@pytest.mark.parametrize("kind,n", [("render", 10000), ("bench", 100000)])
+def test_pruning_keeps_every_hit(gpu, mirt, oracle, kind, n):
+    """Closest hits with pruning == without == the oracle's reference DFS,
+    bit for bit, on 300k hard rays (oracle on a 30k subset)."""
+    abi = mirt.abi
+    s, b = _scene(mirt, kind, n)
+    gpu.upload(s, b)
+    rays = _hard_rays(np.random.default_rng(7), s, 300_000)
+    try:
+        gpu.set_option(abi.OPT_PRUNE, 1)
+        on = gpu.ray_bvh_intersect(rays)
+        gpu.set_option(abi.OPT_PRUNE, 0)
+        off = gpu.ray_bvh_intersect(rays)
+    finally:
+        gpu.set_option(abi.OPT_PRUNE, 1)
+    assert on.tobytes() == off.tobytes()
+    assert (on["hit"] == 1).sum() > 50_000
+    s2 = mirt.create_random_spheres(n, 1) if kind == "render" else mirt.create_benchmark_spheres(n, 1)
+    t = oracle.build(s2)
+    sub = np.ascontiguousarray(rays[::10])
+    ref = oracle.intersect(t, s2, sub)
+    oracle.free(t)
+    assert on[::10].tobytes() == ref.tobytes()
 
 
 def test_phase_timing(gpu, mirt):
@@ -210,14 +280,16 @@ def test_sentinel_and_edge_scenes(gpu, mirt, oracle):
 
 
 @pytest.mark.parametrize("trav", [0, 1, 2, 3, 4, 5])
-@pytest.mark.parametrize("fast", [0, 1])
+@pytest.mark.parametrize("fast,prune", [(0, 0), (1, 0), (1, 1)])
 @pytest.mark.parametrize("defer", [0, 1])
-def test_all_schedules_bit_identical(gpu, mirt, golden, small, scene1000, trav, fast, defer):
-    """Every traversal schedule x slab-test form gives the reference's bytes:
-    per-ray hits and traces, and the 1080p 10k depth-1/depth-5 frames."""
+def test_all_schedules_bit_identical(gpu, mirt, golden, small, scene1000, trav, fast, prune, defer):
+    """Every traversal schedule x slab-test form x pruning gives the
+    reference's bytes: per-ray hits and traces, and the 1080p 10k
+    depth-1/depth-5 frames."""
     abi = mirt.abi
     gpu.set_option(abi.OPT_TRAVERSAL, trav)
     gpu.set_option(abi.OPT_FAST_SLAB, fast)
+    gpu.set_option(abi.OPT_PRUNE, prune)
     gpu.set_option(abi.OPT_DEFER, defer)
     try:
         s, b = scene1000
@@ -234,6 +306,7 @@ def test_all_schedules_bit_identical(gpu, mirt, golden, small, scene1000, trav, 
     finally:
         gpu.set_option(abi.OPT_TRAVERSAL, abi.TRAV_WAVEFRONT)
         gpu.set_option(abi.OPT_FAST_SLAB, 1)
+        gpu.set_option(abi.OPT_PRUNE, 1)
         gpu.set_option(abi.OPT_DEFER, 1)
 
 
