@@ -297,7 +297,7 @@ __global__ __launch_bounds__(256) void primary_kernel(DevScene sc, FrameConst f,
     }
 }
 
-template <bool FAST>
+template <bool FAST, bool ORD>
 __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
                                                      float* __restrict__ acc, const BounceRec* __restrict__ queue,
                                                      uint32_t* __restrict__ qctl, int threshold)
@@ -312,7 +312,8 @@ __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, 
     SlabRay sr = slab_ray(ray);
     SphRay sp = sph_ray(ray);
     Prune pr = prune_off();
-    uint32_t next = end, pixel = 0, k = 0, base0 = 0;
+    LaneWalk w = lane_walk_start(false);
+    uint32_t pixel = 0, k = 0, base0 = 0;
     int level = 0, best_s = -1;
     float best_t = INFINITY;
     uint64_t key = 0;
@@ -338,7 +339,7 @@ __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, 
                     level = 1;
                     const int r = (int)(pixel / f.width), x = (int)(pixel - r * f.width);
                     key = pixel_key(f.seed, (uint32_t)(shard_row_to_y(f, r) * f.width + x), f.sample);
-                    next = 0;
+                    w = ORD ? lane_walk_start(true) : lane_walk_dfs(end);
                     best_t = INFINITY;
                     best_s = -1;
                     pr = prune_off();
@@ -349,15 +350,15 @@ __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, 
         if (!__ballot(has)) break;
         // walk until few lanes are still walking and the others can make progress
         for (;;) {
-            const uint64_t walking = __ballot(has && next < end);
+            const uint64_t walking = __ballot(has && lane_walking(w));
             if (!walking) break;
             if (__popcll(walking) < threshold &&
-                (__ballot(has && next >= end) || (!exhausted && __ballot(!has))))
+                (__ballot(has && !lane_walking(w)) || (!exhausted && __ballot(!has))))
                 break;
-            if (has && next < end) lane_step<FAST, false>(sc, sr, sp, pr, next, best_t, best_s, cnt);
+            if (has && lane_walking(w)) ordered_lane_step<FAST, false, ORD>(sc, sr, sp, pr, w, best_t, best_s, cnt);
         }
         // shade every lane whose ray is done (renderer.c:46-77 for that level)
-        if (has && next >= end) {
+        if (has && !lane_walking(w)) {
             bool finish = true;
             uint32_t tail = 255u << 24;          // depth exhausted: black (renderer.c:23-24)
             int stored = level - 1;
@@ -375,7 +376,7 @@ __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, 
                     ray = Ray{p[0], p[1], p[2], bx, by, bz};
                     sr = slab_ray(ray);
                     sp = sph_ray(ray);
-                    next = 0;
+                    w = ORD ? lane_walk_start(true) : lane_walk_dfs(end);
                     best_t = INFINITY;
                     best_s = -1;
                     pr = prune_off();
@@ -526,6 +527,9 @@ struct mirt_ctx {
     int defer = 1;        // trace zero-component camera rays in leading waves
     int prune = 1;              // closest-hit pruning (trace.h Prune), FAST slab only
     bool prune_ok = false;      // the uploaded tree's boxes enclose their subtrees
+    PNode* d_pnodes = nullptr;  // ordered-walk layout of the tree
+    bool ordered_ok = false;    // leaves in DFS order hold increasing sphere indices, depth < 63
+    int ordered = 1;            // ordered (nearer-child-first) walks where the tree admits them
     float r_max = 0.0f, c_max = 0.0f;
     int bounce_threshold = 40;  // wavefront: shade finished rays once fewer lanes walk
     int bounce_blocks = 0;      // wavefront: persistent workgroups (set in mirt_create)
@@ -602,10 +606,67 @@ bool tree_encloses(const mirt_sphere* sp, int ns, const mirt_node* nd, int nn, f
     return true;
 }
 
+// PNode layout (trace.h) of a validated flat tree. Returns whether ordered
+// walks may use it: hit-able leaves must carry strictly increasing sphere
+// indices in DFS order (then the index is hit.c:108's tie key -- true of the
+// reference's trees, whose build partitions the array in place) and the
+// inner depth must leave the packet walk's stack (one entry per level)
+// within 64.
+bool build_pnodes(const mirt_node* nd, int nn, int ns, std::vector<PNode>& pn)
+{
+    std::vector<uint32_t> pidx((size_t)nn, kPNone);
+    uint32_t np = 1;
+    for (int i = 0; i < nn; i++)
+        if (nd[i].sphere < 0) pidx[i] = np++;
+    pn.assign(np, PNode{});
+    auto set_child = [&](PNode& p, int k, uint32_t ci) {
+        const mirt_node& n = nd[ci];
+        float* slot = k ? p.c1 : p.c0;
+        uint32_t ref = pidx[ci];
+        std::memcpy(slot, n.bmin, sizeof n.bmin);
+        std::memcpy(slot + 3, n.bmax, sizeof n.bmax);
+        if (n.skip & MIRT_NODE_EMPTY) {
+            ref = kPNone;  // a 0-sphere leaf: passes, never hits
+        } else if (n.sphere >= 0) {
+            if (n.sphere >= ns) {
+                ref = kPNone;
+            } else {
+                ref = kPLeaf | (uint32_t)n.sphere;
+            }
+        }
+        (k ? p.ref1 : p.ref0) = ref;
+    };
+    pn[0].ref0 = pn[0].ref1 = kPNone;
+    pn[0].flat = 0xffffffffu;  // flat + 1 == 0: the whole tree
+    pn[0].end = (uint32_t)nn;
+    if (nn > 0) set_child(pn[0], 0, 0);
+    bool mono = nn > 0;
+    int last = -1;
+    std::vector<uint32_t> ends;  // subtree ends of the open inner nodes
+    size_t depth = 0;
+    for (int i = 0; i < nn; i++) {
+        while (!ends.empty() && ends.back() <= (uint32_t)i) ends.pop_back();
+        if (nd[i].sphere < 0) {
+            PNode& p = pn[pidx[i]];
+            set_child(p, 0, (uint32_t)i + 1);
+            set_child(p, 1, nd[i + 1].skip & MIRT_SKIP_MASK);
+            p.flat = (uint32_t)i;
+            p.end = nd[i].skip & MIRT_SKIP_MASK;
+            ends.push_back(nd[i].skip & MIRT_SKIP_MASK);
+            depth = std::max(depth, ends.size());
+        } else if (!(nd[i].skip & MIRT_NODE_EMPTY) && nd[i].sphere < ns) {
+            if (nd[i].sphere <= last) mono = false;
+            last = nd[i].sphere;
+        }
+    }
+    return mono && depth + 2 <= 64;
+}
+
 DevScene dev_scene(const mirt_ctx* c)
 {
+    const bool prune = c->prune && c->prune_ok;
     return DevScene{c->d_nodes, c->d_nodes32, c->d_geo, c->d_color, (uint32_t)c->num_nodes, c->num_spheres,
-                    c->prune && c->prune_ok, c->r_max, c->c_max};
+                    prune, c->r_max, c->c_max, c->d_pnodes, prune && c->ordered && c->ordered_ok && c->fast_slab};
 }
 
 bool ctx_ok(mirt_ctx* c, bool need_scene, const char* fn)
@@ -688,10 +749,15 @@ int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_ac
             primary_kernel<false><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ph1, s));
-        if (c->fast_slab)
-            bounce_kernel<true><<<c->bounce_blocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold);
+        if (c->fast_slab && sc.ordered)
+            bounce_kernel<true, true><<<c->bounce_blocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
+                                                                     c->bounce_threshold);
+        else if (c->fast_slab)
+            bounce_kernel<true, false><<<c->bounce_blocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
+                                                                      c->bounce_threshold);
         else
-            bounce_kernel<false><<<c->bounce_blocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold);
+            bounce_kernel<false, false><<<c->bounce_blocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
+                                                                       c->bounce_threshold);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ph2, s));
         if (timed) HIP_TRY(hipEventRecord(c->ev1, s));
@@ -734,7 +800,7 @@ int mirt_create(int device, mirt_ctx** out)
         int cus = 0, per_cu = 0;
         e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
         if (e == hipSuccess)
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bounce_kernel<true>, 256, 0);
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bounce_kernel<true, true>, 256, 0);
         c->bounce_blocks = std::max(1, cus) * std::max(1, per_cu);
     }
     if (e != hipSuccess) {
@@ -751,7 +817,7 @@ void mirt_destroy(mirt_ctx* c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : {(void*)c->d_nodes, (void*)c->d_nodes32, (void*)c->d_geo, (void*)c->d_color, (void*)c->d_out, (void*)c->d_acc,
-                    c->d_in, c->d_res, (void*)c->d_counts, (void*)c->d_defer, c->d_queue})
+                    c->d_in, c->d_res, (void*)c->d_counts, (void*)c->d_defer, c->d_queue, (void*)c->d_pnodes})
         if (p) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -792,8 +858,9 @@ int mirt_scene_upload_flat(mirt_ctx* c, const mirt_sphere* spheres, int ns, cons
     }
     geo[ns] = make_float4(NAN, NAN, NAN, NAN);  // &spheres[N] sentinel: never hits
     col[ns] = 0xff000000u;
-    for (void* p : {(void*)c->d_nodes, (void*)c->d_nodes32, (void*)c->d_geo, (void*)c->d_color})
+    for (void* p : {(void*)c->d_nodes, (void*)c->d_nodes32, (void*)c->d_geo, (void*)c->d_color, (void*)c->d_pnodes})
         if (p) (void)hipFree(p);
+    c->d_pnodes = nullptr;
     c->d_nodes = nullptr;
     c->d_nodes32 = nullptr;
     c->d_geo = nullptr;
@@ -818,8 +885,13 @@ int mirt_scene_upload_flat(mirt_ctx* c, const mirt_sphere* spheres, int ns, cons
     if (nn > 0) HIP_TRY(hipMemcpy(c->d_nodes32, nodes, sizeof(mirt_node) * (size_t)nn, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_geo, geo.data(), sizeof(float4) * geo.size(), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_color, col.data(), sizeof(uint32_t) * col.size(), hipMemcpyHostToDevice));
+    std::vector<PNode> pn;
+    const bool ordered = build_pnodes(nodes, nn, ns, pn);
+    HIP_TRY(hipMalloc((void**)&c->d_pnodes, sizeof(PNode) * pn.size()));
+    HIP_TRY(hipMemcpy(c->d_pnodes, pn.data(), sizeof(PNode) * pn.size(), hipMemcpyHostToDevice));
     c->num_nodes = nn;
     c->num_spheres = ns;
+    c->ordered_ok = ordered;
     c->prune_ok = encloses;
     c->r_max = r_max;
     c->c_max = c_max;
@@ -1114,6 +1186,9 @@ int mirt_set_option(mirt_ctx* c, int option, int value)
     case MIRT_OPT_PRUNE:
         c->prune = value != 0;
         return MIRT_OK;
+    case MIRT_OPT_ORDERED:
+        c->ordered = value != 0;
+        return MIRT_OK;
     case MIRT_OPT_BLOCK_WAVES:
         if (value != 1 && value != 2 && value != 4 && value != 8) break;
         c->block_waves = value;
@@ -1134,6 +1209,7 @@ int mirt_get_option(mirt_ctx* c, int option)
     if (option == MIRT_OPT_DEFER) return c->defer;
     if (option == MIRT_OPT_BOUNCE_THRESHOLD) return c->bounce_threshold;
     if (option == MIRT_OPT_PRUNE) return c->prune;
+    if (option == MIRT_OPT_ORDERED) return c->ordered;
     set_error("mirt_get_option: bad option %d", option);
     return MIRT_E_INVALID;
 }

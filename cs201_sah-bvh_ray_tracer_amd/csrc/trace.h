@@ -35,6 +35,29 @@ struct __attribute__((aligned(64))) DNode {
 };
 static_assert(sizeof(DNode) == 64, "device node is 64 B");
 
+// The same tree re-laid for ordered walks: one node per inner node of the
+// reference tree holding BOTH children, so one load tests both and the walk
+// can enter the nearer child first. PNode 0 is a virtual parent whose only
+// child is the root. A child reference is an inner PNode index, kPLeaf |
+// sphere index (a leaf that can hit), or kPNone (no child that can ever hit:
+// a 0-sphere leaf or the &spheres[N] sentinel of hit.c). A child slot holds
+// the child's box (lo.xyz, hi.xyz) -- for a leaf that is the box of the
+// node's whole sphere range, not of its one sphere (a depth-40 leaf keeps
+// the range's bounds but tests only node->sphere, bvh.c:122-136), so the
+// sphere itself is fetched when the box passes.
+// `flat` and `end` locate the node in the flat pre-order tree, [flat + 1,
+// end) being its children's subtrees, which a walk can take in DFS order
+// without a stack.
+constexpr uint32_t kPLeaf = 0x80000000u;
+constexpr uint32_t kPNone = 0xffffffffu;
+struct __attribute__((aligned(64))) PNode {
+    float c0[6];
+    float c1[6];
+    uint32_t ref0, ref1;
+    uint32_t flat, end;
+};
+static_assert(sizeof(PNode) == 64, "ordered node is 64 B");
+
 // Read-only scene in HBM (L2 / Infinity-Cache resident at the BASELINE sizes).
 struct DevScene {
     const DNode* nodes;     // 64 B, leaf sphere inline: scalar (wave-uniform) walks
@@ -48,6 +71,11 @@ struct DevScene {
     int prune;
     float r_max;   // largest sphere radius
     float c_max;   // largest |centre|_inf + radius
+    // ordered walks (PNode): set when leaves hold increasing sphere indices
+    // in DFS order (so the index is the DFS tie key) and the tree is shallow
+    // enough for the 64-entry walk stack
+    const PNode* pnodes;
+    int ordered;
 };
 
 struct Ray {
@@ -245,7 +273,7 @@ __device__ __forceinline__ void prune_update(Prune& p, const DevScene& sc, float
 // component take slab_test (`generic`), whose +-inf handling is exact.
 // A box beyond the pruning limit (Prune) fails before any of this.
 __device__ __forceinline__ bool slab_fast(const SlabRay& r, const Prune& p, float x0, float y0, float z0, float x1,
-                                          float y1, float z1)
+                                          float y1, float z1, float& near)
 {
     const float tx1 = (x0 - r.ox) * r.ix, tx2 = (x1 - r.ox) * r.ix;
     const float ty1 = (y0 - r.oy) * r.iy, ty2 = (y1 - r.oy) * r.iy;
@@ -256,6 +284,7 @@ __device__ __forceinline__ bool slab_fast(const SlabRay& r, const Prune& p, floa
                               fmaxf(fmaf(ny, c, -(p.m * fabsf(r.iy))), fmaf(nz, c, -(p.m * fabsf(r.iz)))));
     if (entry > p.lim) return false;
     const float tmin = fmaxf(nx, fmaxf(ny, nz));
+    near = tmin;
     const float tmax = fminf(fmaxf(tx1, tx2), fminf(fmaxf(ty1, ty2), fmaxf(tz1, tz2)));
     const float m = (fabsf(tmin) + fabsf(tmax)) * 0x1p-20f;
     const float gap = tmax - tmin, above = tmax - kEps;
@@ -264,11 +293,41 @@ __device__ __forceinline__ bool slab_fast(const SlabRay& r, const Prune& p, floa
     return slab_test(r, x0, y0, z0, x1, y1, z1);
 }
 
+// The Prune test for any ray, including those slab_fast leaves to slab_test:
+// an axis whose direction component is zero or tiny (|d| < 2^-40) is left
+// out of the max, which only lowers the entry bound; the other axes use the
+// same normal-range reciprocals and margins as slab_fast.
+__device__ __forceinline__ bool pruned_any(const SlabRay& r, const Prune& p, const NodeV& n)
+{
+    constexpr float c = 1.0f - 0x1p-20f;
+    const float tiny = 0x1p-40f;
+    float e = -INFINITY;
+    if (fabsf(r.dx) >= tiny)
+        e = fmaxf(e, fmaf(fminf((n.b0 - r.ox) * r.ix, (n.b3 - r.ox) * r.ix), c, -(p.m * fabsf(r.ix))));
+    if (fabsf(r.dy) >= tiny)
+        e = fmaxf(e, fmaf(fminf((n.b1 - r.oy) * r.iy, (n.b4 - r.oy) * r.iy), c, -(p.m * fabsf(r.iy))));
+    if (fabsf(r.dz) >= tiny)
+        e = fmaxf(e, fmaf(fminf((n.b2 - r.oz) * r.iz, (n.b5 - r.oz) * r.iz), c, -(p.m * fabsf(r.iz))));
+    return e > p.lim;
+}
+
 template <bool FAST>
 __device__ __forceinline__ bool slab(const SlabRay& r, const Prune& p, const NodeV& n)
 {
-    if (FAST && !r.generic) return slab_fast(r, p, n.b0, n.b1, n.b2, n.b3, n.b4, n.b5);
+    float near;
+    if (FAST && !r.generic) return slab_fast(r, p, n.b0, n.b1, n.b2, n.b3, n.b4, n.b5, near);
     return slab_test(r, n.b0, n.b1, n.b2, n.b3, n.b4, n.b5);
+}
+
+// The slab predicate of one box plus an entry estimate for ordering the
+// walk (any value is correct there; only the visiting order changes).
+template <bool FAST>
+__device__ __forceinline__ bool slab_box(const SlabRay& r, const Prune& p, float x0, float y0, float z0, float x1,
+                                         float y1, float z1, float& near)
+{
+    if (FAST && !r.generic) return slab_fast(r, p, x0, y0, z0, x1, y1, z1, near);
+    near = 0.0f;
+    return slab_test(r, x0, y0, z0, x1, y1, z1);
 }
 
 // Per-ray constants of ray_sphere_intersect: a = d.d, 4a and 2a (hit.c:22-28).
@@ -456,7 +515,9 @@ __device__ __forceinline__ void closest_bvh(const DevScene& sc, const Ray& ray, 
 // One step of the per-lane walk with on-demand loads (the body of
 // closest_bvh's LANE_NP loop), for kernels that interleave walking with
 // other per-lane work.
-template <bool FAST, bool COUNT>
+// TIEKEY: inside an ordered walk the best so far may come from a later DFS
+// leaf, so a tie replaces it only for a larger sphere index (the DFS key).
+template <bool FAST, bool COUNT, bool TIEKEY = false>
 __device__ __forceinline__ void lane_step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
                                           uint32_t& next, float& best_t, int& best_s, Counters& cnt)
 {
@@ -475,7 +536,7 @@ __device__ __forceinline__ void lane_step(const DevScene& sc, const SlabRay& sr,
         if (pass) {
             if (COUNT) cnt.spheres++;
             const float t = sphere_t<FAST>(sp, sc.geo[nd.sphere], best_t);
-            if (t > 0.0f) {
+            if (t > 0.0f && (!TIEKEY || t < best_t || nd.sphere > best_s)) {
                 best_t = t;
                 best_s = nd.sphere;
                 if (sc.prune) prune_update(pr, sc, sr.ox, sr.oy, sr.oz, sp.a4, t);
@@ -516,6 +577,7 @@ __device__ __forceinline__ void closest_bvh_chunked(const DevScene& sc, const Ra
     uint32_t cur = 0;
     float bt = INFINITY;
     int bs = -1;
+    Prune pr = prune_off();  // wave-uniform: one ray
     while (cur < end) {
         if (COUNT) cnt.steps++;
         const uint32_t base = cur;
@@ -529,7 +591,9 @@ __device__ __forceinline__ void closest_bvh_chunked(const DevScene& sc, const Ra
             skip = nd.skip & MIRT_SKIP_MASK;
             leaf = nd.sphere >= 0;
             sph = nd.sphere;
-            pass = (nd.skip & MIRT_NODE_EMPTY) || slab<FAST>(sr, prune_off(), nd);
+            // pruned against the best at the chunk's start: a box beyond it
+            // is beyond every later best too
+            pass = (nd.skip & MIRT_NODE_EMPTY) || (!(FAST && pruned_any(sr, pr, nd)) && slab<FAST>(sr, prune_off(), nd));
             if (pass && leaf) t = sphere_t<FAST>(sp, nd.g, bt);
         }
         const uint64_t descend = __ballot(pass && !leaf);
@@ -557,6 +621,7 @@ __device__ __forceinline__ void closest_bvh_chunked(const DevScene& sc, const Ra
             const int last = 63 - __builtin_clzll(eq);
             bt = tmin;
             bs = __builtin_amdgcn_readlane(sph, last);
+            if (FAST && sc.prune) prune_update(pr, sc, ray.ox, ray.oy, ray.oz, sp.a4, bt);
         }
         const uint64_t passed_leaves = __ballot(pass && leaf);
         if (COUNT) {  // uniform values: every lane holds the ray's totals
@@ -573,15 +638,271 @@ __device__ __forceinline__ float readlane_f(float v, int l)
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
+struct PNodeV {
+    float a0, a1, a2, a3, a4, a5;  // child 0 slot
+    float b0, b1, b2, b3, b4, b5;  // child 1 slot
+    uint32_t r0, r1, flat, end;
+};
+
+__device__ __forceinline__ PNodeV load_pnode_uniform(const PNode* base, uint32_t i)
+{
+    const cu32_t* p = (const cu32_t*)base + 16u * i;
+    PNodeV n;
+    n.a0 = __uint_as_float(p[0]);
+    n.a1 = __uint_as_float(p[1]);
+    n.a2 = __uint_as_float(p[2]);
+    n.a3 = __uint_as_float(p[3]);
+    n.a4 = __uint_as_float(p[4]);
+    n.a5 = __uint_as_float(p[5]);
+    n.b0 = __uint_as_float(p[6]);
+    n.b1 = __uint_as_float(p[7]);
+    n.b2 = __uint_as_float(p[8]);
+    n.b3 = __uint_as_float(p[9]);
+    n.b4 = __uint_as_float(p[10]);
+    n.b5 = __uint_as_float(p[11]);
+    n.r0 = p[12];
+    n.r1 = p[13];
+    n.flat = p[14];
+    n.end = p[15];
+    return n;
+}
+
+__device__ __forceinline__ PNodeV load_pnode_lane(const PNode* base, uint32_t i)
+{
+    const float4* p = (const float4*)(base + i);
+    const float4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+    PNodeV n;
+    n.a0 = q0.x;
+    n.a1 = q0.y;
+    n.a2 = q0.z;
+    n.a3 = q0.w;
+    n.a4 = q1.x;
+    n.a5 = q1.y;
+    n.b0 = q1.z;
+    n.b1 = q1.w;
+    n.b2 = q2.x;
+    n.b3 = q2.y;
+    n.b4 = q2.z;
+    n.b5 = q2.w;
+    n.r0 = __float_as_uint(q3.x);
+    n.r1 = __float_as_uint(q3.y);
+    n.flat = __float_as_uint(q3.z);
+    n.end = __float_as_uint(q3.w);
+    return n;
+}
+
+__device__ __forceinline__ bool pref_leaf(uint32_t r) { return r != kPNone && (r & kPLeaf); }
+__device__ __forceinline__ bool pref_inner(uint32_t r) { return !(r & kPLeaf); }
+
+// A leaf's sphere (hit.c:94-99) as a candidate of an ORDERED walk: the
+// closest hit is the least t, a tie going to the later DFS leaf (hit.c:108),
+// which is the larger sphere index for the trees `DevScene::ordered` admits
+// -- so the result does not depend on the visiting order.
+template <bool FAST>
+__device__ __forceinline__ void consider_sphere(const DevScene& sc, const SphRay& sp, Prune& pr, float ox, float oy,
+                                                float oz, int si, float4 g, float& best_t, int& best_s)
+{
+    const float t = sphere_t<FAST>(sp, g, best_t);
+    if (t > 0.0f && (t < best_t || si > best_s)) {
+        best_t = t;
+        best_s = si;
+        if (sc.prune) prune_update(pr, sc, ox, oy, oz, sp.a4, t);
+    }
+}
+
+// One child slot of a PNode for one lane: a leaf's box then its sphere; an
+// inner child's box. Returns whether the walk should enter the child (inner
+// and passed), with its entry estimate.
+template <bool FAST, bool COUNT>
+__device__ __forceinline__ bool visit_child(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
+                                            uint32_t ref, float s0, float s1, float s2, float s3, float s4, float s5,
+                                            float& near, float& best_t, int& best_s, Counters& cnt)
+{
+    if (ref == kPNone) return false;
+    if (ref & kPLeaf) {
+        if (COUNT) cnt.nodes++;
+        if (slab_box<FAST>(sr, pr, s0, s1, s2, s3, s4, s5, near)) {
+            if (COUNT) cnt.spheres++;
+            const int si = (int)(ref & ~kPLeaf);
+            consider_sphere<FAST>(sc, sp, pr, sr.ox, sr.oy, sr.oz, si, sc.geo[si], best_t, best_s);
+        }
+        return false;
+    }
+    if (COUNT) cnt.nodes++;
+    return slab_box<FAST>(sr, pr, s0, s1, s2, s3, s4, s5, near);
+}
+
+// Ordered closest hit of a wave of rays walked as one packet (camera rays),
+// over PNodes with scalar loads. `mask` holds the lanes that passed every
+// box on the path to the current node, so a lane tests a child only when
+// hit.c:91-109 would (the reference gates each subtree by all its
+// ancestors' boxes); a node's two children are tested together, leaf
+// children's spheres at once, and the walk enters the child that the lanes
+// passing both see nearer (a vote), pushing the other (node, lane mask) on
+// a stack kept one entry per lane (entry k in lane k). Pruning (Prune)
+// drops boxes beyond each lane's best hit. Stack depth <= tree depth + 1 <=
+// 64 (checked at upload).
+template <bool FAST, bool COUNT>
+__device__ __forceinline__ void closest_packet_ordered(const DevScene& sc, const Ray& ray, bool active, float& best_t,
+                                                       int& best_s, Counters& cnt)
+{
+    const SlabRay sr = slab_ray(ray);
+    const SphRay sp = sph_ray(ray);
+    Prune pr = prune_off();
+    best_t = INFINITY;
+    best_s = -1;
+    const uint32_t lane = threadIdx.x & 63;
+    uint64_t mask = __ballot(active);
+    uint32_t cur = 0;
+    uint32_t top = 0;
+    uint32_t st_node = 0, st_lo = 0, st_hi = 0;
+    while (mask) {
+        if (COUNT) cnt.steps++;
+        const PNodeV nd = load_pnode_uniform(sc.pnodes, cur);
+        const bool in = (mask >> lane) & 1;
+        float e0 = 0.0f, e1 = 0.0f;
+        bool h0 = false, h1 = false;
+        if (in) {
+            h0 = visit_child<FAST, COUNT>(sc, sr, sp, pr, nd.r0, nd.a0, nd.a1, nd.a2, nd.a3, nd.a4, nd.a5, e0, best_t,
+                                          best_s, cnt);
+            h1 = visit_child<FAST, COUNT>(sc, sr, sp, pr, nd.r1, nd.b0, nd.b1, nd.b2, nd.b3, nd.b4, nd.b5, e1, best_t,
+                                          best_s, cnt);
+        }
+        const uint64_t m0 = __ballot(h0), m1 = __ballot(h1);
+        if (m0 && m1) {
+            const uint64_t both = m0 & m1;
+            const uint64_t v = __ballot(((both >> lane) & 1) && e1 < e0);
+            const bool swap = 2 * __popcll(v) > __popcll(both);
+            const uint32_t second = swap ? nd.r0 : nd.r1;
+            const uint64_t sm = swap ? m0 : m1;
+            if (lane == top) {
+                st_node = second;
+                st_lo = (uint32_t)sm;
+                st_hi = (uint32_t)(sm >> 32);
+            }
+            top++;
+            cur = swap ? nd.r1 : nd.r0;
+            mask = swap ? m1 : m0;
+        } else if (m0 | m1) {
+            cur = m0 ? nd.r0 : nd.r1;
+            mask = m0 | m1;
+        } else if (top > 0) {
+            top--;
+            cur = (uint32_t)__builtin_amdgcn_readlane(st_node, top);
+            // readlane returns int: zero-extend both halves
+            mask = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(st_hi, top) << 32) |
+                   (uint64_t)(uint32_t)__builtin_amdgcn_readlane(st_lo, top);
+        } else {
+            break;
+        }
+    }
+}
+
+// Per-lane ordered walk state (bounce rays): `cur` is the PNode to visit
+// (kPNone: done), or, while `end` != 0, the next flat node of a DFS segment
+// that ends at `end`. The far children still to visit sit in a 4-entry
+// shift-register stack; when it is full and both children pass, the node's
+// children are walked as the flat DFS segment [flat + 1, end) instead (the
+// reference order, pruned, no stack) -- ordering matters most near the root
+// (a 4-entry stack keeps all but ~1% of its gain on the 10k scene).
+constexpr int kLaneStack = 4;
+struct LaneWalk {
+    uint32_t cur, end;
+    uint32_t top;
+    uint32_t s0, s1, s2, s3;
+};
+
+__device__ __forceinline__ LaneWalk lane_walk_start(bool active)
+{
+    return LaneWalk{active ? 0u : kPNone, 0u, 0u, 0u, 0u, 0u, 0u};
+}
+
+__device__ __forceinline__ bool lane_walking(const LaneWalk& w) { return w.cur != kPNone; }
+
+__device__ __forceinline__ void lane_walk_pop(LaneWalk& w)
+{
+    if (w.top == 0) {
+        w.cur = kPNone;
+        return;
+    }
+    w.cur = w.s0;
+    w.s0 = w.s1;
+    w.s1 = w.s2;
+    w.s2 = w.s3;
+    w.top--;
+}
+
+// ORD = false: the walk is one DFS segment over the whole tree (the
+// reference order, hit.c's tie rule `t <= best`), started by lane_walk_dfs.
+__device__ __forceinline__ LaneWalk lane_walk_dfs(uint32_t num_nodes)
+{
+    return LaneWalk{0u, num_nodes, 0u, 0u, 0u, 0u, 0u};
+}
+
+template <bool FAST, bool COUNT, bool ORD = true>
+__device__ __forceinline__ void ordered_lane_step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
+                                                  LaneWalk& w, float& best_t, int& best_s, Counters& cnt)
+{
+    if (COUNT) cnt.steps++;
+    if (!ORD || w.end) {
+        lane_step<FAST, COUNT, ORD>(sc, sr, sp, pr, w.cur, best_t, best_s, cnt);
+        if (w.cur >= w.end) {
+            w.end = 0;
+            lane_walk_pop(w);
+        }
+        return;
+    }
+    const PNodeV nd = load_pnode_lane(sc.pnodes, w.cur);
+    float e0 = 0.0f, e1 = 0.0f;
+    const bool h0 = visit_child<FAST, COUNT>(sc, sr, sp, pr, nd.r0, nd.a0, nd.a1, nd.a2, nd.a3, nd.a4, nd.a5, e0,
+                                             best_t, best_s, cnt);
+    const bool h1 = visit_child<FAST, COUNT>(sc, sr, sp, pr, nd.r1, nd.b0, nd.b1, nd.b2, nd.b3, nd.b4, nd.b5, e1,
+                                             best_t, best_s, cnt);
+    if (h0 && h1) {
+        if (w.top < kLaneStack) {
+            const bool swap = e1 < e0;
+            w.s3 = w.s2;
+            w.s2 = w.s1;
+            w.s1 = w.s0;
+            w.s0 = swap ? nd.r0 : nd.r1;
+            w.top++;
+            w.cur = swap ? nd.r1 : nd.r0;
+        } else {
+            w.cur = nd.flat + 1;
+            w.end = nd.end;
+        }
+    } else if (h0) {
+        w.cur = nd.r0;
+    } else if (h1) {
+        w.cur = nd.r1;
+    } else {
+        lane_walk_pop(w);
+    }
+}
+
 // Closest hit for every active lane: degenerate rays (a zero or tiny
 // direction component, `SlabRay::generic`) one at a time with the whole
-// wave (closest_bvh_chunked), the rest with the lane-parallel walk.
+// wave (closest_bvh_chunked), the rest with the lane-parallel walk (or the
+// ordered packet walk, for UNIFORM on a tree that admits it).
 template <bool UNIFORM, bool FAST, bool COUNT, bool LPF = true>
 __device__ __forceinline__ void closest_hit(const DevScene& sc, const Ray& ray, bool active, float& best_t,
                                             int& best_s, Counters& cnt)
 {
     const bool gen = active && slab_ray(ray).generic;
-    closest_bvh<UNIFORM, FAST, COUNT, LPF>(sc, ray, active && !gen, best_t, best_s, cnt);
+    if (UNIFORM && FAST && sc.ordered) {
+        closest_packet_ordered<FAST, COUNT>(sc, ray, active && !gen, best_t, best_s, cnt);
+    } else if (!UNIFORM && FAST && sc.ordered) {
+        const SlabRay sr = slab_ray(ray);
+        const SphRay sp = sph_ray(ray);
+        Prune pr = prune_off();
+        best_t = INFINITY;
+        best_s = -1;
+        LaneWalk w = lane_walk_start(active && !gen);
+        while (__ballot(lane_walking(w)))
+            if (lane_walking(w)) ordered_lane_step<FAST, COUNT>(sc, sr, sp, pr, w, best_t, best_s, cnt);
+    } else {
+        closest_bvh<UNIFORM, FAST, COUNT, LPF>(sc, ray, active && !gen, best_t, best_s, cnt);
+    }
     uint64_t gm = __ballot(gen);
     const int lane = threadIdx.x & 63;
     while (gm) {

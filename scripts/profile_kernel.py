@@ -2,7 +2,7 @@
 reference-DFS work and SIMD efficiency of every schedule.
 
     python scripts/profile_kernel.py --counts                 # work + efficiency table
-    python scripts/profile_kernel.py --trav 2 --fast 1 --depth 5 --frames 5   # frames to profile
+    python scripts/profile_kernel.py --trav 2 --fast 1 --depth 5 --frames 5 [--opt 7=0]  # frames to profile
 """
 import argparse
 import importlib
@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--depth", type=int, default=5)
     ap.add_argument("--frames", type=int, default=3)
     ap.add_argument("--counts", action="store_true")
+    ap.add_argument("--opt", action="append", default=[], help="OPTION=VALUE (mirt_set_option), repeatable")
     a = ap.parse_args()
     kind = "render" if a.scene.startswith("render") else "bench"
     n = int(a.scene[len(kind):])
@@ -46,6 +47,9 @@ def main():
         return
     r.set_option(abi.OPT_TRAVERSAL, a.trav)
     r.set_option(abi.OPT_FAST_SLAB, a.fast)
+    for kv in a.opt:
+        k, v = kv.split("=")
+        r.set_option(int(k), int(v))
     for _ in range(a.frames):
         r.render_frame(cam, a.W, a.H, depth=a.depth)
         print(json.dumps({"trav": a.trav, "fast": a.fast, "depth": a.depth, "kernel_ms": round(r.last_kernel_ms, 3)}))

@@ -5,7 +5,7 @@
  * conservative pruning bound ever change a result?
  *
  *   gcc -O2 -ffp-contract=off -fopenmp scripts/prune_study.c -lm -o /tmp/prune_study
- *   /tmp/prune_study [W H nspheres depth]
+ *   /tmp/prune_study [W H nspheres depth rel stack_cap]
  *
  * Walks compared per ray, on the same paths (bounce rays follow the
  * reference's hit, RNG contract mode 1):
@@ -107,6 +107,8 @@ static void pdfs(const mirt_ray *r, const ONode *nd, const mirt_sphere *s, int n
     pdfs(r, nd->kid[1], s, ns, b, cnt);
 }
 
+static int g_stack_cap = 128;   /* near-first stack entries; when full, the node's children are walked in DFS order */
+
 static void nearfirst(const mirt_ray *r, const ONode *root, const mirt_sphere *s, int ns, Best *b, OCount *cnt)
 {
     const ONode *stack[128];
@@ -122,13 +124,21 @@ static void nearfirst(const mirt_ray *r, const ONode *root, const mirt_sphere *s
             if (cnt) cnt->nodes += 2;
             int h0 = o_slab(r, &k0->box) && !prunable(r, k0, b);
             int h1 = o_slab(r, &k1->box) && !prunable(r, k1, b);
-            if (h0 && h1) {
+            if (h0 && h1 && sp >= g_stack_cap) {
+                /* no room: both subtrees in the reference order, pruned, no stack */
+                if (k0->first >= 0) consider_leaf(r, k0, s, ns, b, cnt);
+                else { pdfs(r, k0->kid[0], s, ns, b, cnt); pdfs(r, k0->kid[1], s, ns, b, cnt); }
+                if (!prunable(r, k1, b)) {
+                    if (k1->first >= 0) consider_leaf(r, k1, s, ns, b, cnt);
+                    else { pdfs(r, k1->kid[0], s, ns, b, cnt); pdfs(r, k1->kid[1], s, ns, b, cnt); }
+                }
+            } else if (h0 && h1) {
                 double e0 = entry_lb(r, &k0->box, 0), e1 = entry_lb(r, &k1->box, 0);
                 if (e1 < e0) { stack[sp++] = k0; nd = k1; } else { stack[sp++] = k1; nd = k0; }
                 continue;
             }
-            if (h0) { nd = k0; continue; }
-            if (h1) { nd = k1; continue; }
+            else if (h0) { nd = k0; continue; }
+            else if (h1) { nd = k1; continue; }
         }
         for (;;) {
             if (!sp) return;
@@ -143,6 +153,7 @@ int main(int argc, char **argv)
     int W = argc > 1 ? atoi(argv[1]) : 480, H = argc > 2 ? atoi(argv[2]) : 270;
     int N = argc > 3 ? atoi(argv[3]) : 10000, depth = argc > 4 ? atoi(argv[4]) : 5;
     if (argc > 5) g_rel = atof(argv[5]);
+    if (argc > 6) g_stack_cap = atoi(argv[6]);
     mirt_sphere *s = malloc(sizeof(mirt_sphere) * (N + 1));
     o_gen_render_scene(1, N, s);
     ONode *root = o_build(s, 0, N, 0);

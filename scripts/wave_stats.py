@@ -2,7 +2,7 @@
 throughput or by its slowest 8x8 tiles? Saves the raw table to
 gpurun_out/wave_stats_<depth>.npy and prints a summary.
 
-    python scripts/wave_stats.py
+    python scripts/wave_stats.py [depth,trav,ordered ...]
 """
 import importlib
 import json
@@ -54,12 +54,16 @@ def main():
     r.upload(s, b)
     cam = mirt.default_camera()
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    for depth, trav in [(1, abi.TRAV_UNIFORM), (5, abi.TRAV_HYBRID)]:
+    configs = [(1, abi.TRAV_UNIFORM, 0), (1, abi.TRAV_UNIFORM, 1)]
+    if len(sys.argv) > 1:   # depth,trav,ordered ...
+        configs = [tuple(int(v) for v in a.split(",")) for a in sys.argv[1:]]
+    for depth, trav, ordered in configs:
         r.set_option(abi.OPT_TRAVERSAL, trav)
+        r.set_option(abi.OPT_ORDERED, ordered)
         r.wave_stats(cam, 1920, 1080, depth=depth)           # warm
         st = r.wave_stats(cam, 1920, 1080, depth=depth)
-        np.save(os.path.join(ROOT, "gpurun_out", f"wave_stats_d{depth}.npy"), st)
-        summarize(st, 1920, 1080, f"1080p 10k depth {depth} trav {trav}")
+        np.save(os.path.join(ROOT, "gpurun_out", f"wave_stats_d{depth}_t{trav}_o{ordered}.npy"), st)
+        summarize(st, 1920, 1080, f"1080p 10k depth {depth} trav {trav} ordered {ordered}")
     r.close()
 
 

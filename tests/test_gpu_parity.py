@@ -225,12 +225,16 @@ def test_pruning_keeps_every_hit(gpu, mirt, oracle, kind, n):
     rays = _hard_rays(np.random.default_rng(7), s, 300_000)
     try:
         gpu.set_option(abi.OPT_PRUNE, 1)
-        on = gpu.ray_bvh_intersect(rays)
+        on = gpu.ray_bvh_intersect(rays)                  # ordered packet walk
+        gpu.set_option(abi.OPT_ORDERED, 0)
+        dfs = gpu.ray_bvh_intersect(rays)                 # pruned, DFS order
         gpu.set_option(abi.OPT_PRUNE, 0)
-        off = gpu.ray_bvh_intersect(rays)
+        off = gpu.ray_bvh_intersect(rays)                 # the reference's walk
     finally:
         gpu.set_option(abi.OPT_PRUNE, 1)
+        gpu.set_option(abi.OPT_ORDERED, 1)
     assert on.tobytes() == off.tobytes()
+    assert dfs.tobytes() == off.tobytes()
     assert (on["hit"] == 1).sum() > 50_000
     s2 = mirt.create_random_spheres(n, 1) if kind == "render" else mirt.create_benchmark_spheres(n, 1)
     t = oracle.build(s2)
@@ -280,9 +284,9 @@ def test_sentinel_and_edge_scenes(gpu, mirt, oracle):
 
 
 @pytest.mark.parametrize("trav", [0, 1, 2, 3, 4, 5])
-@pytest.mark.parametrize("fast,prune", [(0, 0), (1, 0), (1, 1)])
+@pytest.mark.parametrize("fast,prune,ordered", [(0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 1, 1)])
 @pytest.mark.parametrize("defer", [0, 1])
-def test_all_schedules_bit_identical(gpu, mirt, golden, small, scene1000, trav, fast, prune, defer):
+def test_all_schedules_bit_identical(gpu, mirt, golden, small, scene1000, trav, fast, prune, ordered, defer):
     """Every traversal schedule x slab-test form x pruning gives the
     reference's bytes: per-ray hits and traces, and the 1080p 10k
     depth-1/depth-5 frames."""
@@ -290,6 +294,7 @@ def test_all_schedules_bit_identical(gpu, mirt, golden, small, scene1000, trav, 
     gpu.set_option(abi.OPT_TRAVERSAL, trav)
     gpu.set_option(abi.OPT_FAST_SLAB, fast)
     gpu.set_option(abi.OPT_PRUNE, prune)
+    gpu.set_option(abi.OPT_ORDERED, ordered)
     gpu.set_option(abi.OPT_DEFER, defer)
     try:
         s, b = scene1000
@@ -307,6 +312,7 @@ def test_all_schedules_bit_identical(gpu, mirt, golden, small, scene1000, trav, 
         gpu.set_option(abi.OPT_TRAVERSAL, abi.TRAV_WAVEFRONT)
         gpu.set_option(abi.OPT_FAST_SLAB, 1)
         gpu.set_option(abi.OPT_PRUNE, 1)
+        gpu.set_option(abi.OPT_ORDERED, 1)
         gpu.set_option(abi.OPT_DEFER, 1)
 
 
@@ -321,3 +327,54 @@ def test_errors_are_loud(gpu, mirt):
     bad[0] = ([0] * 3, [1] * 3, -1, 7)                          # skip out of range
     with pytest.raises(mirt.MirtError):
         gpu.upload(np.zeros(1, mirt.abi.SPHERE), mirt.Bvh(bad))
+
+
+def test_ties_go_to_the_later_leaf(gpu, mirt, oracle):
+    """Duplicate spheres tie exactly on t; hit.c:108 keeps the later DFS leaf.
+    The ordered walk (nearer child first) must pick the same one."""
+    abi = mirt.abi
+    base = mirt.create_random_spheres(2000, 5)
+    dup = base[:600].copy()
+    dup["color"][:, 0] ^= 0x55                    # tell the copies apart
+    s = np.concatenate([base, dup])
+    s2 = s.copy()
+    b = mirt.build_bvh(s)
+    gpu.upload(s, b)
+    rays = _hard_rays(np.random.default_rng(11), s, 60_000)
+    try:
+        on = gpu.ray_bvh_intersect(rays)
+        gpu.set_option(abi.OPT_PRUNE, 0)
+        off = gpu.ray_bvh_intersect(rays)
+    finally:
+        gpu.set_option(abi.OPT_PRUNE, 1)
+    t = oracle.build(s2)
+    ref = oracle.intersect(t, s2, rays)
+    oracle.free(t)
+    assert on.tobytes() == ref.tobytes()
+    assert off.tobytes() == ref.tobytes()
+    hit = on["hit"] == 1
+    assert hit.sum() > 10_000
+
+
+def test_ordered_walk_stays_within_its_lanes(gpu, mirt):
+    """The ordered packet walk may only carry lanes that passed every box on
+    the path. A lane-mask leak lets inactive lanes (e.g. the deferred
+    zero-component rays of the centre row) walk the whole tree without
+    changing any result, so parity cannot see it; per-wave loop steps can:
+    no wave of the ordered walk may take more steps than the slowest wave
+    of the DFS-order walk."""
+    abi = mirt.abi
+    s, b = _scene(mirt, "render", 10000)
+    gpu.upload(s, b)
+    cam = mirt.default_camera()
+    gpu.set_option(abi.OPT_TRAVERSAL, abi.TRAV_UNIFORM)
+    try:
+        gpu.set_option(abi.OPT_ORDERED, 0)
+        dfs = gpu.wave_stats(cam, 1920, 1080, depth=1)
+        gpu.set_option(abi.OPT_ORDERED, 1)
+        ordered = gpu.wave_stats(cam, 1920, 1080, depth=1)
+    finally:
+        gpu.set_option(abi.OPT_TRAVERSAL, abi.TRAV_WAVEFRONT)
+        gpu.set_option(abi.OPT_ORDERED, 1)
+    assert ordered[:, 1].max() <= dfs[:, 1].max()
+    assert ordered[:, 1].sum() < dfs[:, 1].sum()
