@@ -245,15 +245,31 @@ struct Prune {
     float lim;  // prune when the grown box's entry t exceeds this; +inf = off
 };
 
-__device__ __forceinline__ Prune prune_off() { return {0.0f, INFINITY}; }
+__device__ __forceinline__ Prune prune_off() { return {INFINITY, INFINITY}; }
 
-// After a hit at t = best (finite). a4 = 4 d.d (SphRay).
+// Without any hit, M <= |o - c| + r <= sqrt(3) (|o|_inf + c_max) bounds every
+// sphere, so m0 = (2^-7 + 2^-20)(|o|_inf + c_max) is a valid growth from the
+// start (used by the zero-component test of pruned_any; the entry test also
+// needs a best).
+__device__ __forceinline__ float prune_m0(const DevScene& sc, float ox, float oy, float oz)
+{
+    const float oi = fmaxf(fabsf(ox), fmaxf(fabsf(oy), fabsf(oz)));
+    return (oi + sc.c_max) * (0x1p-7f + 0x1p-20f);
+}
+
+__device__ __forceinline__ Prune prune_start(const DevScene& sc, float ox, float oy, float oz)
+{
+    return sc.prune ? Prune{prune_m0(sc, ox, oy, oz), INFINITY} : prune_off();
+}
+
+// After a hit at t = best (finite). a4 = 4 d.d (SphRay). Both growths bound
+// the same error, so the smaller one is used.
 __device__ __forceinline__ void prune_update(Prune& p, const DevScene& sc, float ox, float oy, float oz, float a4,
                                              float best)
 {
     const float dl = __builtin_amdgcn_sqrtf(a4) * (0.5f + 0x1p-20f);  // >= |d|
     const float oi = fmaxf(fabsf(ox), fmaxf(fabsf(oy), fabsf(oz)));
-    p.m = (best * dl + sc.r_max) * 0x1p-8f + (oi + sc.c_max) * 0x1p-20f;
+    p.m = fminf((best * dl + sc.r_max) * 0x1p-8f + (oi + sc.c_max) * 0x1p-20f, prune_m0(sc, ox, oy, oz));
     p.lim = best + best * 0x1p-18f;
 }
 
@@ -296,9 +312,17 @@ __device__ __forceinline__ bool slab_fast(const SlabRay& r, const Prune& p, floa
 // The Prune test for any ray, including those slab_fast leaves to slab_test:
 // an axis whose direction component is zero or tiny (|d| < 2^-40) is left
 // out of the max, which only lowers the entry bound; the other axes use the
-// same normal-range reciprocals and margins as slab_fast.
+// same normal-range reciprocals and margins as slab_fast. An axis with d == 0
+// exactly prunes on its own when o lies outside the grown slab: every point
+// o + t d has that coordinate, and a recordable hit lies within the grown box
+// (Prune), although hit.c:54-57 passes such boxes by ignoring the slab.
+// (lo - m, hi + m are rounded, but m carries a 2x margin far above 2^-24
+// (c_max + m).)
 __device__ __forceinline__ bool pruned_any(const SlabRay& r, const Prune& p, const NodeV& n)
 {
+    if (r.zx && (r.ox < n.b0 - p.m || r.ox > n.b3 + p.m)) return true;
+    if (r.zy && (r.oy < n.b1 - p.m || r.oy > n.b4 + p.m)) return true;
+    if (r.zz && (r.oz < n.b2 - p.m || r.oz > n.b5 + p.m)) return true;
     constexpr float c = 1.0f - 0x1p-20f;
     const float tiny = 0x1p-40f;
     float e = -INFINITY;
@@ -577,7 +601,7 @@ __device__ __forceinline__ void closest_bvh_chunked(const DevScene& sc, const Ra
     uint32_t cur = 0;
     float bt = INFINITY;
     int bs = -1;
-    Prune pr = prune_off();  // wave-uniform: one ray
+    Prune pr = prune_start(sc, ray.ox, ray.oy, ray.oz);  // wave-uniform: one ray
     while (cur < end) {
         if (COUNT) cnt.steps++;
         const uint32_t base = cur;

@@ -1,8 +1,9 @@
 """The error bound behind closest-hit pruning (csrc/trace.h, struct Prune).
 
 A sphere hit that hit.c:19-39 records at t lies, as the exact point o + t d,
-within 2^-9.3 (t|d| + r) of the sphere's surface (analysis in trace.h); the
-kernel grows boxes by 2^-8 (best |d| + r_max). This sweeps the reference's
+within 2^-9.3 max(|o - c|, r) <= 2^-9.3 (t|d| + r + ...) of the sphere's
+surface (analysis in trace.h); the kernel grows boxes by 2^-8 (best |d| +
+r_max), or before any hit by 2^-7 (|o|_inf + c_max). This sweeps the reference's
 float32 arithmetic (numpy float32 is IEEE with no contraction, the same
 operation order as hit.c:19-39 with hit.c:28 in double) over random and
 grazing configurations, including unnormalised directions, and checks the
@@ -42,17 +43,22 @@ def _sweep(rng, n, grazing, unnormalised, radii):
     p = o.astype(np.float64) + t.astype(np.float64)[:, None] * d.astype(np.float64)
     dist = np.abs(np.linalg.norm(p - c.astype(np.float64), axis=1) - r.astype(np.float64))
     scale = t.astype(np.float64) * np.sqrt(a.astype(np.float64)) + r.astype(np.float64)
-    return (dist / scale)[ok]
+    m_geo = np.maximum(np.linalg.norm(oc.astype(np.float64), axis=1), r.astype(np.float64))
+    return (dist / scale)[ok], (dist / m_geo)[ok]
 
 
 def test_hit_point_error_inside_prune_margin():
     rng = np.random.default_rng(1)
-    worst = 0.0
+    worst = worst_m = 0.0
     for grazing in (True, False):
         for unnorm in (False, True):
             for radii in (lambda n: rng.uniform(0.5, 5.0, n), lambda n: 10 ** rng.uniform(-3, 3, n)):
-                ratio = _sweep(rng, 400_000, grazing, unnorm, radii)
+                ratio, ratio_m = _sweep(rng, 400_000, grazing, unnorm, radii)
                 assert ratio.size > 1000
                 worst = max(worst, float(ratio.max()))
-    # analysis: < 2^-9.3; the kernel's growth is 2^-8
+                worst_m = max(worst_m, float(ratio_m.max()))
+    # analysis: D < 2^-9.3 M with M = max(|o - c|, r) <= t|d| + r + D; the
+    # kernel grows boxes by 2^-8 (best |d| + r_max), or by 2^-7 (|o| + c_max)
+    # >= 2^-8 M before any hit (prune_m0)
     assert worst < 2.0 ** -9.3, worst
+    assert worst_m < 2.0 ** -9.3, worst_m
