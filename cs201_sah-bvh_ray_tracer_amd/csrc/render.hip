@@ -298,7 +298,7 @@ __global__ __launch_bounds__(256) void primary_kernel(DevScene sc, FrameConst f,
 }
 
 template <bool FAST, bool ORD>
-__global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
+__global__ __launch_bounds__(256, 5) void bounce_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
                                                      float* __restrict__ acc, const BounceRec* __restrict__ queue,
                                                      uint32_t* __restrict__ qctl, int threshold)
 {

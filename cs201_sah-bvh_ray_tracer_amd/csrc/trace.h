@@ -824,21 +824,22 @@ __device__ __forceinline__ void closest_packet_ordered(const DevScene& sc, const
 
 // Per-lane ordered walk state (bounce rays): `cur` is the PNode to visit
 // (kPNone: done), or, while `end` != 0, the next flat node of a DFS segment
-// that ends at `end`. The far children still to visit sit in a 4-entry
+// that ends at `end`. The far children still to visit sit in an 8-entry
 // shift-register stack; when it is full and both children pass, the node's
 // children are walked as the flat DFS segment [flat + 1, end) instead (the
-// reference order, pruned, no stack) -- ordering matters most near the root
-// (a 4-entry stack keeps all but ~1% of its gain on the 10k scene).
-constexpr int kLaneStack = 4;
+// reference order, pruned, no stack). 8 entries: on the 10k scene a 4-entry
+// stack costs little on average but doubles the longest walks (p99 147 ->
+// 210 steps, max 258 -> 492), which set the bounce pass's tail.
+constexpr int kLaneStack = 8;
 struct LaneWalk {
     uint32_t cur, end;
     uint32_t top;
-    uint32_t s0, s1, s2, s3;
+    uint32_t s0, s1, s2, s3, s4, s5, s6, s7;
 };
 
 __device__ __forceinline__ LaneWalk lane_walk_start(bool active)
 {
-    return LaneWalk{active ? 0u : kPNone, 0u, 0u, 0u, 0u, 0u, 0u};
+    return LaneWalk{active ? 0u : kPNone, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
 }
 
 __device__ __forceinline__ bool lane_walking(const LaneWalk& w) { return w.cur != kPNone; }
@@ -853,6 +854,10 @@ __device__ __forceinline__ void lane_walk_pop(LaneWalk& w)
     w.s0 = w.s1;
     w.s1 = w.s2;
     w.s2 = w.s3;
+    w.s3 = w.s4;
+    w.s4 = w.s5;
+    w.s5 = w.s6;
+    w.s6 = w.s7;
     w.top--;
 }
 
@@ -860,7 +865,7 @@ __device__ __forceinline__ void lane_walk_pop(LaneWalk& w)
 // reference order, hit.c's tie rule `t <= best`), started by lane_walk_dfs.
 __device__ __forceinline__ LaneWalk lane_walk_dfs(uint32_t num_nodes)
 {
-    return LaneWalk{0u, num_nodes, 0u, 0u, 0u, 0u, 0u};
+    return LaneWalk{0u, num_nodes, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
 }
 
 template <bool FAST, bool COUNT, bool ORD = true>
@@ -885,6 +890,10 @@ __device__ __forceinline__ void ordered_lane_step(const DevScene& sc, const Slab
     if (h0 && h1) {
         if (w.top < kLaneStack) {
             const bool swap = e1 < e0;
+            w.s7 = w.s6;
+            w.s6 = w.s5;
+            w.s5 = w.s4;
+            w.s4 = w.s3;
             w.s3 = w.s2;
             w.s2 = w.s1;
             w.s1 = w.s0;

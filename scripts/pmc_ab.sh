@@ -10,8 +10,7 @@ mkdir -p "$OUT"
 SETS=(
  "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU"
  "SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_IFETCH GRBM_GUI_ACTIVE"
- "SQ_WAIT_INST_LDS SQ_INST_CYCLES_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE"
- "SQC_ICACHE_MISSES SQC_ICACHE_HITS SQC_DCACHE_MISSES SQC_DCACHE_HITS"
+ ${PMC_EXTRA:-}
 )
 for cfg in "$@"; do
   name=${cfg%%:*}; opts=${cfg#*:}
