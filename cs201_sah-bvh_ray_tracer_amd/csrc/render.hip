@@ -297,13 +297,59 @@ __global__ __launch_bounds__(256) void primary_kernel(DevScene sc, FrameConst f,
     }
 }
 
-template <bool FAST, bool ORD>
-__global__ __launch_bounds__(256, 5) void bounce_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
+// The walk of one bounce ray: WALK 0 = reference DFS order, 1 = ordered
+// binary (PNode, register stack), 2 = ordered four-wide (QNode, LDS stack).
+template <int WALK>
+struct BounceWalk;
+template <>
+struct BounceWalk<0> {
+    LaneWalk w;
+    __device__ void start(const DevScene& sc) { w = lane_walk_dfs(sc.num_nodes); }
+    __device__ void stop() { w = lane_walk_start(false); }
+    __device__ bool walking() const { return lane_walking(w); }
+    template <bool FAST>
+    __device__ void step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr, uint32_t*, float& bt,
+                         int& bs, Counters& cnt)
+    {
+        ordered_lane_step<FAST, false, false>(sc, sr, sp, pr, w, bt, bs, cnt);
+    }
+};
+template <>
+struct BounceWalk<1> {
+    LaneWalk w;
+    __device__ void start(const DevScene&) { w = lane_walk_start(true); }
+    __device__ void stop() { w = lane_walk_start(false); }
+    __device__ bool walking() const { return lane_walking(w); }
+    template <bool FAST>
+    __device__ void step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr, uint32_t*, float& bt,
+                         int& bs, Counters& cnt)
+    {
+        ordered_lane_step<FAST, false, true>(sc, sr, sp, pr, w, bt, bs, cnt);
+    }
+};
+template <>
+struct BounceWalk<2> {
+    WideWalk w;
+    __device__ void start(const DevScene&) { w = wide_walk_start(true); }
+    __device__ void stop() { w = wide_walk_start(false); }
+    __device__ bool walking() const { return wide_walking(w); }
+    template <bool FAST>
+    __device__ void step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr, uint32_t* stk,
+                         float& bt, int& bs, Counters& cnt)
+    {
+        wide_lane_step<FAST, false>(sc, sr, sp, pr, w, stk, bt, bs, cnt);
+    }
+};
+
+template <bool FAST, int WALK>
+__global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
                                                      float* __restrict__ acc, const BounceRec* __restrict__ queue,
                                                      uint32_t* __restrict__ qctl, int threshold)
 {
     __shared__ uint32_t cstack[kMaxDepth * 256];
+    __shared__ uint32_t wstack[WALK == 2 ? kWideStack * kWideStride : 1];
     uint32_t* cs = cstack + threadIdx.x;
+    uint32_t* stk = wstack + (WALK == 2 ? threadIdx.x : 0);
     Counters cnt{0, 0, 0, 0, 0};
     const uint32_t n = __builtin_amdgcn_readfirstlane(qctl[0]);
     const uint32_t end = sc.num_nodes;
@@ -312,7 +358,8 @@ __global__ __launch_bounds__(256, 5) void bounce_kernel(DevScene sc, FrameConst 
     SlabRay sr = slab_ray(ray);
     SphRay sp = sph_ray(ray);
     Prune pr = prune_off();
-    LaneWalk w = lane_walk_start(false);
+    BounceWalk<WALK> w;
+    w.stop();
     uint32_t pixel = 0, k = 0, base0 = 0;
     int level = 0, best_s = -1;
     float best_t = INFINITY;
@@ -339,7 +386,7 @@ __global__ __launch_bounds__(256, 5) void bounce_kernel(DevScene sc, FrameConst 
                     level = 1;
                     const int r = (int)(pixel / f.width), x = (int)(pixel - r * f.width);
                     key = pixel_key(f.seed, (uint32_t)(shard_row_to_y(f, r) * f.width + x), f.sample);
-                    w = ORD ? lane_walk_start(true) : lane_walk_dfs(end);
+                    w.start(sc);
                     best_t = INFINITY;
                     best_s = -1;
                     pr = prune_off();
@@ -350,15 +397,15 @@ __global__ __launch_bounds__(256, 5) void bounce_kernel(DevScene sc, FrameConst 
         if (!__ballot(has)) break;
         // walk until few lanes are still walking and the others can make progress
         for (;;) {
-            const uint64_t walking = __ballot(has && lane_walking(w));
+            const uint64_t walking = __ballot(has && w.walking());
             if (!walking) break;
             if (__popcll(walking) < threshold &&
-                (__ballot(has && !lane_walking(w)) || (!exhausted && __ballot(!has))))
+                (__ballot(has && !w.walking()) || (!exhausted && __ballot(!has))))
                 break;
-            if (has && lane_walking(w)) ordered_lane_step<FAST, false, ORD>(sc, sr, sp, pr, w, best_t, best_s, cnt);
+            if (has && w.walking()) w.template step<FAST>(sc, sr, sp, pr, stk, best_t, best_s, cnt);
         }
         // shade every lane whose ray is done (renderer.c:46-77 for that level)
-        if (has && !lane_walking(w)) {
+        if (has && !w.walking()) {
             bool finish = true;
             uint32_t tail = 255u << 24;          // depth exhausted: black (renderer.c:23-24)
             int stored = level - 1;
@@ -376,7 +423,7 @@ __global__ __launch_bounds__(256, 5) void bounce_kernel(DevScene sc, FrameConst 
                     ray = Ray{p[0], p[1], p[2], bx, by, bz};
                     sr = slab_ray(ray);
                     sp = sph_ray(ray);
-                    w = ORD ? lane_walk_start(true) : lane_walk_dfs(end);
+                    w.start(sc);
                     best_t = INFINITY;
                     best_s = -1;
                     pr = prune_off();
@@ -530,6 +577,10 @@ struct mirt_ctx {
     PNode* d_pnodes = nullptr;  // ordered-walk layout of the tree
     bool ordered_ok = false;    // leaves in DFS order hold increasing sphere indices, depth < 63
     int ordered = 1;            // ordered (nearer-child-first) walks where the tree admits them
+    HNode* d_hnodes = nullptr;  // four-wide layout (per-lane walks)
+    HAux* d_haux = nullptr;
+    LeafRec* d_leaves = nullptr;
+    int wide = 1;               // four-wide per-lane walks where the tree admits them
     float r_max = 0.0f, c_max = 0.0f;
     int bounce_threshold = 40;  // wavefront: shade finished rays once fewer lanes walk
     int bounce_blocks = 0;      // wavefront: persistent workgroups (set in mirt_create)
@@ -662,11 +713,100 @@ bool build_pnodes(const mirt_node* nd, int nn, int ns, std::vector<PNode>& pn)
     return mono && depth + 2 <= 64;
 }
 
+// fp16 bits of the largest half <= v / the smallest half >= v (a value
+// beyond the fp16 range rounds out to -inf / +inf: still a superset).
+uint16_t half_bits(float v)
+{
+    const _Float16 h = (_Float16)v;
+    uint16_t b;
+    std::memcpy(&b, &h, 2);
+    return b;
+}
+float half_value(uint16_t b)
+{
+    _Float16 h;
+    std::memcpy(&h, &b, 2);
+    return (float)h;
+}
+uint16_t half_down(float v)
+{
+    uint16_t b = half_bits(v);
+    while (half_value(b) > v) b = b == 0x0000 ? 0x8001 : (b & 0x8000) ? b + 1 : b - 1;
+    return b;
+}
+uint16_t half_up(float v)
+{
+    uint16_t b = half_bits(v);
+    while (half_value(b) < v) b = b == 0x8000 ? 0x0001 : (b & 0x8000) ? b - 1 : b + 1;
+    return b;
+}
+
+// HNode layout (trace.h) of a validated flat tree: HNode 0 holds the root;
+// an HNode for each inner node that is some HNode's slot holds that node's
+// grandchildren (a leaf child standing in for its own); one LeafRec per
+// leaf slot. Used only when the PNode conditions hold and the boxes nest.
+void build_hnodes(const mirt_node* nd, int nn, const mirt_sphere* sp, int ns, std::vector<HNode>& hn,
+                  std::vector<HAux>& aux, std::vector<LeafRec>& leaves)
+{
+    hn.assign(1, HNode{});
+    aux.assign(1, HAux{0xffffffffu, (uint32_t)nn});  // flat + 1 == 0: the whole tree
+    leaves.clear();
+    std::vector<uint32_t> todo;  // inner nodes waiting for their HNode: HNode 1 + i is todo[i]
+    auto fill = [&](HNode& h, int k, uint32_t ci) {
+        const mirt_node& n = nd[ci];
+        for (int a = 0; a < 3; a++)
+            h.box[k][a] = (uint32_t)half_down(n.bmin[a]) | ((uint32_t)half_up(n.bmax[a]) << 16);
+        uint32_t ref;
+        if (n.skip & MIRT_NODE_EMPTY) {
+            ref = kPNone;
+        } else if (n.sphere >= 0) {
+            if (n.sphere >= ns) {
+                ref = kPNone;
+            } else {
+                LeafRec l{};
+                std::memcpy(l.lo, n.bmin, sizeof l.lo);
+                std::memcpy(l.hi, n.bmax, sizeof l.hi);
+                l.sphere = n.sphere;
+                const mirt_sphere& s = sp[n.sphere];
+                l.geo = make_float4(s.center.x, s.center.y, s.center.z, s.radius);
+                ref = kPLeaf | (uint32_t)leaves.size();
+                leaves.push_back(l);
+            }
+        } else {
+            todo.push_back(ci);
+            ref = (uint32_t)todo.size();
+        }
+        h.ref[k] = ref;
+    };
+    for (int k = 0; k < 4; k++) hn[0].ref[k] = kPNone;
+    if (nn == 0) return;
+    fill(hn[0], 0, 0);
+    for (size_t next = 0; next < todo.size(); next++) {
+        const uint32_t y = todo[next];
+        HNode h{};
+        for (int k = 0; k < 4; k++) h.ref[k] = kPNone;
+        hn.push_back(h);
+        aux.push_back(HAux{y, nd[y].skip & MIRT_SKIP_MASK});
+        const uint32_t kids[2] = {y + 1, nd[y + 1].skip & MIRT_SKIP_MASK};
+        int k = 0;
+        for (uint32_t c : kids) {
+            if (nd[c].sphere < 0 && !(nd[c].skip & MIRT_NODE_EMPTY)) {
+                fill(hn.back(), k++, c + 1);
+                fill(hn.back(), k++, nd[c + 1].skip & MIRT_SKIP_MASK);
+            } else {
+                fill(hn.back(), k++, c);
+            }
+        }
+    }
+}
+
 DevScene dev_scene(const mirt_ctx* c)
 {
     const bool prune = c->prune && c->prune_ok;
     return DevScene{c->d_nodes, c->d_nodes32, c->d_geo, c->d_color, (uint32_t)c->num_nodes, c->num_spheres,
-                    prune, c->r_max, c->c_max, c->d_pnodes, prune && c->ordered && c->ordered_ok && c->fast_slab};
+                    prune, c->r_max, c->c_max, c->d_pnodes, prune && c->ordered && c->ordered_ok && c->fast_slab,
+                    c->d_hnodes, c->d_haux, c->d_leaves,
+                    prune && c->ordered && c->ordered_ok && c->fast_slab && c->wide};
 }
 
 bool ctx_ok(mirt_ctx* c, bool need_scene, const char* fn)
@@ -749,15 +889,18 @@ int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_ac
             primary_kernel<false><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ph1, s));
-        if (c->fast_slab && sc.ordered)
-            bounce_kernel<true, true><<<c->bounce_blocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
-                                                                     c->bounce_threshold);
+        if (c->fast_slab && sc.wide)
+            bounce_kernel<true, 2><<<c->bounce_blocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
+                                                                  c->bounce_threshold);
+        else if (c->fast_slab && sc.ordered)
+            bounce_kernel<true, 1><<<c->bounce_blocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
+                                                                  c->bounce_threshold);
         else if (c->fast_slab)
-            bounce_kernel<true, false><<<c->bounce_blocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
-                                                                      c->bounce_threshold);
+            bounce_kernel<true, 0><<<c->bounce_blocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
+                                                                  c->bounce_threshold);
         else
-            bounce_kernel<false, false><<<c->bounce_blocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
-                                                                       c->bounce_threshold);
+            bounce_kernel<false, 0><<<c->bounce_blocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
+                                                                   c->bounce_threshold);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ph2, s));
         if (timed) HIP_TRY(hipEventRecord(c->ev1, s));
@@ -800,7 +943,7 @@ int mirt_create(int device, mirt_ctx** out)
         int cus = 0, per_cu = 0;
         e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
         if (e == hipSuccess)
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bounce_kernel<true, true>, 256, 0);
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bounce_kernel<true, 2>, 256, 0);
         c->bounce_blocks = std::max(1, cus) * std::max(1, per_cu);
     }
     if (e != hipSuccess) {
@@ -817,7 +960,8 @@ void mirt_destroy(mirt_ctx* c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : {(void*)c->d_nodes, (void*)c->d_nodes32, (void*)c->d_geo, (void*)c->d_color, (void*)c->d_out, (void*)c->d_acc,
-                    c->d_in, c->d_res, (void*)c->d_counts, (void*)c->d_defer, c->d_queue, (void*)c->d_pnodes})
+                    c->d_in, c->d_res, (void*)c->d_counts, (void*)c->d_defer, c->d_queue, (void*)c->d_pnodes,
+                    (void*)c->d_hnodes, (void*)c->d_haux, (void*)c->d_leaves})
         if (p) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -858,9 +1002,13 @@ int mirt_scene_upload_flat(mirt_ctx* c, const mirt_sphere* spheres, int ns, cons
     }
     geo[ns] = make_float4(NAN, NAN, NAN, NAN);  // &spheres[N] sentinel: never hits
     col[ns] = 0xff000000u;
-    for (void* p : {(void*)c->d_nodes, (void*)c->d_nodes32, (void*)c->d_geo, (void*)c->d_color, (void*)c->d_pnodes})
+    for (void* p : {(void*)c->d_nodes, (void*)c->d_nodes32, (void*)c->d_geo, (void*)c->d_color, (void*)c->d_pnodes,
+                    (void*)c->d_hnodes, (void*)c->d_haux, (void*)c->d_leaves})
         if (p) (void)hipFree(p);
     c->d_pnodes = nullptr;
+    c->d_hnodes = nullptr;
+    c->d_haux = nullptr;
+    c->d_leaves = nullptr;
     c->d_nodes = nullptr;
     c->d_nodes32 = nullptr;
     c->d_geo = nullptr;
@@ -889,6 +1037,16 @@ int mirt_scene_upload_flat(mirt_ctx* c, const mirt_sphere* spheres, int ns, cons
     const bool ordered = build_pnodes(nodes, nn, ns, pn);
     HIP_TRY(hipMalloc((void**)&c->d_pnodes, sizeof(PNode) * pn.size()));
     HIP_TRY(hipMemcpy(c->d_pnodes, pn.data(), sizeof(PNode) * pn.size(), hipMemcpyHostToDevice));
+    std::vector<HNode> hn;
+    std::vector<HAux> hx;
+    std::vector<LeafRec> lr;
+    build_hnodes(nodes, nn, spheres, ns, hn, hx, lr);
+    HIP_TRY(hipMalloc((void**)&c->d_hnodes, sizeof(HNode) * hn.size()));
+    HIP_TRY(hipMalloc((void**)&c->d_haux, sizeof(HAux) * hx.size()));
+    HIP_TRY(hipMalloc((void**)&c->d_leaves, sizeof(LeafRec) * std::max<size_t>(lr.size(), 1)));
+    HIP_TRY(hipMemcpy(c->d_hnodes, hn.data(), sizeof(HNode) * hn.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->d_haux, hx.data(), sizeof(HAux) * hx.size(), hipMemcpyHostToDevice));
+    if (!lr.empty()) HIP_TRY(hipMemcpy(c->d_leaves, lr.data(), sizeof(LeafRec) * lr.size(), hipMemcpyHostToDevice));
     c->num_nodes = nn;
     c->num_spheres = ns;
     c->ordered_ok = ordered;
@@ -1189,6 +1347,9 @@ int mirt_set_option(mirt_ctx* c, int option, int value)
     case MIRT_OPT_ORDERED:
         c->ordered = value != 0;
         return MIRT_OK;
+    case MIRT_OPT_WIDE:
+        c->wide = value != 0;
+        return MIRT_OK;
     case MIRT_OPT_BLOCK_WAVES:
         if (value != 1 && value != 2 && value != 4 && value != 8) break;
         c->block_waves = value;
@@ -1210,6 +1371,7 @@ int mirt_get_option(mirt_ctx* c, int option)
     if (option == MIRT_OPT_BOUNCE_THRESHOLD) return c->bounce_threshold;
     if (option == MIRT_OPT_PRUNE) return c->prune;
     if (option == MIRT_OPT_ORDERED) return c->ordered;
+    if (option == MIRT_OPT_WIDE) return c->wide;
     set_error("mirt_get_option: bad option %d", option);
     return MIRT_E_INVALID;
 }

@@ -58,6 +58,40 @@ struct __attribute__((aligned(64))) PNode {
 };
 static_assert(sizeof(PNode) == 64, "ordered node is 64 B");
 
+// Four-wide layout for per-lane walks: HNode(Y), for an inner node Y of the
+// reference tree, holds Y's grandchildren (a child that is a leaf stands in
+// for its own slot), so a walk takes half the dependent steps. The skipped
+// children's boxes need no test: the tree's boxes nest (checked at upload)
+// and hit.c's slab test is monotone under containment (correctly rounded
+// subtraction and division are monotone, so a box inside another gets a
+// later entry and an earlier exit), so a ray that passes a box passes every
+// enclosing one -- the leaves reached are exactly those hit.c:91-109
+// reaches. The same argument lets slot boxes be CONSERVATIVE: each is
+// stored in fp16 rounded outward (a superset) and tested with a fast test
+// that passes when undecided -- entering an inner node too eagerly costs
+// work, never a result, because every leaf is still gated by its exact box.
+// A leaf slot's exact box and its sphere live in a LeafRec fetched when the
+// fp16 box passes. 64 B per node = the bytes of two fp32 boxes: divergent
+// per-lane loads are bound by the bytes the texture path returns.
+// HNode 0 is a virtual node whose only slot is the root; slot references: an
+// inner HNode index, kPLeaf | LeafRec index, or kPNone. HAux holds the
+// node's flat DFS segment [flat + 1, end), read only when the stack is full.
+struct __attribute__((aligned(64))) HNode {
+    uint32_t box[4][3];  // per slot and axis: fp16 lo (bits 0-15) | fp16 hi (bits 16-31)
+    uint32_t ref[4];
+};
+static_assert(sizeof(HNode) == 64, "wide node is 64 B");
+struct HAux {
+    uint32_t flat, end;
+};
+struct __attribute__((aligned(16))) LeafRec {
+    float lo[3], hi[3];  // the leaf's exact box (bvh.c bounds)
+    int32_t sphere;
+    uint32_t pad;
+    float4 geo;          // the sphere: centre, radius
+};
+static_assert(sizeof(LeafRec) == 48, "leaf record is 48 B");
+
 // Read-only scene in HBM (L2 / Infinity-Cache resident at the BASELINE sizes).
 struct DevScene {
     const DNode* nodes;     // 64 B, leaf sphere inline: scalar (wave-uniform) walks
@@ -76,6 +110,11 @@ struct DevScene {
     // enough for the 64-entry walk stack
     const PNode* pnodes;
     int ordered;
+    // four-wide per-lane walks (HNode): ordered trees whose boxes nest
+    const HNode* hnodes;
+    const HAux* haux;
+    const LeafRec* leaves;
+    int wide;
 };
 
 struct Ray {
@@ -911,6 +950,139 @@ __device__ __forceinline__ void ordered_lane_step(const DevScene& sc, const Slab
     } else {
         lane_walk_pop(w);
     }
+}
+
+// Per-lane four-wide walk (bounce rays): `cur` is the HNode to visit (kPNone:
+// done) or, while `end` != 0, the next node of a flat DFS segment ending at
+// `end`. Subtrees still to visit wait on a per-lane stack in LDS (`stk`:
+// entry k at stk[k * kWideStride]); a step pushes all passing inner slots but
+// the nearest, farthest first. When that would overflow kWideStack, the
+// node's whole subtree is walked as a DFS segment instead.
+constexpr int kWideStack = 16;
+constexpr int kWideStride = 256;  // threads per workgroup of the bounce kernel
+struct WideWalk {
+    uint32_t cur, end, top;
+};
+
+__device__ __forceinline__ WideWalk wide_walk_start(bool active) { return WideWalk{active ? 0u : kPNone, 0u, 0u}; }
+__device__ __forceinline__ bool wide_walking(const WideWalk& w) { return w.cur != kPNone; }
+
+__device__ __forceinline__ void wide_walk_pop(WideWalk& w, const uint32_t* stk)
+{
+    if (w.top == 0) {
+        w.cur = kPNone;
+        return;
+    }
+    w.top--;
+    w.cur = stk[w.top * kWideStride];
+}
+
+// Compare-exchange of (entry, ref) pairs: ascending entry.
+__device__ __forceinline__ void cx(float& ka, uint32_t& ra, float& kb, uint32_t& rb)
+{
+    const bool sw = kb < ka;
+    const float k = sw ? kb : ka;
+    const uint32_t r = sw ? rb : ra;
+    kb = sw ? ka : kb;
+    rb = sw ? ra : rb;
+    ka = k;
+    ra = r;
+}
+
+__device__ __forceinline__ float h_lo(uint32_t v) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(v & 0xffffu)); }
+__device__ __forceinline__ float h_hi(uint32_t v) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(v >> 16)); }
+
+// Conservative box test: passes whenever hit.c's slab test on this box
+// would (slab_fast's margins, with "undecided" counted as a pass; the exact
+// division test for rays with a zero/tiny component), and also applies the
+// pruning bound, which holds for any box containing the subtree.
+__device__ __forceinline__ bool slab_cons(const SlabRay& r, const Prune& p, float x0, float y0, float z0, float x1,
+                                          float y1, float z1, float& near)
+{
+    if (r.generic) {
+        near = 0.0f;
+        return slab_test(r, x0, y0, z0, x1, y1, z1);
+    }
+    const float tx1 = (x0 - r.ox) * r.ix, tx2 = (x1 - r.ox) * r.ix;
+    const float ty1 = (y0 - r.oy) * r.iy, ty2 = (y1 - r.oy) * r.iy;
+    const float tz1 = (z0 - r.oz) * r.iz, tz2 = (z1 - r.oz) * r.iz;
+    const float nx = fminf(tx1, tx2), ny = fminf(ty1, ty2), nz = fminf(tz1, tz2);
+    constexpr float c = 1.0f - 0x1p-20f;
+    const float entry = fmaxf(fmaf(nx, c, -(p.m * fabsf(r.ix))),
+                              fmaxf(fmaf(ny, c, -(p.m * fabsf(r.iy))), fmaf(nz, c, -(p.m * fabsf(r.iz)))));
+    if (entry > p.lim) return false;
+    const float tmin = fmaxf(nx, fmaxf(ny, nz));
+    const float tmax = fminf(fmaxf(tx1, tx2), fminf(fmaxf(ty1, ty2), fmaxf(tz1, tz2)));
+    near = tmin;
+    const float m = (fabsf(tmin) + fabsf(tmax)) * 0x1p-20f;
+    return !(tmax - tmin < -m || tmax - kEps < -m);
+}
+
+// One HNode slot for one lane. Returns whether the walk should enter it.
+template <bool FAST>
+__device__ __forceinline__ bool wide_slot(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
+                                          uint32_t ref, uint32_t bx, uint32_t by, uint32_t bz, float& near,
+                                          float& best_t, int& best_s)
+{
+    if (ref == kPNone) return false;
+    if (!slab_cons(sr, pr, h_lo(bx), h_lo(by), h_lo(bz), h_hi(bx), h_hi(by), h_hi(bz), near)) return false;
+    if (!(ref & kPLeaf)) return true;
+    // the leaf's gate: its exact box under hit.c's test, then its sphere
+    const float4* lp = (const float4*)(sc.leaves + (ref & ~kPLeaf));
+    const float4 l0 = lp[0], l1 = lp[1], g = lp[2];
+    float e;
+    if (slab_box<FAST>(sr, pr, l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, e))
+        consider_sphere<FAST>(sc, sp, pr, sr.ox, sr.oy, sr.oz, __float_as_int(l1.z), g, best_t, best_s);
+    return false;
+}
+
+template <bool FAST, bool COUNT>
+__device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
+                                               WideWalk& w, uint32_t* stk, float& best_t, int& best_s, Counters& cnt)
+{
+    if (COUNT) cnt.steps++;
+    if (w.end) {
+        lane_step<FAST, COUNT, true>(sc, sr, sp, pr, w.cur, best_t, best_s, cnt);
+        if (w.cur >= w.end) {
+            w.end = 0;
+            wide_walk_pop(w, stk);
+        }
+        return;
+    }
+    const uint4* p = (const uint4*)(sc.hnodes + w.cur);
+    const uint4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+    float e0 = 0.0f, e1 = 0.0f, e2 = 0.0f, e3 = 0.0f;
+    const bool h0 = wide_slot<FAST>(sc, sr, sp, pr, q3.x, q0.x, q0.y, q0.z, e0, best_t, best_s);
+    const bool h1 = wide_slot<FAST>(sc, sr, sp, pr, q3.y, q0.w, q1.x, q1.y, e1, best_t, best_s);
+    const bool h2 = wide_slot<FAST>(sc, sr, sp, pr, q3.z, q1.z, q1.w, q2.x, e2, best_t, best_s);
+    const bool h3 = wide_slot<FAST>(sc, sr, sp, pr, q3.w, q2.y, q2.z, q2.w, e3, best_t, best_s);
+    const uint32_t n = (uint32_t)h0 + (uint32_t)h1 + (uint32_t)h2 + (uint32_t)h3;
+    if (n == 0) {
+        wide_walk_pop(w, stk);
+        return;
+    }
+    if (w.top + n - 1 > (uint32_t)kWideStack) {
+        const HAux ax = sc.haux[w.cur];
+        w.cur = ax.flat + 1;
+        w.end = ax.end;
+        return;
+    }
+    // sort the passing slots by entry, nearest first; failing slots get +inf
+    // and passing ones a finite key, so the n passing slots come first
+    constexpr float big = 3.0e38f;
+    float k0 = h0 ? fminf(e0, big) : INFINITY, k1 = h1 ? fminf(e1, big) : INFINITY;
+    float k2 = h2 ? fminf(e2, big) : INFINITY, k3 = h3 ? fminf(e3, big) : INFINITY;
+    uint32_t a0 = q3.x, a1 = q3.y, a2 = q3.z, a3 = q3.w;
+    cx(k0, a0, k1, a1);
+    cx(k2, a2, k3, a3);
+    cx(k0, a0, k2, a2);
+    cx(k1, a1, k3, a3);
+    cx(k1, a1, k2, a2);
+    if (n >= 2) stk[(w.top + n - 2) * kWideStride] = a1;
+    if (n >= 3) stk[(w.top + n - 3) * kWideStride] = a2;
+    if (n >= 4) stk[(w.top + n - 4) * kWideStride] = a3;
+    w.top += n - 1;
+    w.cur = a0;
 }
 
 // Closest hit for every active lane: degenerate rays (a zero or tiny

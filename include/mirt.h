@@ -257,11 +257,15 @@ int mirt_last_phase_ms(mirt_ctx *ctx, float *phase);
    MIRT_OPT_ORDERED: 1 (default) = with pruning, walks enter the nearer child
    first (same closest hit: ties still go to the later DFS leaf; active only
    for a tree whose leaves hold increasing sphere indices in DFS order, as
-   the reference's builds do, and depth < 63); 0 = DFS order. */
+   the reference's builds do, and depth < 63); 0 = DFS order.
+   MIRT_OPT_WIDE: 1 (default) = with ordering, per-lane (bounce) walks use a
+   four-wide re-layout of the same tree (half the dependent steps; exact
+   because the reference slab test is monotone under box containment);
+   0 = the binary ordered walk. */
 enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3, MIRT_OPT_DEFER = 4,
        MIRT_OPT_BOUNCE_THRESHOLD = 5, /* wavefront: shade finished bounce rays once fewer than
                                          this many lanes of a wave still walk (0..64, default 40) */
-       MIRT_OPT_PRUNE = 6, MIRT_OPT_ORDERED = 7 };
+       MIRT_OPT_PRUNE = 6, MIRT_OPT_ORDERED = 7, MIRT_OPT_WIDE = 8 };
 enum { MIRT_TRAV_UNIFORM = 0, MIRT_TRAV_LANE = 1, MIRT_TRAV_HYBRID = 2, MIRT_TRAV_LANE_NP = 3,
        MIRT_TRAV_HYBRID_NP = 4,  /* *_NP: per-lane walk without successor prefetch */
        MIRT_TRAV_WAVEFRONT = 5   /* default: camera-ray packets, then persistent per-lane

@@ -7,11 +7,12 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/$1; DEPTH=$2; shift 2
 mkdir -p "$OUT"
+# extra counter sets: PMC_EXTRA="SET A COUNTERS;SET B COUNTERS"
 SETS=(
  "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU"
  "SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_IFETCH GRBM_GUI_ACTIVE"
- ${PMC_EXTRA:-}
 )
+if [ -n "${PMC_EXTRA:-}" ]; then IFS=';' read -ra extra <<< "$PMC_EXTRA"; SETS+=("${extra[@]}"); fi
 for cfg in "$@"; do
   name=${cfg%%:*}; opts=${cfg#*:}
   args=()

@@ -284,9 +284,10 @@ def test_sentinel_and_edge_scenes(gpu, mirt, oracle):
 
 
 @pytest.mark.parametrize("trav", [0, 1, 2, 3, 4, 5])
-@pytest.mark.parametrize("fast,prune,ordered", [(0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 1, 1)])
+@pytest.mark.parametrize("fast,prune,ordered,wide", [(0, 0, 0, 0), (1, 0, 0, 0), (1, 1, 0, 0), (1, 1, 1, 0),
+                                                     (1, 1, 1, 1)])
 @pytest.mark.parametrize("defer", [0, 1])
-def test_all_schedules_bit_identical(gpu, mirt, golden, small, scene1000, trav, fast, prune, ordered, defer):
+def test_all_schedules_bit_identical(gpu, mirt, golden, small, scene1000, trav, fast, prune, ordered, wide, defer):
     """Every traversal schedule x slab-test form x pruning gives the
     reference's bytes: per-ray hits and traces, and the 1080p 10k
     depth-1/depth-5 frames."""
@@ -295,6 +296,7 @@ def test_all_schedules_bit_identical(gpu, mirt, golden, small, scene1000, trav, 
     gpu.set_option(abi.OPT_FAST_SLAB, fast)
     gpu.set_option(abi.OPT_PRUNE, prune)
     gpu.set_option(abi.OPT_ORDERED, ordered)
+    gpu.set_option(abi.OPT_WIDE, wide)
     gpu.set_option(abi.OPT_DEFER, defer)
     try:
         s, b = scene1000
@@ -313,6 +315,7 @@ def test_all_schedules_bit_identical(gpu, mirt, golden, small, scene1000, trav, 
         gpu.set_option(abi.OPT_FAST_SLAB, 1)
         gpu.set_option(abi.OPT_PRUNE, 1)
         gpu.set_option(abi.OPT_ORDERED, 1)
+        gpu.set_option(abi.OPT_WIDE, 1)
         gpu.set_option(abi.OPT_DEFER, 1)
 
 
