@@ -116,14 +116,15 @@ struct Deferred {
 template <int TRAV, bool FAST, bool COUNT>
 __device__ __forceinline__ void render_pixel(const DevScene& sc, const FrameConst& f, int x, int r, bool alive,
                                              bool skip_generic, uint32_t* __restrict__ out, float* __restrict__ acc,
-                                             Counters& cnt, uint32_t* cstack, int cstride)
+                                             Counters& cnt, uint32_t* cstack, int cstride,
+                                             uint32_t* wstk = nullptr)
 {
     const int y = alive ? shard_row_to_y(f, r) : 0;
     const Ray ray = camera_ray(f, alive ? x : 0, y);
     if (skip_generic && alive && slab_ray(ray).generic) alive = false;  // a deferred wave traces it
     const uint64_t key = pixel_key(f.seed, (uint32_t)(y * f.width + x), f.sample);
     const uint32_t c = trace_path<TRAV, FAST, COUNT>(sc, ray, alive, f.depth, f.use_bvh != 0, key, cnt, cstack,
-                                                     cstride);
+                                                     cstride, wstk);
     if (!alive) return;
     const size_t i = (size_t)r * f.width + x;
     uint32_t shown = c;
@@ -153,6 +154,9 @@ __global__ __launch_bounds__(512) void render_kernel(DevScene sc, FrameConst f, 
     uint64_t t0 = 0;
     if (COUNT) t0 = __builtin_amdgcn_s_memrealtime();
     __shared__ uint32_t cstack[kMaxDepth * 512];
+    // the four-wide walk's stack (stride kWideStride: workgroups of up to 256)
+    __shared__ uint32_t wstack[kWideStack * kWideStride];
+    uint32_t* wstk = blockDim.x <= kWideStride ? wstack + threadIdx.x : nullptr;
     Counters cnt{0, 0, 0, 0, 0};
     const int bw = blockDim.x >> 6;
     const int wave = threadIdx.x >> 6;
@@ -162,7 +166,7 @@ __global__ __launch_bounds__(512) void render_kernel(DevScene sc, FrameConst f, 
         for (uint32_t j = blockIdx.x * bw + wave; j < n; j += stride) {
             const uint32_t p = __builtin_amdgcn_readfirstlane(dfr.list[j]);
             render_pixel<TRAV, FAST, COUNT>(sc, f, (int)(p % f.width), (int)(p / f.width), (threadIdx.x & 63) == 0,
-                                            false, out, acc, cnt, cstack + threadIdx.x, blockDim.x);
+                                            false, out, acc, cnt, cstack + threadIdx.x, blockDim.x, wstk);
         }
         if (COUNT) add_counts(counts, cnt);
         return;
@@ -173,7 +177,7 @@ __global__ __launch_bounds__(512) void render_kernel(DevScene sc, FrameConst f, 
     const int x = (tile % tiles_x) * 8 + (lane & 7);
     const int r = (tile / tiles_x) * 8 + (lane >> 3);
     render_pixel<TRAV, FAST, COUNT>(sc, f, x, r, x < f.width && r < f.num_rows, dfr.blocks > 0, out, acc, cnt,
-                                    cstack + threadIdx.x, blockDim.x);
+                                    cstack + threadIdx.x, blockDim.x, wstk);
     if (COUNT) {
         add_counts(counts, cnt);
         if (wave_stats && lane == 0) {
@@ -453,8 +457,10 @@ __global__ __launch_bounds__(256) void trace_rays_kernel(DevScene sc, const mirt
     const Ray ray{rr.origin.x, rr.origin.y, rr.origin.z, rr.direction.x, rr.direction.y, rr.direction.z};
     Counters cnt{0, 0, 0, 0, 0};
     __shared__ uint32_t cstack[kMaxDepth * 256];
+    __shared__ uint32_t wstack[kWideStack * kWideStride];
     const uint32_t c = trace_path<TRAV, FAST, false>(sc, ray, alive, depth, use_bvh != 0,
-                                                  pixel_key(seed, (uint32_t)i, sample), cnt, cstack + threadIdx.x, 256);
+                                                  pixel_key(seed, (uint32_t)i, sample), cnt, cstack + threadIdx.x, 256,
+                                                  wstack + threadIdx.x);
     if (alive) out[i] = c;
 }
 

@@ -1019,20 +1019,25 @@ __device__ __forceinline__ bool slab_cons(const SlabRay& r, const Prune& p, floa
 }
 
 // One HNode slot for one lane. Returns whether the walk should enter it.
-template <bool FAST>
+// COUNT: a slot test counts as a node test, a leaf's exact gate does not
+// (it re-tests the same node), a sphere test as a sphere test.
+template <bool FAST, bool COUNT>
 __device__ __forceinline__ bool wide_slot(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
                                           uint32_t ref, uint32_t bx, uint32_t by, uint32_t bz, float& near,
-                                          float& best_t, int& best_s)
+                                          float& best_t, int& best_s, Counters& cnt)
 {
     if (ref == kPNone) return false;
+    if (COUNT) cnt.nodes++;
     if (!slab_cons(sr, pr, h_lo(bx), h_lo(by), h_lo(bz), h_hi(bx), h_hi(by), h_hi(bz), near)) return false;
     if (!(ref & kPLeaf)) return true;
     // the leaf's gate: its exact box under hit.c's test, then its sphere
     const float4* lp = (const float4*)(sc.leaves + (ref & ~kPLeaf));
     const float4 l0 = lp[0], l1 = lp[1], g = lp[2];
     float e;
-    if (slab_box<FAST>(sr, pr, l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, e))
+    if (slab_box<FAST>(sr, pr, l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, e)) {
+        if (COUNT) cnt.spheres++;
         consider_sphere<FAST>(sc, sp, pr, sr.ox, sr.oy, sr.oz, __float_as_int(l1.z), g, best_t, best_s);
+    }
     return false;
 }
 
@@ -1052,10 +1057,10 @@ __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay
     const uint4* p = (const uint4*)(sc.hnodes + w.cur);
     const uint4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
     float e0 = 0.0f, e1 = 0.0f, e2 = 0.0f, e3 = 0.0f;
-    const bool h0 = wide_slot<FAST>(sc, sr, sp, pr, q3.x, q0.x, q0.y, q0.z, e0, best_t, best_s);
-    const bool h1 = wide_slot<FAST>(sc, sr, sp, pr, q3.y, q0.w, q1.x, q1.y, e1, best_t, best_s);
-    const bool h2 = wide_slot<FAST>(sc, sr, sp, pr, q3.z, q1.z, q1.w, q2.x, e2, best_t, best_s);
-    const bool h3 = wide_slot<FAST>(sc, sr, sp, pr, q3.w, q2.y, q2.z, q2.w, e3, best_t, best_s);
+    const bool h0 = wide_slot<FAST, COUNT>(sc, sr, sp, pr, q3.x, q0.x, q0.y, q0.z, e0, best_t, best_s, cnt);
+    const bool h1 = wide_slot<FAST, COUNT>(sc, sr, sp, pr, q3.y, q0.w, q1.x, q1.y, e1, best_t, best_s, cnt);
+    const bool h2 = wide_slot<FAST, COUNT>(sc, sr, sp, pr, q3.z, q1.z, q1.w, q2.x, e2, best_t, best_s, cnt);
+    const bool h3 = wide_slot<FAST, COUNT>(sc, sr, sp, pr, q3.w, q2.y, q2.z, q2.w, e3, best_t, best_s, cnt);
     const uint32_t n = (uint32_t)h0 + (uint32_t)h1 + (uint32_t)h2 + (uint32_t)h3;
     if (n == 0) {
         wide_walk_pop(w, stk);
@@ -1091,11 +1096,21 @@ __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay
 // ordered packet walk, for UNIFORM on a tree that admits it).
 template <bool UNIFORM, bool FAST, bool COUNT, bool LPF = true>
 __device__ __forceinline__ void closest_hit(const DevScene& sc, const Ray& ray, bool active, float& best_t,
-                                            int& best_s, Counters& cnt)
+                                            int& best_s, Counters& cnt, uint32_t* wstk = nullptr)
 {
     const bool gen = active && slab_ray(ray).generic;
     if (UNIFORM && FAST && sc.ordered) {
         closest_packet_ordered<FAST, COUNT>(sc, ray, active && !gen, best_t, best_s, cnt);
+    } else if (!UNIFORM && FAST && sc.wide && wstk) {
+        // the bounce kernel's walk (wstk: a kWideStack-entry LDS column)
+        const SlabRay sr = slab_ray(ray);
+        const SphRay sp = sph_ray(ray);
+        Prune pr = prune_off();
+        best_t = INFINITY;
+        best_s = -1;
+        WideWalk w = wide_walk_start(active && !gen);
+        while (__ballot(wide_walking(w)))
+            if (wide_walking(w)) wide_lane_step<FAST, COUNT>(sc, sr, sp, pr, w, wstk, best_t, best_s, cnt);
     } else if (!UNIFORM && FAST && sc.ordered) {
         const SlabRay sr = slab_ray(ray);
         const SphRay sp = sph_ray(ray);
@@ -1229,7 +1244,8 @@ enum Trav { kTravUniform = 0, kTravLane = 1, kTravHybrid = 2, kTravLaneNP = 3, k
 // thread, to keep them out of the register budget.
 template <int TRAV, bool FAST, bool COUNT>
 __device__ __forceinline__ uint32_t trace_path(const DevScene& sc, Ray ray, bool alive, int depth, bool use_bvh,
-                                               uint64_t key, Counters& cnt, uint32_t* cstack, int cstride)
+                                               uint64_t key, Counters& cnt, uint32_t* cstack, int cstride,
+                                               uint32_t* wstk = nullptr)
 {
     int levels = 0;
     uint32_t tail = 255u << 24;  // renderer.c:23-24 depth exhausted -> (0,0,0,255)
@@ -1245,7 +1261,7 @@ __device__ __forceinline__ uint32_t trace_path(const DevScene& sc, Ray ray, bool
             if (TRAV == kTravUniform || ((TRAV == kTravHybrid || TRAV == kTravHybridNP) && level == 0))
                 closest_hit<true, FAST, COUNT>(sc, ray, alive, t, s, cnt);
             else
-                closest_hit<false, FAST, COUNT, lpf>(sc, ray, alive, t, s, cnt);
+                closest_hit<false, FAST, COUNT, lpf>(sc, ray, alive, t, s, cnt, wstk);
         } else {
             closest_brute<FAST, COUNT>(sc, ray, alive, t, s, cnt);
         }
