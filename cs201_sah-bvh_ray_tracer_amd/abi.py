@@ -121,10 +121,12 @@ SIGNATURES = [
     ("mirt_wave_stats", I, [P, P, P, P, I]),
     ("mirt_last_kernel_ms", C.c_float, [P]),
     ("mirt_last_phase_ms", I, [P, C.POINTER(C.c_float)]),
+    ("mirt_bounce_stats", I, [P, P, P, P, I]),
     ("mirt_set_option", I, [P, I, I]),
     ("mirt_get_option", I, [P, I]),
 ]
 
 OPT_TRAVERSAL, OPT_FAST_SLAB, OPT_BLOCK_WAVES, OPT_DEFER, OPT_BOUNCE_THRESHOLD, OPT_PRUNE, OPT_ORDERED, OPT_WIDE = (
     1, 2, 3, 4, 5, 6, 7, 8)
+OPT_BOUNCE_BLOCKS = 9
 TRAV_UNIFORM, TRAV_LANE, TRAV_HYBRID, TRAV_LANE_NP, TRAV_HYBRID_NP, TRAV_WAVEFRONT = 0, 1, 2, 3, 4, 5

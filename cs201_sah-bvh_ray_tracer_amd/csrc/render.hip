@@ -345,11 +345,18 @@ struct BounceWalk<2> {
     }
 };
 
-template <bool FAST, int WALK>
-__global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
+// DIAG (mirt_bounce_stats): per wave {loop iterations, walking lanes summed
+// over them, the same two after the queue ran dry, start / queue-dry / end
+// time (100 MHz clock), longest chain << 32 | longest walk (in steps)}.
+template <bool FAST, int WALK, bool DIAG = false>
+__global__ __launch_bounds__(256, 5) void bounce_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
                                                      float* __restrict__ acc, const BounceRec* __restrict__ queue,
-                                                     uint32_t* __restrict__ qctl, int threshold)
+                                                     uint32_t* __restrict__ qctl, int threshold,
+                                                     uint64_t* __restrict__ diag = nullptr)
 {
+    uint64_t dg_it = 0, dg_lanes = 0, dg_it_x = 0, dg_lanes_x = 0, dg_tx = 0;
+    const uint64_t dg_t0 = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
+    uint32_t dg_steps = 0, dg_chain = 0, dg_walk_max = 0, dg_chain_max = 0;
     __shared__ uint32_t cstack[kMaxDepth * 256];
     __shared__ uint32_t wstack[WALK == 2 ? kWideStack * kWideStride : 1];
     uint32_t* cs = cstack + threadIdx.x;
@@ -399,6 +406,7 @@ __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, 
             }
         }
         if (!__ballot(has)) break;
+        if (DIAG && exhausted && !dg_tx) dg_tx = __builtin_amdgcn_s_memrealtime();
         // walk until few lanes are still walking and the others can make progress
         for (;;) {
             const uint64_t walking = __ballot(has && w.walking());
@@ -406,10 +414,24 @@ __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, 
             if (__popcll(walking) < threshold &&
                 (__ballot(has && !w.walking()) || (!exhausted && __ballot(!has))))
                 break;
+            if (DIAG) {
+                dg_it++;
+                dg_lanes += __popcll(walking);
+                if (exhausted) {
+                    dg_it_x++;
+                    dg_lanes_x += __popcll(walking);
+                }
+                if (has && w.walking()) dg_steps++;
+            }
             if (has && w.walking()) w.template step<FAST>(sc, sr, sp, pr, stk, best_t, best_s, cnt);
         }
         // shade every lane whose ray is done (renderer.c:46-77 for that level)
         if (has && !w.walking()) {
+            if (DIAG) {
+                dg_walk_max = max(dg_walk_max, dg_steps);
+                dg_chain += dg_steps;
+                dg_steps = 0;
+            }
             bool finish = true;
             uint32_t tail = 255u << 24;          // depth exhausted: black (renderer.c:23-24)
             int stored = level - 1;
@@ -440,7 +462,28 @@ __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, 
                 for (int l = stored - 1; l >= 0; l--) c = blend_rgba(cs[l * 256], c);
                 store_pixel(f, out, acc, pixel, blend_rgba(base0, c));
                 has = false;
+                if (DIAG) {
+                    dg_chain_max = max(dg_chain_max, dg_chain);
+                    dg_chain = 0;
+                }
             }
+        }
+    }
+    if (DIAG) {
+        for (int o = 32; o; o >>= 1) {
+            dg_walk_max = max(dg_walk_max, (uint32_t)__shfl_xor((int)dg_walk_max, o));
+            dg_chain_max = max(dg_chain_max, (uint32_t)__shfl_xor((int)dg_chain_max, o));
+        }
+        if ((threadIdx.x & 63) == 0) {
+            uint64_t* d = diag + 8 * (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+            d[0] = dg_it;
+            d[1] = dg_lanes;
+            d[2] = dg_it_x;
+            d[3] = dg_lanes_x;
+            d[4] = dg_t0;
+            d[5] = dg_tx;
+            d[6] = __builtin_amdgcn_s_memrealtime();
+            d[7] = ((uint64_t)dg_chain_max << 32) | dg_walk_max;
         }
     }
 }
@@ -590,6 +633,7 @@ struct mirt_ctx {
     float r_max = 0.0f, c_max = 0.0f;
     int bounce_threshold = 40;  // wavefront: shade finished rays once fewer lanes walk
     int bounce_blocks = 0;      // wavefront: persistent workgroups (set in mirt_create)
+    int bounce_blocks_opt = 0;  // MIRT_OPT_BOUNCE_BLOCKS override (0: occupancy x CUs)
     void* d_queue = nullptr;    // wavefront: {count, head} + bounce records
     size_t queue_cap = 0;
     uint32_t* d_defer = nullptr;  // [count, list...]
@@ -856,7 +900,7 @@ void dispatch_render(int trav, bool fast, const DevScene& sc, const FrameConst& 
 }
 
 int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_acc, hipStream_t s, bool timed,
-                  mirt_counts* d_counts, uint32_t* d_wave_stats = nullptr)
+                  mirt_counts* d_counts, uint32_t* d_wave_stats = nullptr, uint64_t* d_bdiag = nullptr)
 {
     const int tiles = ((f.width + 7) / 8) * ((f.num_rows + 7) / 8);
     const int bw = c->block_waves;
@@ -889,23 +933,33 @@ int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_ac
         BounceRec* queue = (BounceRec*)((char*)c->d_queue + 64);
         HIP_TRY(hipMemsetAsync(qctl, 0, 8, s));
         const int pblocks = (tiles + 3) / 4 + dfr.blocks;
+        const int bblocks = c->bounce_blocks_opt ? c->bounce_blocks_opt : c->bounce_blocks;
         if (c->fast_slab)
             primary_kernel<true><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
         else
             primary_kernel<false><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ph1, s));
-        if (c->fast_slab && sc.wide)
-            bounce_kernel<true, 2><<<c->bounce_blocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
+        if (d_bdiag && sc.wide)
+            bounce_kernel<true, 2, true><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
+                                                                        c->bounce_threshold, d_bdiag);
+        else if (d_bdiag && sc.ordered)
+            bounce_kernel<true, 1, true><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
+                                                                        c->bounce_threshold, d_bdiag);
+        else if (d_bdiag)
+            bounce_kernel<true, 0, true><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
+                                                                        c->bounce_threshold, d_bdiag);
+        else if (c->fast_slab && sc.wide)
+            bounce_kernel<true, 2><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
                                                                   c->bounce_threshold);
         else if (c->fast_slab && sc.ordered)
-            bounce_kernel<true, 1><<<c->bounce_blocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
+            bounce_kernel<true, 1><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
                                                                   c->bounce_threshold);
         else if (c->fast_slab)
-            bounce_kernel<true, 0><<<c->bounce_blocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
+            bounce_kernel<true, 0><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
                                                                   c->bounce_threshold);
         else
-            bounce_kernel<false, 0><<<c->bounce_blocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
+            bounce_kernel<false, 0><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
                                                                    c->bounce_threshold);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ph2, s));
@@ -1174,6 +1228,28 @@ int mirt_wave_stats(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* 
     return waves;
 }
 
+int mirt_bounce_stats(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, uint64_t* out, int cap)
+{
+    if (!ctx_ok(c, true, "mirt_bounce_stats")) return MIRT_E_NOSCENE;
+    if (!cam || !frame_desc_valid(fd) || !fd->use_bvh || fd->max_depth < 2 || c->trav != kTravWavefront) {
+        set_error("mirt_bounce_stats: needs a BVH frame of depth >= 2 under the wavefront schedule");
+        return MIRT_E_INVALID;
+    }
+    const int waves = (c->bounce_blocks_opt ? c->bounce_blocks_opt : c->bounce_blocks) * 4;
+    if (!out || cap < waves) return -waves;
+    FrameConst f = make_frame_const(cam, fd);
+    f.accumulate = 0;
+    const size_t pixels = (size_t)f.num_rows * f.width;
+    int rc = ensure((void**)&c->d_out, &c->out_cap, pixels * 4 + 4);
+    if (!rc) rc = ensure(&c->d_res, &c->res_cap, 64 * (size_t)waves + 64);
+    if (rc) return rc;
+    rc = launch_render(c, f, c->d_out, nullptr, c->stream, false, nullptr, nullptr, (uint64_t*)c->d_res);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(out, c->d_res, 64 * (size_t)waves, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return waves;
+}
+
 int mirt_camera_rays(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, mirt_ray* out)
 {
     if (!ctx_ok(c, false, "mirt_camera_rays")) return MIRT_E_INVALID;
@@ -1356,6 +1432,10 @@ int mirt_set_option(mirt_ctx* c, int option, int value)
     case MIRT_OPT_WIDE:
         c->wide = value != 0;
         return MIRT_OK;
+    case MIRT_OPT_BOUNCE_BLOCKS:
+        if (value < 0) break;
+        c->bounce_blocks_opt = value;
+        return MIRT_OK;
     case MIRT_OPT_BLOCK_WAVES:
         if (value != 1 && value != 2 && value != 4 && value != 8) break;
         c->block_waves = value;
@@ -1378,6 +1458,7 @@ int mirt_get_option(mirt_ctx* c, int option)
     if (option == MIRT_OPT_PRUNE) return c->prune;
     if (option == MIRT_OPT_ORDERED) return c->ordered;
     if (option == MIRT_OPT_WIDE) return c->wide;
+    if (option == MIRT_OPT_BOUNCE_BLOCKS) return c->bounce_blocks_opt;
     set_error("mirt_get_option: bad option %d", option);
     return MIRT_E_INVALID;
 }

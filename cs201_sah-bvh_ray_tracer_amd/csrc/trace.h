@@ -1018,19 +1018,12 @@ __device__ __forceinline__ bool slab_cons(const SlabRay& r, const Prune& p, floa
     return !(tmax - tmin < -m || tmax - kEps < -m);
 }
 
-// One HNode slot for one lane. Returns whether the walk should enter it.
-// COUNT: a slot test counts as a node test, a leaf's exact gate does not
-// (it re-tests the same node), a sphere test as a sphere test.
+// The leaf gate of a leaf slot whose fp16 box passed: its exact box under
+// hit.c's test, then its sphere. COUNT: the sphere test counts.
 template <bool FAST, bool COUNT>
-__device__ __forceinline__ bool wide_slot(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
-                                          uint32_t ref, uint32_t bx, uint32_t by, uint32_t bz, float& near,
-                                          float& best_t, int& best_s, Counters& cnt)
+__device__ __forceinline__ void wide_leaf(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
+                                          uint32_t ref, float& best_t, int& best_s, Counters& cnt)
 {
-    if (ref == kPNone) return false;
-    if (COUNT) cnt.nodes++;
-    if (!slab_cons(sr, pr, h_lo(bx), h_lo(by), h_lo(bz), h_hi(bx), h_hi(by), h_hi(bz), near)) return false;
-    if (!(ref & kPLeaf)) return true;
-    // the leaf's gate: its exact box under hit.c's test, then its sphere
     const float4* lp = (const float4*)(sc.leaves + (ref & ~kPLeaf));
     const float4 l0 = lp[0], l1 = lp[1], g = lp[2];
     float e;
@@ -1038,7 +1031,6 @@ __device__ __forceinline__ bool wide_slot(const DevScene& sc, const SlabRay& sr,
         if (COUNT) cnt.spheres++;
         consider_sphere<FAST>(sc, sp, pr, sr.ox, sr.oy, sr.oz, __float_as_int(l1.z), g, best_t, best_s);
     }
-    return false;
 }
 
 template <bool FAST, bool COUNT>
@@ -1056,11 +1048,35 @@ __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay
     }
     const uint4* p = (const uint4*)(sc.hnodes + w.cur);
     const uint4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+    // 1. the four conservative slot tests (COUNT: a slot test is a node test)
     float e0 = 0.0f, e1 = 0.0f, e2 = 0.0f, e3 = 0.0f;
-    const bool h0 = wide_slot<FAST, COUNT>(sc, sr, sp, pr, q3.x, q0.x, q0.y, q0.z, e0, best_t, best_s, cnt);
-    const bool h1 = wide_slot<FAST, COUNT>(sc, sr, sp, pr, q3.y, q0.w, q1.x, q1.y, e1, best_t, best_s, cnt);
-    const bool h2 = wide_slot<FAST, COUNT>(sc, sr, sp, pr, q3.z, q1.z, q1.w, q2.x, e2, best_t, best_s, cnt);
-    const bool h3 = wide_slot<FAST, COUNT>(sc, sr, sp, pr, q3.w, q2.y, q2.z, q2.w, e3, best_t, best_s, cnt);
+    auto test = [&](uint32_t ref, uint32_t bx, uint32_t by, uint32_t bz, float& e) {
+        if (ref == kPNone) return false;
+        if (COUNT) cnt.nodes++;
+        return slab_cons(sr, pr, h_lo(bx), h_lo(by), h_lo(bz), h_hi(bx), h_hi(by), h_hi(bz), e);
+    };
+    bool h0 = test(q3.x, q0.x, q0.y, q0.z, e0);
+    bool h1 = test(q3.y, q0.w, q1.x, q1.y, e1);
+    bool h2 = test(q3.z, q1.z, q1.w, q2.x, e2);
+    bool h3 = test(q3.w, q2.y, q2.z, q2.w, e3);
+    // 2. passing leaf slots, one at a time (the node's boxes are dead here)
+    if (h0 && (q3.x & kPLeaf)) {
+        wide_leaf<FAST, COUNT>(sc, sr, sp, pr, q3.x, best_t, best_s, cnt);
+        h0 = false;
+    }
+    if (h1 && (q3.y & kPLeaf)) {
+        wide_leaf<FAST, COUNT>(sc, sr, sp, pr, q3.y, best_t, best_s, cnt);
+        h1 = false;
+    }
+    if (h2 && (q3.z & kPLeaf)) {
+        wide_leaf<FAST, COUNT>(sc, sr, sp, pr, q3.z, best_t, best_s, cnt);
+        h2 = false;
+    }
+    if (h3 && (q3.w & kPLeaf)) {
+        wide_leaf<FAST, COUNT>(sc, sr, sp, pr, q3.w, best_t, best_s, cnt);
+        h3 = false;
+    }
+    // 3. passing inner slots: nearest next, the others pushed farthest first
     const uint32_t n = (uint32_t)h0 + (uint32_t)h1 + (uint32_t)h2 + (uint32_t)h3;
     if (n == 0) {
         wide_walk_pop(w, stk);
@@ -1072,8 +1088,8 @@ __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay
         w.end = ax.end;
         return;
     }
-    // sort the passing slots by entry, nearest first; failing slots get +inf
-    // and passing ones a finite key, so the n passing slots come first
+    // failing slots get +inf keys and passing ones a finite key, so the n
+    // passing slots sort first
     constexpr float big = 3.0e38f;
     float k0 = h0 ? fminf(e0, big) : INFINITY, k1 = h1 ? fminf(e1, big) : INFINITY;
     float k2 = h2 ? fminf(e2, big) : INFINITY, k3 = h3 ? fminf(e3, big) : INFINITY;

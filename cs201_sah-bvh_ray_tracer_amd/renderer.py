@@ -215,6 +215,18 @@ class Renderer:
     def get_option(self, option):
         return check(self.L.mirt_get_option(self.h, option), "mirt_get_option")
 
+    def bounce_stats(self, cam, width, height, depth=5, seed=1, sample=0):
+        """Per-wave diagnostic of the bounce kernel: uint64 array of (iterations,
+        walking lanes summed, iterations after the queue ran dry, their lanes,
+        t_start, t_dry, t_end [10 ns ticks], longest chain << 32 | longest walk)."""
+        fd = frame_desc(width, height, depth, True, seed, sample, False, 1, 8, 0, 1)
+        n = -self.L.mirt_bounce_stats(self.h, C.byref(cam), C.byref(fd), None, 0)
+        if n <= 0:
+            check(-n, "mirt_bounce_stats")
+        out = np.zeros((n, 8), np.uint64)
+        check(self.L.mirt_bounce_stats(self.h, C.byref(cam), C.byref(fd), ptr(out), n), "mirt_bounce_stats")
+        return out
+
     def wave_stats(self, cam, width, height, depth=5, use_bvh=True, seed=1, sample=0, row_block=8, shard=0,
                    num_shards=1):
         """Per-wave (8x8 tile) diagnostic: array of (tile, steps, start, end),

@@ -229,6 +229,14 @@ int mirt_count_frame(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_des
    (or -waves if cap is too small). */
 int mirt_wave_stats(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_desc *fd, uint32_t *out, int cap);
 
+/* Diagnostic: renders the frame (depth >= 2, BVH, wavefront schedule) with the
+   instrumented bounce kernel and writes 8 uint64 per bounce wave: loop
+   iterations, walking lanes summed over them, the same two after the bounce
+   queue ran dry, start / queue-dry / end time (100 MHz clock), and
+   longest chain << 32 | longest walk (steps). Returns the number of waves
+   (or -waves if cap is too small). */
+int mirt_bounce_stats(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_desc *fd, uint64_t *out, int cap);
+
 /* Device time (ms) of the last render kernel launched by a blocking call. */
 float mirt_last_kernel_ms(mirt_ctx *ctx);
 
@@ -265,7 +273,8 @@ int mirt_last_phase_ms(mirt_ctx *ctx, float *phase);
 enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3, MIRT_OPT_DEFER = 4,
        MIRT_OPT_BOUNCE_THRESHOLD = 5, /* wavefront: shade finished bounce rays once fewer than
                                          this many lanes of a wave still walk (0..64, default 40) */
-       MIRT_OPT_PRUNE = 6, MIRT_OPT_ORDERED = 7, MIRT_OPT_WIDE = 8 };
+       MIRT_OPT_PRUNE = 6, MIRT_OPT_ORDERED = 7, MIRT_OPT_WIDE = 8,
+       MIRT_OPT_BOUNCE_BLOCKS = 9  /* wavefront: persistent bounce workgroups, 0 = occupancy x CUs */ };
 enum { MIRT_TRAV_UNIFORM = 0, MIRT_TRAV_LANE = 1, MIRT_TRAV_HYBRID = 2, MIRT_TRAV_LANE_NP = 3,
        MIRT_TRAV_HYBRID_NP = 4,  /* *_NP: per-lane walk without successor prefetch */
        MIRT_TRAV_WAVEFRONT = 5   /* default: camera-ray packets, then persistent per-lane
