@@ -993,16 +993,13 @@ __device__ __forceinline__ float h_lo(uint32_t v) { return (float)__builtin_bit_
 __device__ __forceinline__ float h_hi(uint32_t v) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(v >> 16)); }
 
 // Conservative box test: passes whenever hit.c's slab test on this box
-// would (slab_fast's margins, with "undecided" counted as a pass; the exact
-// division test for rays with a zero/tiny component), and also applies the
-// pruning bound, which holds for any box containing the subtree.
-__device__ __forceinline__ bool slab_cons(const SlabRay& r, const Prune& p, float x0, float y0, float z0, float x1,
-                                          float y1, float z1, float& near)
+// would (slab_fast's margins, with "undecided" counted as a pass), and also
+// applies the pruning bound, which holds for any box containing the subtree.
+// Branch-free, valid for rays without a zero/tiny direction component
+// (slab_cons handles those with the exact division test).
+__device__ __forceinline__ bool slab_cons_fast(const SlabRay& r, const Prune& p, float x0, float y0, float z0,
+                                               float x1, float y1, float z1, float& near)
 {
-    if (r.generic) {
-        near = 0.0f;
-        return slab_test(r, x0, y0, z0, x1, y1, z1);
-    }
     const float tx1 = (x0 - r.ox) * r.ix, tx2 = (x1 - r.ox) * r.ix;
     const float ty1 = (y0 - r.oy) * r.iy, ty2 = (y1 - r.oy) * r.iy;
     const float tz1 = (z0 - r.oz) * r.iz, tz2 = (z1 - r.oz) * r.iz;
@@ -1010,12 +1007,22 @@ __device__ __forceinline__ bool slab_cons(const SlabRay& r, const Prune& p, floa
     constexpr float c = 1.0f - 0x1p-20f;
     const float entry = fmaxf(fmaf(nx, c, -(p.m * fabsf(r.ix))),
                               fmaxf(fmaf(ny, c, -(p.m * fabsf(r.iy))), fmaf(nz, c, -(p.m * fabsf(r.iz)))));
-    if (entry > p.lim) return false;
     const float tmin = fmaxf(nx, fmaxf(ny, nz));
     const float tmax = fminf(fmaxf(tx1, tx2), fminf(fmaxf(ty1, ty2), fmaxf(tz1, tz2)));
     near = tmin;
     const float m = (fabsf(tmin) + fabsf(tmax)) * 0x1p-20f;
-    return !(tmax - tmin < -m || tmax - kEps < -m);
+    return !(entry > p.lim) & !(tmax - tmin < -m) & !(tmax - kEps < -m);
+}
+
+__device__ __forceinline__ bool slab_cons(const SlabRay& r, const Prune& p, float x0, float y0, float z0, float x1,
+                                          float y1, float z1, float& near)
+{
+    bool pass = slab_cons_fast(r, p, x0, y0, z0, x1, y1, z1, near);
+    if (r.generic) {  // a lane branch taken only by rays with a zero/tiny component
+        near = 0.0f;
+        pass = slab_test(r, x0, y0, z0, x1, y1, z1);
+    }
+    return pass;
 }
 
 // The leaf gate of a leaf slot whose fp16 box passed: its exact box under
@@ -1048,12 +1055,13 @@ __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay
     }
     const uint4* p = (const uint4*)(sc.hnodes + w.cur);
     const uint4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
-    // 1. the four conservative slot tests (COUNT: a slot test is a node test)
+    // 1. the four conservative slot tests, computed for every slot (no branch
+    // for the compiler to sink a load into); COUNT: a slot test is a node test
     float e0 = 0.0f, e1 = 0.0f, e2 = 0.0f, e3 = 0.0f;
     auto test = [&](uint32_t ref, uint32_t bx, uint32_t by, uint32_t bz, float& e) {
-        if (ref == kPNone) return false;
-        if (COUNT) cnt.nodes++;
-        return slab_cons(sr, pr, h_lo(bx), h_lo(by), h_lo(bz), h_hi(bx), h_hi(by), h_hi(bz), e);
+        if (COUNT && ref != kPNone) cnt.nodes++;
+        const bool pass = slab_cons(sr, pr, h_lo(bx), h_lo(by), h_lo(bz), h_hi(bx), h_hi(by), h_hi(bz), e);
+        return pass & (ref != kPNone);
     };
     bool h0 = test(q3.x, q0.x, q0.y, q0.z, e0);
     bool h1 = test(q3.y, q0.w, q1.x, q1.y, e1);
