@@ -1067,22 +1067,22 @@ __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay
     bool h1 = test(q3.y, q0.w, q1.x, q1.y, e1);
     bool h2 = test(q3.z, q1.z, q1.w, q2.x, e2);
     bool h3 = test(q3.w, q2.y, q2.z, q2.w, e3);
-    // 2. passing leaf slots, one at a time (the node's boxes are dead here)
-    if (h0 && (q3.x & kPLeaf)) {
-        wide_leaf<FAST, COUNT>(sc, sr, sp, pr, q3.x, best_t, best_s, cnt);
-        h0 = false;
-    }
-    if (h1 && (q3.y & kPLeaf)) {
-        wide_leaf<FAST, COUNT>(sc, sr, sp, pr, q3.y, best_t, best_s, cnt);
-        h1 = false;
-    }
-    if (h2 && (q3.z & kPLeaf)) {
-        wide_leaf<FAST, COUNT>(sc, sr, sp, pr, q3.z, best_t, best_s, cnt);
-        h2 = false;
-    }
-    if (h3 && (q3.w & kPLeaf)) {
-        wide_leaf<FAST, COUNT>(sc, sr, sp, pr, q3.w, best_t, best_s, cnt);
-        h3 = false;
+    // 2. passing leaf slots (the node's boxes are dead here): each lane works
+    // through its own list, so the gate code runs max-over-lanes times
+    // instead of once per slot that any lane passes
+    uint32_t lm = (uint32_t)(h0 && (q3.x & kPLeaf)) | (uint32_t)(h1 && (q3.y & kPLeaf)) << 1 |
+                  (uint32_t)(h2 && (q3.z & kPLeaf)) << 2 | (uint32_t)(h3 && (q3.w & kPLeaf)) << 3;
+    h0 = h0 && !(lm & 1);
+    h1 = h1 && !(lm & 2);
+    h2 = h2 && !(lm & 4);
+    h3 = h3 && !(lm & 8);
+    while (__ballot(lm != 0)) {
+        if (lm) {
+            const uint32_t i = __builtin_ctz(lm);
+            lm &= lm - 1;
+            const uint32_t ref = i == 0 ? q3.x : i == 1 ? q3.y : i == 2 ? q3.z : q3.w;
+            wide_leaf<FAST, COUNT>(sc, sr, sp, pr, ref, best_t, best_s, cnt);
+        }
     }
     // 3. passing inner slots: nearest next, the others pushed farthest first
     const uint32_t n = (uint32_t)h0 + (uint32_t)h1 + (uint32_t)h2 + (uint32_t)h3;
