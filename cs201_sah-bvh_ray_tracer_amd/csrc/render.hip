@@ -348,22 +348,81 @@ struct BounceWalk<2> {
 // DIAG (mirt_bounce_stats): per wave {loop iterations, walking lanes summed
 // over them, the same two after the queue ran dry, start / queue-dry / end
 // time (100 MHz clock), longest chain << 32 | longest walk (in steps)}.
+template <>
+struct BounceWalk<3> {
+    QuadWalk w;
+    __device__ void start(const DevScene&) { w = QuadWalk{0u, 0u, 0u}; }
+    __device__ void stop() { w = QuadWalk{kPNone, 0u, 0u}; }
+    __device__ bool walking() const { return w.cur != kPNone; }
+    template <bool FAST>
+    __device__ void step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr, uint32_t* stk,
+                         float& bt, int& bs, Counters&)
+    {
+        quad_step<FAST>(sc, sr, sp, pr, w, stk, bt, bs);
+    }
+};
+
+// The shading of one lane whose walk for this level is done (renderer.c:46-77
+// for that level): returns true if the chain goes on (ray re-aimed); else the
+// pixel's colour is folded from the colour stack and stored (if `store`).
+__device__ __forceinline__ bool shade_level(const DevScene& sc, const FrameConst& f, Ray& ray, float best_t,
+                                            int best_s, int& level, uint32_t& k, uint64_t key, uint32_t* cs,
+                                            int cstride, uint32_t base0, uint32_t pixel, uint32_t* __restrict__ out,
+                                            float* __restrict__ acc, bool store)
+{
+    uint32_t tail = 255u << 24;  // depth exhausted: black (renderer.c:23-24)
+    int stored = level - 1;
+    if (best_s < 0) {
+        tail = sky_rgba(ray.dy);
+    } else {
+        cs[(level - 1) * cstride] = sc.color[best_s];
+        stored = level;
+        if (level + 1 < f.depth) {  // trace_ray(bounce, depth - 1) still has depth
+            const float4 g = sc.geo[best_s];
+            float p[3], nn[3];
+            hit_point_normal(ray, best_t, g, p, nn);
+            float bx, by, bz;
+            hemisphere(key, k, nn, bx, by, bz);
+            ray = Ray{p[0], p[1], p[2], bx, by, bz};
+            level++;
+            return true;
+        }
+    }
+    uint32_t c = tail;
+    for (int l = stored - 1; l >= 0; l--) c = blend_rgba(cs[l * cstride], c);
+    if (store) store_pixel(f, out, acc, pixel, blend_rgba(base0, c));
+    return false;
+}
+
+// Persistent bounce pass: each lane (WALK 3: each quad of lanes) owns one
+// pixel's chain of bounces, refilled from the primary pass's queue. WALK 2
+// (default) ends with a QUAD DRAIN: once the queue is dry and at most 16 of
+// a wave's lanes are still busy, their chains move to quads (registers by
+// ds_bpermute; the LDS stacks stay in the source lane's columns) and are
+// finished four lanes per ray -- a sparse wave costs full issue slots per
+// step, so four lanes per ray make the drain's steps about four times
+// shorter at no extra cost.
 template <bool FAST, int WALK, bool DIAG = false>
 __global__ __launch_bounds__(256, 5) void bounce_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
                                                      float* __restrict__ acc, const BounceRec* __restrict__ queue,
-                                                     uint32_t* __restrict__ qctl, int threshold,
+                                                     uint32_t* __restrict__ qctl, int threshold, int quad_drain,
                                                      uint64_t* __restrict__ diag = nullptr)
 {
     uint64_t dg_it = 0, dg_lanes = 0, dg_it_x = 0, dg_lanes_x = 0, dg_tx = 0;
     const uint64_t dg_t0 = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
     uint32_t dg_steps = 0, dg_chain = 0, dg_walk_max = 0, dg_chain_max = 0;
-    __shared__ uint32_t cstack[kMaxDepth * 256];
-    __shared__ uint32_t wstack[WALK == 2 ? kWideStack * kWideStride : 1];
-    uint32_t* cs = cstack + threadIdx.x;
-    uint32_t* stk = wstack + (WALK == 2 ? threadIdx.x : 0);
+    // WALK 3: one ray per quad of lanes -- its colour stack and walk stack are
+    // per ray (quad); the ray's state is replicated in the quad's lanes
+    constexpr bool QUAD = WALK == 3;
+    constexpr int cstride = QUAD ? kQuadStride : 256;
+    __shared__ uint32_t cstack[kMaxDepth * cstride];
+    __shared__ uint32_t wstack[WALK == 2 ? kWideStack * kWideStride : QUAD ? kQuadStack * kQuadStride : 1];
+    __shared__ uint32_t qsrc[WALK == 2 ? 4 * 16 : 1];  // quad drain: source lane of each quad, per wave
+    const uint32_t slot = QUAD ? threadIdx.x >> 2 : threadIdx.x;
+    uint32_t* cs = cstack + slot;
+    uint32_t* stk = wstack + (WALK >= 2 ? slot : 0);
     Counters cnt{0, 0, 0, 0, 0};
     const uint32_t n = __builtin_amdgcn_readfirstlane(qctl[0]);
-    const uint32_t end = sc.num_nodes;
     bool has = false, exhausted = false;
     Ray ray{0, 0, 0, 0, 0, 0};
     SlabRay sr = slab_ray(ray);
@@ -377,7 +436,8 @@ __global__ __launch_bounds__(256, 5) void bounce_kernel(DevScene sc, FrameConst 
     uint64_t key = 0;
     for (;;) {
         // refill lanes that own no chain (one atomic per wave, tile order kept)
-        const uint64_t need = __ballot(!has);
+        const uint64_t need_all = __ballot(!has);
+        const uint64_t need = QUAD ? (need_all & 0x1111111111111111ull) : need_all;  // one per ray
         if (need && !exhausted) {
             const int leader = __builtin_ctzll(need);
             uint32_t b = 0;
@@ -385,7 +445,8 @@ __global__ __launch_bounds__(256, 5) void bounce_kernel(DevScene sc, FrameConst 
             b = __builtin_amdgcn_readlane(b, leader);
             if (b + (uint32_t)__popcll(need) >= n) exhausted = true;
             if (!has) {
-                const uint32_t idx = b + lanes_below(need);
+                const uint32_t lane0 = QUAD ? (threadIdx.x & 60) : (threadIdx.x & 63);
+                const uint32_t idx = b + (uint32_t)__popcll(need & ((1ull << lane0) - 1));
                 if (idx < n) {
                     const BounceRec rec = queue[idx];
                     ray = Ray{rec.ox, rec.oy, rec.oz, rec.dx, rec.dy, rec.dz};
@@ -407,6 +468,7 @@ __global__ __launch_bounds__(256, 5) void bounce_kernel(DevScene sc, FrameConst 
         }
         if (!__ballot(has)) break;
         if (DIAG && exhausted && !dg_tx) dg_tx = __builtin_amdgcn_s_memrealtime();
+        if (WALK == 2 && quad_drain && exhausted && __popcll(__ballot(has)) <= 16) break;  // -> quad drain
         // walk until few lanes are still walking and the others can make progress
         for (;;) {
             const uint64_t walking = __ballot(has && w.walking());
@@ -425,46 +487,77 @@ __global__ __launch_bounds__(256, 5) void bounce_kernel(DevScene sc, FrameConst 
             }
             if (has && w.walking()) w.template step<FAST>(sc, sr, sp, pr, stk, best_t, best_s, cnt);
         }
-        // shade every lane whose ray is done (renderer.c:46-77 for that level)
+        // shade every lane whose ray is done
         if (has && !w.walking()) {
             if (DIAG) {
                 dg_walk_max = max(dg_walk_max, dg_steps);
                 dg_chain += dg_steps;
                 dg_steps = 0;
             }
-            bool finish = true;
-            uint32_t tail = 255u << 24;          // depth exhausted: black (renderer.c:23-24)
-            int stored = level - 1;
-            if (best_s < 0) {
-                tail = sky_rgba(ray.dy);
+            if (shade_level(sc, f, ray, best_t, best_s, level, k, key, cs, cstride, base0, pixel, out, acc,
+                            !QUAD || (threadIdx.x & 3) == 0)) {
+                sr = slab_ray(ray);
+                sp = sph_ray(ray);
+                w.start(sc);
+                best_t = INFINITY;
+                best_s = -1;
+                pr = prune_off();
             } else {
-                cs[(level - 1) * 256] = sc.color[best_s];
-                stored = level;
-                if (level + 1 < f.depth) {       // trace_ray(bounce, depth - 1) still has depth
-                    const float4 g = sc.geo[best_s];
-                    float p[3], nn[3];
-                    hit_point_normal(ray, best_t, g, p, nn);
-                    float bx, by, bz;
-                    hemisphere(key, k, nn, bx, by, bz);
-                    ray = Ray{p[0], p[1], p[2], bx, by, bz};
-                    sr = slab_ray(ray);
-                    sp = sph_ray(ray);
-                    w.start(sc);
-                    best_t = INFINITY;
-                    best_s = -1;
-                    pr = prune_off();
-                    level++;
-                    finish = false;
-                }
-            }
-            if (finish) {
-                uint32_t c = tail;
-                for (int l = stored - 1; l >= 0; l--) c = blend_rgba(cs[l * 256], c);
-                store_pixel(f, out, acc, pixel, blend_rgba(base0, c));
                 has = false;
                 if (DIAG) {
                     dg_chain_max = max(dg_chain_max, dg_chain);
                     dg_chain = 0;
+                }
+            }
+        }
+    }
+    if constexpr (WALK == 2) {
+        // quad drain (uniform control flow here: every lane is active)
+        const uint64_t busy = __ballot(has);
+        if (busy) {
+            const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+            if (has) qsrc[wv * 16 + lanes_below(busy)] = lane;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint32_t q = lane >> 2;
+            const bool qhas = q < (uint32_t)__popcll(busy);
+            const uint32_t src = qsrc[wv * 16 + (qhas ? q : 0)];
+            auto pull = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v); };
+            auto pullf = [&](float v) { return __uint_as_float(pull(__float_as_uint(v))); };
+            ray = Ray{pullf(ray.ox), pullf(ray.oy), pullf(ray.oz), pullf(ray.dx), pullf(ray.dy), pullf(ray.dz)};
+            pixel = pull(pixel);
+            k = pull(k);
+            level = (int)pull((uint32_t)level);
+            base0 = pull(base0);
+            key = ((uint64_t)pull((uint32_t)(key >> 32)) << 32) | pull((uint32_t)key);
+            best_t = pullf(best_t);
+            best_s = (int)pull((uint32_t)best_s);
+            pr = Prune{pullf(pr.m), pullf(pr.lim)};
+            const WideWalk& lw = w.w;
+            QuadWalk qw{pull(lw.cur), pull(lw.end), pull(lw.top)};
+            has = qhas;
+            if (!qhas) qw.cur = kPNone;
+            sr = slab_ray(ray);
+            sp = sph_ray(ray);
+            // the ray's LDS stacks stay in its source lane's columns
+            uint32_t* qstk = wstack + (threadIdx.x & ~63u) + src;
+            uint32_t* qcs = cstack + (threadIdx.x & ~63u) + src;
+            while (__ballot(has)) {
+                if (has && qw.cur != kPNone)
+                    quad_step<FAST, kWideStride, kWideStack>(sc, sr, sp, pr, qw, qstk, best_t, best_s);
+                if (has && qw.cur == kPNone) {
+                    if (shade_level(sc, f, ray, best_t, best_s, level, k, key, qcs, kWideStride, base0, pixel, out,
+                                    acc, (lane & 3) == 0)) {
+                        sr = slab_ray(ray);
+                        sp = sph_ray(ray);
+                        qw = QuadWalk{0u, 0u, 0u};
+                        best_t = INFINITY;
+                        best_s = -1;
+                        pr = prune_off();
+                    } else {
+                        has = false;
+                    }
                 }
             }
         }
@@ -631,9 +724,11 @@ struct mirt_ctx {
     LeafRec* d_leaves = nullptr;
     int wide = 1;               // four-wide per-lane walks where the tree admits them
     float r_max = 0.0f, c_max = 0.0f;
-    int bounce_threshold = 40;  // wavefront: shade finished rays once fewer lanes walk
+    int bounce_threshold = 32;  // wavefront: shade finished rays once fewer lanes walk
     int bounce_blocks = 0;      // wavefront: persistent workgroups (set in mirt_create)
     int bounce_blocks_opt = 0;  // MIRT_OPT_BOUNCE_BLOCKS override (0: occupancy x CUs)
+    int quad = 0;               // four-wide bounce walk with one ray per quad of lanes
+    int quad_drain = 1;         // four-wide bounce walk: finish the drain four lanes per ray
     void* d_queue = nullptr;    // wavefront: {count, head} + bounce records
     size_t queue_cap = 0;
     uint32_t* d_defer = nullptr;  // [count, list...]
@@ -805,7 +900,7 @@ void build_hnodes(const mirt_node* nd, int nn, const mirt_sphere* sp, int ns, st
     auto fill = [&](HNode& h, int k, uint32_t ci) {
         const mirt_node& n = nd[ci];
         for (int a = 0; a < 3; a++)
-            h.box[k][a] = (uint32_t)half_down(n.bmin[a]) | ((uint32_t)half_up(n.bmax[a]) << 16);
+            h.slot[k].box[a] = (uint32_t)half_down(n.bmin[a]) | ((uint32_t)half_up(n.bmax[a]) << 16);
         uint32_t ref;
         if (n.skip & MIRT_NODE_EMPTY) {
             ref = kPNone;
@@ -826,15 +921,15 @@ void build_hnodes(const mirt_node* nd, int nn, const mirt_sphere* sp, int ns, st
             todo.push_back(ci);
             ref = (uint32_t)todo.size();
         }
-        h.ref[k] = ref;
+        h.slot[k].ref = ref;
     };
-    for (int k = 0; k < 4; k++) hn[0].ref[k] = kPNone;
+    for (int k = 0; k < 4; k++) hn[0].slot[k].ref = kPNone;
     if (nn == 0) return;
     fill(hn[0], 0, 0);
     for (size_t next = 0; next < todo.size(); next++) {
         const uint32_t y = todo[next];
         HNode h{};
-        for (int k = 0; k < 4; k++) h.ref[k] = kPNone;
+        for (int k = 0; k < 4; k++) h.slot[k].ref = kPNone;
         hn.push_back(h);
         aux.push_back(HAux{y, nd[y].skip & MIRT_SKIP_MASK});
         const uint32_t kids[2] = {y + 1, nd[y + 1].skip & MIRT_SKIP_MASK};
@@ -941,26 +1036,21 @@ int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_ac
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ph1, s));
         if (d_bdiag && sc.wide)
-            bounce_kernel<true, 2, true><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
-                                                                        c->bounce_threshold, d_bdiag);
+            bounce_kernel<true, 2, true><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, d_bdiag);
         else if (d_bdiag && sc.ordered)
-            bounce_kernel<true, 1, true><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
-                                                                        c->bounce_threshold, d_bdiag);
+            bounce_kernel<true, 1, true><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, d_bdiag);
         else if (d_bdiag)
-            bounce_kernel<true, 0, true><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
-                                                                        c->bounce_threshold, d_bdiag);
+            bounce_kernel<true, 0, true><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, d_bdiag);
+        else if (c->fast_slab && sc.wide && c->quad)
+            bounce_kernel<true, 3><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain);
         else if (c->fast_slab && sc.wide)
-            bounce_kernel<true, 2><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
-                                                                  c->bounce_threshold);
+            bounce_kernel<true, 2><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain);
         else if (c->fast_slab && sc.ordered)
-            bounce_kernel<true, 1><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
-                                                                  c->bounce_threshold);
+            bounce_kernel<true, 1><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain);
         else if (c->fast_slab)
-            bounce_kernel<true, 0><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
-                                                                  c->bounce_threshold);
+            bounce_kernel<true, 0><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain);
         else
-            bounce_kernel<false, 0><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl,
-                                                                   c->bounce_threshold);
+            bounce_kernel<false, 0><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ph2, s));
         if (timed) HIP_TRY(hipEventRecord(c->ev1, s));
@@ -1436,6 +1526,12 @@ int mirt_set_option(mirt_ctx* c, int option, int value)
         if (value < 0) break;
         c->bounce_blocks_opt = value;
         return MIRT_OK;
+    case MIRT_OPT_QUAD:
+        c->quad = value != 0;
+        return MIRT_OK;
+    case MIRT_OPT_QUAD_DRAIN:
+        c->quad_drain = value != 0;
+        return MIRT_OK;
     case MIRT_OPT_BLOCK_WAVES:
         if (value != 1 && value != 2 && value != 4 && value != 8) break;
         c->block_waves = value;
@@ -1459,6 +1555,8 @@ int mirt_get_option(mirt_ctx* c, int option)
     if (option == MIRT_OPT_ORDERED) return c->ordered;
     if (option == MIRT_OPT_WIDE) return c->wide;
     if (option == MIRT_OPT_BOUNCE_BLOCKS) return c->bounce_blocks_opt;
+    if (option == MIRT_OPT_QUAD) return c->quad;
+    if (option == MIRT_OPT_QUAD_DRAIN) return c->quad_drain;
     set_error("mirt_get_option: bad option %d", option);
     return MIRT_E_INVALID;
 }

@@ -77,8 +77,10 @@ static_assert(sizeof(PNode) == 64, "ordered node is 64 B");
 // inner HNode index, kPLeaf | LeafRec index, or kPNone. HAux holds the
 // node's flat DFS segment [flat + 1, end), read only when the stack is full.
 struct __attribute__((aligned(64))) HNode {
-    uint32_t box[4][3];  // per slot and axis: fp16 lo (bits 0-15) | fp16 hi (bits 16-31)
-    uint32_t ref[4];
+    struct Slot {
+        uint32_t box[3];  // per axis: fp16 lo (bits 0-15) | fp16 hi (bits 16-31)
+        uint32_t ref;
+    } slot[4];            // 16 B per slot: one dwordx4 each
 };
 static_assert(sizeof(HNode) == 64, "wide node is 64 B");
 struct HAux {
@@ -1054,19 +1056,20 @@ __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay
         return;
     }
     const uint4* p = (const uint4*)(sc.hnodes + w.cur);
-    const uint4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+    const uint4 s0 = p[0], s1 = p[1], s2 = p[2], s3 = p[3];
     // 1. the four conservative slot tests, computed for every slot (no branch
     // for the compiler to sink a load into); COUNT: a slot test is a node test
     float e0 = 0.0f, e1 = 0.0f, e2 = 0.0f, e3 = 0.0f;
-    auto test = [&](uint32_t ref, uint32_t bx, uint32_t by, uint32_t bz, float& e) {
-        if (COUNT && ref != kPNone) cnt.nodes++;
-        const bool pass = slab_cons(sr, pr, h_lo(bx), h_lo(by), h_lo(bz), h_hi(bx), h_hi(by), h_hi(bz), e);
-        return pass & (ref != kPNone);
+    auto test = [&](const uint4& q, float& e) {
+        if (COUNT && q.w != kPNone) cnt.nodes++;
+        const bool pass = slab_cons(sr, pr, h_lo(q.x), h_lo(q.y), h_lo(q.z), h_hi(q.x), h_hi(q.y), h_hi(q.z), e);
+        return pass & (q.w != kPNone);
     };
-    bool h0 = test(q3.x, q0.x, q0.y, q0.z, e0);
-    bool h1 = test(q3.y, q0.w, q1.x, q1.y, e1);
-    bool h2 = test(q3.z, q1.z, q1.w, q2.x, e2);
-    bool h3 = test(q3.w, q2.y, q2.z, q2.w, e3);
+    bool h0 = test(s0, e0);
+    bool h1 = test(s1, e1);
+    bool h2 = test(s2, e2);
+    bool h3 = test(s3, e3);
+    const uint4 q3 = make_uint4(s0.w, s1.w, s2.w, s3.w);  // the slots' references
     // 2. passing leaf slots (the node's boxes are dead here): each lane works
     // through its own list, so the gate code runs max-over-lanes times
     // instead of once per slot that any lane passes
@@ -1112,6 +1115,127 @@ __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay
     if (n >= 4) stk[(w.top + n - 4) * kWideStride] = a3;
     w.top += n - 1;
     w.cur = a0;
+}
+
+// ---------------------------------------------------------------- quad walk
+// The four-wide walk with one ray per QUAD of lanes (lane j of a quad owns
+// slot j of every HNode): the four slot tests of a step run side by side,
+// and the quad reads its node as one 64-B line (four lanes x one dwordx4)
+// instead of one lane issuing four. The ray and the walk state are
+// replicated in the quad's lanes and change only through quad-uniform
+// values; candidates and the order of the passing children are reduced
+// across the quad with DPP. The result is the same closest hit: least t,
+// a tie to the larger sphere index -- an order-free rule.
+constexpr int kQuadStack = 32;   // entries per ray, in LDS
+constexpr int kQuadStride = 64;  // rays (quads) per 256-thread workgroup
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t quad_perm(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+constexpr int kQuadXor1 = 0xB1;  // quad_perm [1,0,3,2]
+constexpr int kQuadXor2 = 0x4E;  // quad_perm [2,3,0,1]
+constexpr int kQuadXor3 = 0x1B;  // quad_perm [3,2,1,0]
+
+struct QuadWalk {
+    uint32_t cur, end, top;
+};
+
+// a better than b: least t, a tie to the larger sphere index
+__device__ __forceinline__ bool cand_better(float ta, int sa, float tb, int sb)
+{
+    return ta < tb || (ta == tb && sa > sb);
+}
+
+template <int CTRL>
+__device__ __forceinline__ void cand_merge(float& t, int& si)
+{
+    const float ot = __uint_as_float(quad_perm<CTRL>(__float_as_uint(t)));
+    const int os = (int)quad_perm<CTRL>((uint32_t)si);
+    if (cand_better(ot, os, t, si)) {
+        t = ot;
+        si = os;
+    }
+}
+
+// `stk`: this ray's LDS stack column (entry k at stk[k * STRIDE], CAP entries).
+template <bool FAST, int STRIDE = kQuadStride, int CAP = kQuadStack>
+__device__ __forceinline__ void quad_step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
+                                          QuadWalk& w, uint32_t* stk, float& best_t, int& best_s)
+{
+    Counters cnt{0, 0, 0, 0, 0};
+    if (w.end) {  // DFS segment (the stack was full): every lane of the quad walks it alike
+        lane_step<FAST, false, true>(sc, sr, sp, pr, w.cur, best_t, best_s, cnt);
+        if (w.cur >= w.end) {
+            w.end = 0;
+            if (w.top == 0) {
+                w.cur = kPNone;
+            } else {
+                w.top--;
+                w.cur = stk[w.top * STRIDE];
+            }
+        }
+        return;
+    }
+    const uint32_t j = threadIdx.x & 3;
+    const uint4 q = ((const uint4*)(sc.hnodes + w.cur))[j];
+    float e = 0.0f;
+    const bool pass = slab_cons(sr, pr, h_lo(q.x), h_lo(q.y), h_lo(q.z), h_hi(q.x), h_hi(q.y), h_hi(q.z), e) &
+                      (q.w != kPNone);
+    // a passing leaf: its exact gate and sphere give this lane's candidate
+    float ct = INFINITY;
+    int cs = -1;
+    if (pass && (q.w & kPLeaf)) {
+        const float4* lp = (const float4*)(sc.leaves + (q.w & ~kPLeaf));
+        const float4 l0 = lp[0], l1 = lp[1], g = lp[2];
+        float ee;
+        if (slab_box<FAST>(sr, pr, l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, ee)) {
+            const float t = sphere_t<FAST>(sp, g, best_t);
+            if (t > 0.0f) {
+                ct = t;
+                cs = __float_as_int(l1.z);
+            }
+        }
+    }
+    cand_merge<kQuadXor1>(ct, cs);
+    cand_merge<kQuadXor2>(ct, cs);
+    if (cs >= 0 && cand_better(ct, cs, best_t, best_s)) {
+        best_t = ct;
+        best_s = cs;
+        if (sc.prune) prune_update(pr, sc, sr.ox, sr.oy, sr.oz, sp.a4, ct);
+    }
+    // the passing inner slots: rank by entry (ties by slot), nearest next
+    const bool inner = pass && !(q.w & kPLeaf);
+    const float key = inner ? fminf(e, 3.0e38f) : INFINITY;
+    const float k1 = __uint_as_float(quad_perm<kQuadXor1>(__float_as_uint(key)));
+    const float k2 = __uint_as_float(quad_perm<kQuadXor2>(__float_as_uint(key)));
+    const float k3 = __uint_as_float(quad_perm<kQuadXor3>(__float_as_uint(key)));
+    const uint32_t rank = (uint32_t)(k1 < key || (k1 == key && (j ^ 1) < j)) +
+                          (uint32_t)(k2 < key || (k2 == key && (j ^ 2) < j)) +
+                          (uint32_t)(k3 < key || (k3 == key && (j ^ 3) < j));
+    const uint32_t n = (uint32_t)__popcll((__ballot(inner) >> (threadIdx.x & 60)) & 0xF);
+    uint32_t nx = inner && rank == 0 ? q.w + 1 : 0u;  // + 1: 0 means none
+    nx |= quad_perm<kQuadXor1>(nx);
+    nx |= quad_perm<kQuadXor2>(nx);
+    if (n == 0) {
+        if (w.top == 0) {
+            w.cur = kPNone;
+        } else {
+            w.top--;
+            w.cur = stk[w.top * STRIDE];
+        }
+        return;
+    }
+    if (w.top + n - 1 > (uint32_t)CAP) {
+        const HAux ax = sc.haux[w.cur];
+        w.cur = ax.flat + 1;
+        w.end = ax.end;
+        return;
+    }
+    if (inner && rank > 0) stk[(w.top + n - 1 - rank) * STRIDE] = q.w;
+    w.top += n - 1;
+    w.cur = nx - 1;
 }
 
 // Closest hit for every active lane: degenerate rays (a zero or tiny

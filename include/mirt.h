@@ -272,9 +272,13 @@ int mirt_last_phase_ms(mirt_ctx *ctx, float *phase);
    0 = the binary ordered walk. */
 enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3, MIRT_OPT_DEFER = 4,
        MIRT_OPT_BOUNCE_THRESHOLD = 5, /* wavefront: shade finished bounce rays once fewer than
-                                         this many lanes of a wave still walk (0..64, default 40) */
+                                         this many lanes of a wave still walk (0..64, default 32) */
        MIRT_OPT_PRUNE = 6, MIRT_OPT_ORDERED = 7, MIRT_OPT_WIDE = 8,
-       MIRT_OPT_BOUNCE_BLOCKS = 9  /* wavefront: persistent bounce workgroups, 0 = occupancy x CUs */ };
+       MIRT_OPT_BOUNCE_BLOCKS = 9,  /* wavefront: persistent bounce workgroups, 0 = occupancy x CUs */
+       MIRT_OPT_QUAD = 10,          /* four-wide bounce walk: 1 = one ray per quad of lanes throughout,
+                                       the four slot tests side by side; 0 (default) = one ray per lane */
+       MIRT_OPT_QUAD_DRAIN = 11     /* four-wide, one ray per lane: 1 (default) = once the queue is dry
+                                       and <= 16 lanes of a wave are busy, finish them as quads */ };
 enum { MIRT_TRAV_UNIFORM = 0, MIRT_TRAV_LANE = 1, MIRT_TRAV_HYBRID = 2, MIRT_TRAV_LANE_NP = 3,
        MIRT_TRAV_HYBRID_NP = 4,  /* *_NP: per-lane walk without successor prefetch */
        MIRT_TRAV_WAVEFRONT = 5   /* default: camera-ray packets, then persistent per-lane

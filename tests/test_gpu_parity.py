@@ -381,3 +381,27 @@ def test_ordered_walk_stays_within_its_lanes(gpu, mirt):
         gpu.set_option(abi.OPT_ORDERED, 1)
     assert ordered[:, 1].max() <= dfs[:, 1].max()
     assert ordered[:, 1].sum() < dfs[:, 1].sum()
+
+
+@pytest.mark.parametrize("quad,drain", [(0, 0), (0, 1), (1, 0)])
+@pytest.mark.parametrize("threshold,blocks", [(40, 0), (8, 0), (56, 64)])
+def test_bounce_modes_identical(gpu, mirt, golden, quad, drain, threshold, blocks):
+    """The bounce pass's modes (one ray per lane, quad drain, one ray per
+    quad), refill thresholds and grid sizes give the golden 1080p frame."""
+    abi = mirt.abi
+    s, b = _scene(mirt, "render", 10000)
+    gpu.upload(s, b)
+    cam = mirt.default_camera()
+    try:
+        gpu.set_option(abi.OPT_QUAD, quad)
+        gpu.set_option(abi.OPT_QUAD_DRAIN, drain)
+        gpu.set_option(abi.OPT_BOUNCE_THRESHOLD, threshold)
+        gpu.set_option(abi.OPT_BOUNCE_BLOCKS, blocks)
+        img = gpu.render_frame(cam, 1920, 1080, depth=5, seed=1)
+    finally:
+        gpu.set_option(abi.OPT_QUAD, 0)
+        gpu.set_option(abi.OPT_QUAD_DRAIN, 1)
+        gpu.set_option(abi.OPT_BOUNCE_THRESHOLD, 32)
+        gpu.set_option(abi.OPT_BOUNCE_BLOCKS, 0)
+    key = "1920x1080_render10000_d5_m1_b1_s1_c0_step1"
+    assert sha(img) == golden["frames"][key]["sha"]
