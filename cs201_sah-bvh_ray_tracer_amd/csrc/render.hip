@@ -1007,7 +1007,9 @@ int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_ac
     Deferred dfr{nullptr, nullptr, 0};
     c->phases_valid = wavefront;
     if (wavefront) HIP_TRY(hipEventRecord(c->ph0, s));
-    if (f.use_bvh && c->defer) {
+    const DevScene sc = dev_scene(c);
+    // the ordered packet walk takes zero-component camera rays itself
+    if (f.use_bvh && c->defer && !sc.ordered) {
         const size_t pixels = (size_t)f.num_rows * f.width;
         int rc = ensure((void**)&c->d_defer, &c->defer_cap, 4 * (pixels + 1));
         if (rc) return rc;
@@ -1019,7 +1021,6 @@ int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_ac
         const size_t want = std::min(pixels, (size_t)(f.width + f.num_rows + 64));
         dfr = Deferred{c->d_defer + 1, c->d_defer, (int)((want + dbw - 1) / dbw)};
     }
-    const DevScene sc = dev_scene(c);
     if (wavefront) {
         const size_t pixels = (size_t)f.num_rows * f.width;
         int rc = ensure(&c->d_queue, &c->queue_cap, sizeof(BounceRec) * pixels + 64);

@@ -359,21 +359,23 @@ __device__ __forceinline__ bool slab_fast(const SlabRay& r, const Prune& p, floa
 // (Prune), although hit.c:54-57 passes such boxes by ignoring the slab.
 // (lo - m, hi + m are rounded, but m carries a 2x margin far above 2^-24
 // (c_max + m).)
-__device__ __forceinline__ bool pruned_any(const SlabRay& r, const Prune& p, const NodeV& n)
+__device__ __forceinline__ bool pruned_any(const SlabRay& r, const Prune& p, float x0, float y0, float z0, float x1,
+                                           float y1, float z1)
 {
-    if (r.zx && (r.ox < n.b0 - p.m || r.ox > n.b3 + p.m)) return true;
-    if (r.zy && (r.oy < n.b1 - p.m || r.oy > n.b4 + p.m)) return true;
-    if (r.zz && (r.oz < n.b2 - p.m || r.oz > n.b5 + p.m)) return true;
+    if (r.zx && (r.ox < x0 - p.m || r.ox > x1 + p.m)) return true;
+    if (r.zy && (r.oy < y0 - p.m || r.oy > y1 + p.m)) return true;
+    if (r.zz && (r.oz < z0 - p.m || r.oz > z1 + p.m)) return true;
     constexpr float c = 1.0f - 0x1p-20f;
     const float tiny = 0x1p-40f;
     float e = -INFINITY;
-    if (fabsf(r.dx) >= tiny)
-        e = fmaxf(e, fmaf(fminf((n.b0 - r.ox) * r.ix, (n.b3 - r.ox) * r.ix), c, -(p.m * fabsf(r.ix))));
-    if (fabsf(r.dy) >= tiny)
-        e = fmaxf(e, fmaf(fminf((n.b1 - r.oy) * r.iy, (n.b4 - r.oy) * r.iy), c, -(p.m * fabsf(r.iy))));
-    if (fabsf(r.dz) >= tiny)
-        e = fmaxf(e, fmaf(fminf((n.b2 - r.oz) * r.iz, (n.b5 - r.oz) * r.iz), c, -(p.m * fabsf(r.iz))));
+    if (fabsf(r.dx) >= tiny) e = fmaxf(e, fmaf(fminf((x0 - r.ox) * r.ix, (x1 - r.ox) * r.ix), c, -(p.m * fabsf(r.ix))));
+    if (fabsf(r.dy) >= tiny) e = fmaxf(e, fmaf(fminf((y0 - r.oy) * r.iy, (y1 - r.oy) * r.iy), c, -(p.m * fabsf(r.iy))));
+    if (fabsf(r.dz) >= tiny) e = fmaxf(e, fmaf(fminf((z0 - r.oz) * r.iz, (z1 - r.oz) * r.iz), c, -(p.m * fabsf(r.iz))));
     return e > p.lim;
+}
+__device__ __forceinline__ bool pruned_any(const SlabRay& r, const Prune& p, const NodeV& n)
+{
+    return pruned_any(r, p, n.b0, n.b1, n.b2, n.b3, n.b4, n.b5);
 }
 
 template <bool FAST>
@@ -392,6 +394,7 @@ __device__ __forceinline__ bool slab_box(const SlabRay& r, const Prune& p, float
 {
     if (FAST && !r.generic) return slab_fast(r, p, x0, y0, z0, x1, y1, z1, near);
     near = 0.0f;
+    if (FAST && pruned_any(r, p, x0, y0, z0, x1, y1, z1)) return false;
     return slab_test(r, x0, y0, z0, x1, y1, z1);
 }
 
@@ -813,7 +816,7 @@ __device__ __forceinline__ void closest_packet_ordered(const DevScene& sc, const
 {
     const SlabRay sr = slab_ray(ray);
     const SphRay sp = sph_ray(ray);
-    Prune pr = prune_off();
+    Prune pr = prune_start(sc, ray.ox, ray.oy, ray.oz);  // m0: zero-component lanes prune from the start
     best_t = INFINITY;
     best_s = -1;
     const uint32_t lane = threadIdx.x & 63;
@@ -1022,7 +1025,7 @@ __device__ __forceinline__ bool slab_cons(const SlabRay& r, const Prune& p, floa
     bool pass = slab_cons_fast(r, p, x0, y0, z0, x1, y1, z1, near);
     if (r.generic) {  // a lane branch taken only by rays with a zero/tiny component
         near = 0.0f;
-        pass = slab_test(r, x0, y0, z0, x1, y1, z1);
+        pass = !pruned_any(r, p, x0, y0, z0, x1, y1, z1) && slab_test(r, x0, y0, z0, x1, y1, z1);
     }
     return pass;
 }
@@ -1246,9 +1249,13 @@ template <bool UNIFORM, bool FAST, bool COUNT, bool LPF = true>
 __device__ __forceinline__ void closest_hit(const DevScene& sc, const Ray& ray, bool active, float& best_t,
                                             int& best_s, Counters& cnt, uint32_t* wstk = nullptr)
 {
-    const bool gen = active && slab_ray(ray).generic;
+    bool gen = active && slab_ray(ray).generic;
     if (UNIFORM && FAST && sc.ordered) {
-        closest_packet_ordered<FAST, COUNT>(sc, ray, active && !gen, best_t, best_s, cnt);
+        // with pruning (sc.ordered implies it), a zero-component ray is held
+        // to boxes around its own coordinate (pruned_any) and walks in the
+        // packet like any other
+        closest_packet_ordered<FAST, COUNT>(sc, ray, active, best_t, best_s, cnt);
+        gen = false;
     } else if (!UNIFORM && FAST && sc.wide && wstk) {
         // the bounce kernel's walk (wstk: a kWideStack-entry LDS column)
         const SlabRay sr = slab_ray(ray);
