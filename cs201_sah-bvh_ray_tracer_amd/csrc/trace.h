@@ -398,6 +398,39 @@ __device__ __forceinline__ bool slab_box(const SlabRay& r, const Prune& p, float
     return slab_test(r, x0, y0, z0, x1, y1, z1);
 }
 
+// Conservative box test: passes whenever hit.c's slab test on this box
+// would (slab_fast's margins, with "undecided" counted as a pass), and also
+// applies the pruning bound, which holds for any box containing the subtree.
+// Branch-free, valid for rays without a zero/tiny direction component
+// (slab_cons handles those with the exact division test).
+__device__ __forceinline__ bool slab_cons_fast(const SlabRay& r, const Prune& p, float x0, float y0, float z0,
+                                               float x1, float y1, float z1, float& near)
+{
+    const float tx1 = (x0 - r.ox) * r.ix, tx2 = (x1 - r.ox) * r.ix;
+    const float ty1 = (y0 - r.oy) * r.iy, ty2 = (y1 - r.oy) * r.iy;
+    const float tz1 = (z0 - r.oz) * r.iz, tz2 = (z1 - r.oz) * r.iz;
+    const float nx = fminf(tx1, tx2), ny = fminf(ty1, ty2), nz = fminf(tz1, tz2);
+    constexpr float c = 1.0f - 0x1p-20f;
+    const float entry = fmaxf(fmaf(nx, c, -(p.m * fabsf(r.ix))),
+                              fmaxf(fmaf(ny, c, -(p.m * fabsf(r.iy))), fmaf(nz, c, -(p.m * fabsf(r.iz)))));
+    const float tmin = fmaxf(nx, fmaxf(ny, nz));
+    const float tmax = fminf(fmaxf(tx1, tx2), fminf(fmaxf(ty1, ty2), fmaxf(tz1, tz2)));
+    near = tmin;
+    const float m = (fabsf(tmin) + fabsf(tmax)) * 0x1p-20f;
+    return !(entry > p.lim) & !(tmax - tmin < -m) & !(tmax - kEps < -m);
+}
+
+__device__ __forceinline__ bool slab_cons(const SlabRay& r, const Prune& p, float x0, float y0, float z0, float x1,
+                                          float y1, float z1, float& near)
+{
+    bool pass = slab_cons_fast(r, p, x0, y0, z0, x1, y1, z1, near);
+    if (r.generic) {  // a lane branch taken only by rays with a zero/tiny component
+        near = 0.0f;
+        pass = !pruned_any(r, p, x0, y0, z0, x1, y1, z1) && slab_test(r, x0, y0, z0, x1, y1, z1);
+    }
+    return pass;
+}
+
 // Per-ray constants of ray_sphere_intersect: a = d.d, 4a and 2a (hit.c:22-28).
 struct SphRay {
     float ox, oy, oz, dx, dy, dz;
@@ -797,6 +830,10 @@ __device__ __forceinline__ bool visit_child(const DevScene& sc, const SlabRay& s
         return false;
     }
     if (COUNT) cnt.nodes++;
+    // an inner box needs only a conservative test: the reference's test is
+    // monotone under containment, so a ray that passes any leaf box below
+    // passes this one too, and every leaf is still gated exactly
+    if (FAST) return slab_cons(sr, pr, s0, s1, s2, s3, s4, s5, near);
     return slab_box<FAST>(sr, pr, s0, s1, s2, s3, s4, s5, near);
 }
 
@@ -996,39 +1033,6 @@ __device__ __forceinline__ void cx(float& ka, uint32_t& ra, float& kb, uint32_t&
 
 __device__ __forceinline__ float h_lo(uint32_t v) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(v & 0xffffu)); }
 __device__ __forceinline__ float h_hi(uint32_t v) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(v >> 16)); }
-
-// Conservative box test: passes whenever hit.c's slab test on this box
-// would (slab_fast's margins, with "undecided" counted as a pass), and also
-// applies the pruning bound, which holds for any box containing the subtree.
-// Branch-free, valid for rays without a zero/tiny direction component
-// (slab_cons handles those with the exact division test).
-__device__ __forceinline__ bool slab_cons_fast(const SlabRay& r, const Prune& p, float x0, float y0, float z0,
-                                               float x1, float y1, float z1, float& near)
-{
-    const float tx1 = (x0 - r.ox) * r.ix, tx2 = (x1 - r.ox) * r.ix;
-    const float ty1 = (y0 - r.oy) * r.iy, ty2 = (y1 - r.oy) * r.iy;
-    const float tz1 = (z0 - r.oz) * r.iz, tz2 = (z1 - r.oz) * r.iz;
-    const float nx = fminf(tx1, tx2), ny = fminf(ty1, ty2), nz = fminf(tz1, tz2);
-    constexpr float c = 1.0f - 0x1p-20f;
-    const float entry = fmaxf(fmaf(nx, c, -(p.m * fabsf(r.ix))),
-                              fmaxf(fmaf(ny, c, -(p.m * fabsf(r.iy))), fmaf(nz, c, -(p.m * fabsf(r.iz)))));
-    const float tmin = fmaxf(nx, fmaxf(ny, nz));
-    const float tmax = fminf(fmaxf(tx1, tx2), fminf(fmaxf(ty1, ty2), fmaxf(tz1, tz2)));
-    near = tmin;
-    const float m = (fabsf(tmin) + fabsf(tmax)) * 0x1p-20f;
-    return !(entry > p.lim) & !(tmax - tmin < -m) & !(tmax - kEps < -m);
-}
-
-__device__ __forceinline__ bool slab_cons(const SlabRay& r, const Prune& p, float x0, float y0, float z0, float x1,
-                                          float y1, float z1, float& near)
-{
-    bool pass = slab_cons_fast(r, p, x0, y0, z0, x1, y1, z1, near);
-    if (r.generic) {  // a lane branch taken only by rays with a zero/tiny component
-        near = 0.0f;
-        pass = !pruned_any(r, p, x0, y0, z0, x1, y1, z1) && slab_test(r, x0, y0, z0, x1, y1, z1);
-    }
-    return pass;
-}
 
 // The leaf gate of a leaf slot whose fp16 box passed: its exact box under
 // hit.c's test, then its sphere. COUNT: the sphere test counts.
