@@ -243,16 +243,19 @@ struct BounceRec {
     uint32_t pad;
 };
 
-template <bool FAST>
+// ORD: the tree admits the ordered packet walk (DevScene::ordered), which
+// also takes zero-component rays -- that build has no deferred waves and no
+// other walk, so it keeps the register budget of the packet walk alone.
+template <bool FAST, bool ORD>
 __global__ __launch_bounds__(256) void primary_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
                                                       float* __restrict__ acc, Deferred dfr,
                                                       BounceRec* __restrict__ queue, uint32_t* __restrict__ qctl)
 {
-    __shared__ uint32_t cstack[kMaxDepth * 256];
+    __shared__ uint32_t cstack[ORD ? 1 : kMaxDepth * 256];
     Counters cnt{0, 0, 0, 0, 0};
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    if ((int)blockIdx.x < dfr.blocks) {  // zero-component camera rays: whole path in this wave
+    if (!ORD && (int)blockIdx.x < dfr.blocks) {  // zero-component camera rays: whole path in this wave
         const uint32_t n = __builtin_amdgcn_readfirstlane(*dfr.count);
         const uint32_t stride = (uint32_t)(dfr.blocks * 4);
         for (uint32_t j = blockIdx.x * 4 + wave; j < n; j += stride) {
@@ -269,10 +272,13 @@ __global__ __launch_bounds__(256) void primary_kernel(DevScene sc, FrameConst f,
     bool alive = x < f.width && r < f.num_rows;
     const int y = alive ? shard_row_to_y(f, r) : 0;
     const Ray ray = camera_ray(f, alive ? x : 0, y);
-    if (dfr.blocks > 0 && alive && slab_ray(ray).generic) alive = false;  // traced by a deferred wave
+    if (!ORD && dfr.blocks > 0 && alive && slab_ray(ray).generic) alive = false;  // traced by a deferred wave
     float t;
     int s;
-    closest_hit<true, FAST, false>(sc, ray, alive, t, s, cnt);
+    if constexpr (ORD)
+        closest_packet_ordered<FAST, false>(sc, ray, alive, t, s, cnt);
+    else
+        closest_hit<true, FAST, false>(sc, ray, alive, t, s, cnt);
     const size_t i = (size_t)r * f.width + x;
     bool push = false;
     BounceRec rec;
@@ -1030,10 +1036,12 @@ int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_ac
         HIP_TRY(hipMemsetAsync(qctl, 0, 8, s));
         const int pblocks = (tiles + 3) / 4 + dfr.blocks;
         const int bblocks = c->bounce_blocks_opt ? c->bounce_blocks_opt : c->bounce_blocks;
-        if (c->fast_slab)
-            primary_kernel<true><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
+        if (c->fast_slab && sc.ordered)
+            primary_kernel<true, true><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
+        else if (c->fast_slab)
+            primary_kernel<true, false><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
         else
-            primary_kernel<false><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
+            primary_kernel<false, false><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ph1, s));
         if (d_bdiag && sc.wide)
