@@ -31,7 +31,7 @@ shard = importlib.import_module("cs201_sah-bvh_ray_tracer_amd.shard")
 W, H, NSPH, DEPTH, SEED, ROW_BLOCK = 1920, 1080, 10000, 5, 1, 8
 PEAK_HBM_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 NODE_B, SPHERE_B, COLOR_B, PIXEL_B = 32, 16, 4, 4
-KERNEL = "bounce_kernel<true, 2>"   # dominant kernel of the default (wavefront, four-wide) schedule
+KERNEL = "bounce_kernel<true, 2, false>"   # dominant kernel of the default (wavefront, four-wide) schedule
 
 
 def algorithmic_bytes(c, pixels):

@@ -409,7 +409,7 @@ __device__ __forceinline__ bool shade_level(const DevScene& sc, const FrameConst
 // step, so four lanes per ray make the drain's steps about four times
 // shorter at no extra cost.
 template <bool FAST, int WALK, bool DIAG = false>
-__global__ __launch_bounds__(256, 5) void bounce_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
+__global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
                                                      float* __restrict__ acc, const BounceRec* __restrict__ queue,
                                                      uint32_t* __restrict__ qctl, int threshold, int quad_drain,
                                                      uint64_t* __restrict__ diag = nullptr)
