@@ -41,7 +41,9 @@ bool frame_desc_valid(const mirt_frame_desc* fd)
     if (fd->width <= 0 || fd->height <= 0 || fd->max_depth < 0 || fd->max_depth > 8) return false;
     if (fd->row_block <= 0 || fd->num_shards <= 0 || fd->shard < 0 || fd->shard >= fd->num_shards) return false;
     if (fd->accumulate && fd->frames <= 0) return false;
-    return (int64_t)fd->width * fd->height <= (int64_t)1 << 31;
+    if (fd->samples < 0 || fd->samples > 64) return false;
+    const int64_t samples = fd->samples > 1 ? fd->samples : 1;
+    return (int64_t)fd->width * fd->height * samples <= (int64_t)1 << 31;
 }
 
 int shard_row_count(const mirt_frame_desc* fd)

@@ -33,7 +33,10 @@ struct FrameConst {
     uint32_t sample;
     int accumulate;
     float frames;
-    int row_block, shard, num_shards, num_rows;
+    int row_block, shard, num_shards;
+    int num_rows;      // rows of this launch: shard_rows x samples (frame j's rows follow frame j-1's)
+    int shard_rows;    // rows of one frame of this shard
+    int samples;       // frames in this launch (RNG samples sample .. sample + samples - 1)
 };
 
 FrameConst make_frame_const(const mirt_camera* cam, const mirt_frame_desc* fd)
@@ -62,15 +65,24 @@ FrameConst make_frame_const(const mirt_camera* cam, const mirt_frame_desc* fd)
     f.row_block = fd->row_block;
     f.shard = fd->shard;
     f.num_shards = fd->num_shards;
-    f.num_rows = shard_row_count(fd);
+    f.shard_rows = shard_row_count(fd);
+    f.samples = fd->samples > 1 ? fd->samples : 1;
+    f.num_rows = f.shard_rows * f.samples;
     return f;
 }
 
-// Image row of compacted shard row r.
+// Image row of launch row r (compacted shard row r % shard_rows of frame r / shard_rows).
 __device__ __forceinline__ int shard_row_to_y(const FrameConst& f, int r)
 {
+    if (f.samples > 1) r %= f.shard_rows;
     const int blk = r / f.row_block;
     return (blk * f.num_shards + f.shard) * f.row_block + (r - blk * f.row_block);
+}
+
+// RNG contract sample of launch row r (one sample per frame).
+__device__ __forceinline__ uint32_t row_sample(const FrameConst& f, int r)
+{
+    return f.samples > 1 ? f.sample + (uint32_t)(r / f.shard_rows) : f.sample;
 }
 
 // main.c:362-365 + ray.c:26-31 for pixel (x, y).
@@ -122,7 +134,7 @@ __device__ __forceinline__ void render_pixel(const DevScene& sc, const FrameCons
     const int y = alive ? shard_row_to_y(f, r) : 0;
     const Ray ray = camera_ray(f, alive ? x : 0, y);
     if (skip_generic && alive && slab_ray(ray).generic) alive = false;  // a deferred wave traces it
-    const uint64_t key = pixel_key(f.seed, (uint32_t)(y * f.width + x), f.sample);
+    const uint64_t key = pixel_key(f.seed, (uint32_t)(y * f.width + x), row_sample(f, r));
     const uint32_t c = trace_path<TRAV, FAST, COUNT>(sc, ray, alive, f.depth, f.use_bvh != 0, key, cnt, cstack,
                                                      cstride, wstk);
     if (!alive) return;
@@ -223,6 +235,41 @@ __device__ __forceinline__ void store_pixel(const FrameConst& f, uint32_t* __res
     out[i] = shown;
 }
 
+// A launch of f.samples > 1 frames with an accumulation buffer: the kernels
+// wrote each frame's colours to its own slab of `out`; fold them into `acc`
+// in frame order, exactly as f.samples successive store_pixel calls would
+// (frame j: fresh if j == 0 and !f.accumulate, else divisor f.frames + j),
+// and leave the display after the last frame in slab 0.
+__global__ void fold_samples_kernel(FrameConst f, uint32_t* __restrict__ out, float* __restrict__ acc)
+{
+    const size_t n = (size_t)f.shard_rows * f.width;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float* a = acc + 3 * i;
+    float a0 = a[0], a1 = a[1], a2 = a[2];
+    uint32_t shown = 0;
+    for (int j = 0; j < f.samples; j++) {
+        const uint32_t c = out[(size_t)j * n + i];
+        shown = c;
+        float* ch[3] = {&a0, &a1, &a2};
+        for (int k = 0; k < 3; k++) {
+            const float v = (float)((c >> (8 * k)) & 0xff) / 255.0f;       // main.c:368-370 / 394-396
+            if (j == 0 && !f.accumulate) {
+                *ch[k] = v;
+            } else {
+                *ch[k] = *ch[k] + v;
+                const float avg = *ch[k] / (f.frames + (float)j) * 255.0f;  // main.c:398-400
+                const uint32_t q = (uint32_t)(int)fminf(avg, 255.0f);
+                shown = (shown & ~(0xffu << (8 * k))) | ((q & 0xffu) << (8 * k));
+            }
+        }
+    }
+    a[0] = a0;
+    a[1] = a1;
+    a[2] = a2;
+    out[i] = shown;
+}
+
 __device__ __forceinline__ uint32_t lanes_below(uint64_t mask)
 {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
@@ -292,7 +339,7 @@ __global__ __launch_bounds__(256) void primary_kernel(DevScene sc, FrameConst f,
             hit_point_normal(ray, t, g, p, n);
             uint32_t k = 0;
             float bx, by, bz;
-            hemisphere(pixel_key(f.seed, (uint32_t)(y * f.width + x), f.sample), k, n, bx, by, bz);
+            hemisphere(pixel_key(f.seed, (uint32_t)(y * f.width + x), row_sample(f, r)), k, n, bx, by, bz);
             rec = BounceRec{p[0], p[1], p[2], bx, by, bz, (uint32_t)i, k, sc.color[s], 0u};
             push = true;
         }
@@ -463,7 +510,7 @@ __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, 
                     base0 = rec.base0;
                     level = 1;
                     const int r = (int)(pixel / f.width), x = (int)(pixel - r * f.width);
-                    key = pixel_key(f.seed, (uint32_t)(shard_row_to_y(f, r) * f.width + x), f.sample);
+                    key = pixel_key(f.seed, (uint32_t)(shard_row_to_y(f, r) * f.width + x), row_sample(f, r));
                     w.start(sc);
                     best_t = INFINITY;
                     best_s = -1;
@@ -1008,6 +1055,17 @@ int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_ac
     const int blocks = (tiles + bw - 1) / bw;
     if (blocks == 0) return MIRT_OK;
     if (timed) HIP_TRY(hipEventRecord(c->ev0, s));
+    // several frames and an accumulation buffer: raw colours per frame, then
+    // fold_samples_kernel accumulates them in order
+    float* const d_fold = f.samples > 1 ? d_acc : nullptr;
+    if (d_fold) d_acc = nullptr;
+    auto fold = [&]() -> int {
+        if (!d_fold) return MIRT_OK;
+        const size_t n = (size_t)f.shard_rows * f.width;
+        fold_samples_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(f, d_out, d_fold);
+        HIP_TRY(hipGetLastError());
+        return MIRT_OK;
+    };
     const bool wavefront = c->trav == kTravWavefront && f.use_bvh && f.depth >= 2 && !d_counts;
     const int dbw = wavefront ? 4 : bw;  // the wavefront kernels use 256-thread workgroups
     Deferred dfr{nullptr, nullptr, 0};
@@ -1062,6 +1120,7 @@ int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_ac
             bounce_kernel<false, 0><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ph2, s));
+        if (int rc = fold()) return rc;
         if (timed) HIP_TRY(hipEventRecord(c->ev1, s));
         return MIRT_OK;
     }
@@ -1070,6 +1129,7 @@ int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_ac
     else
         dispatch_render<false>(c->trav, c->fast_slab != 0, sc, f, d_out, d_acc, s, blocks, bw, nullptr, nullptr, dfr);
     HIP_TRY(hipGetLastError());
+    if (int rc = fold()) return rc;
     if (timed) HIP_TRY(hipEventRecord(c->ev1, s));
     return MIRT_OK;
 }
@@ -1255,8 +1315,8 @@ int mirt_render_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc
         return MIRT_E_NOSCENE;
     }
     const FrameConst f = make_frame_const(cam, fd);
-    const size_t pixels = (size_t)f.num_rows * f.width;
-    int rc = ensure((void**)&c->d_out, &c->out_cap, pixels * 4 + 4);
+    const size_t pixels = (size_t)f.shard_rows * f.width;  // one frame (several: folded into slab 0)
+    int rc = ensure((void**)&c->d_out, &c->out_cap, pixels * f.samples * 4 + 4);
     if (rc) return rc;
     rc = ensure((void**)&c->d_acc, &c->acc_cap, pixels * 12 + 4);
     if (rc) return rc;

@@ -10,6 +10,15 @@ de-interleaves them on the device. The scene is replicated per rank, so the
 gather is the only exchange. Pixels do not depend on the sharding (the RNG
 contract keys on the full-frame pixel index), so any world size produces the
 same bytes as one GPU.
+
+Frames in flight (`samples` > 1): one launch renders this rank's rows of
+`samples` successive frames of the accumulating display loop (main.c:379-408,
+RNG samples sample .. sample + samples - 1) and folds them into the rank's
+accumulation buffer on the device; only the display after the last frame is
+gathered. The bounce pass's latency tail (its longest chains) is then paid
+once per launch rather than once per frame, which is what lets the frame
+rate grow with the number of GPUs: at N GPUs with samples = N every rank
+traces one frame's worth of rays per step (weak scaling).
 """
 import torch
 import torch.distributed as dist
@@ -71,24 +80,29 @@ class ShardedFrame:
     uploaded. Uses torch's current stream for both the kernel and RCCL.
     """
 
-    def __init__(self, renderer, width, height, row_block=8, group=None):
+    def __init__(self, renderer, width, height, row_block=8, group=None, samples=1):
         self.r = renderer
         self.width, self.height, self.row_block = width, height, row_block
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.samples = samples
         dev = torch.device("cuda", torch.cuda.current_device())
         self.rows = slab_rows(height, row_block, self.world)
-        self.slab = torch.zeros((self.rows, width), dtype=torch.int32, device=dev)
+        # one slab per frame in flight; slab 0 is the display that is gathered
+        self.slabs = torch.zeros((samples, self.rows, width), dtype=torch.int32, device=dev)
+        self.slab = self.slabs[0]
+        self.acc = torch.zeros((self.rows, width, 3), dtype=torch.float32, device=dev) if samples > 1 else None
 
-    def desc(self, depth=5, use_bvh=True, seed=1, sample=0):
+    def desc(self, depth=5, use_bvh=True, seed=1, sample=0, accumulate=False, frames=1):
         from .renderer import frame_desc
-        return frame_desc(self.width, self.height, depth, use_bvh, seed, sample, False, 1, self.row_block,
-                          self.rank, self.world)
+        return frame_desc(self.width, self.height, depth, use_bvh, seed, sample, accumulate, frames, self.row_block,
+                          self.rank, self.world, self.samples)
 
     def render_local(self, cam, fd):
         stream = torch.cuda.current_stream().cuda_stream
-        self.r.render_frame_device(cam, fd, self.slab.data_ptr(), None, stream)
+        self.r.render_frame_device(cam, fd, self.slabs.data_ptr(),
+                                   self.acc.data_ptr() if self.acc is not None else None, stream)
         return self.slab
 
     def render(self, cam, fd):

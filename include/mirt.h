@@ -101,6 +101,13 @@ typedef struct mirt_frame_desc {
     int32_t row_block;       /* rows per interleave block (default 8) */
     int32_t shard;           /* this shard renders row blocks b with b % num_shards == shard */
     int32_t num_shards;
+    int32_t samples;         /* frames rendered by this call, samples sample .. sample+samples-1 of the
+                                RNG contract (0 or 1: one). One launch covers all of them, so the
+                                bounce pass's tail (its longest chains) is paid once, not per frame.
+                                Output: `samples` consecutive slabs, one per frame; with an
+                                accumulation buffer, the frames are folded into it in order (as
+                                `samples` successive calls would: frame j has divisor frames + j)
+                                and slab 0 holds the display after the last one (main.c:379-408) */
 } mirt_frame_desc;
 
 /* Work counters of the walk as configured; with MIRT_OPT_PRUNE = 0 they are
@@ -188,13 +195,17 @@ int mirt_shard_rows(const mirt_frame_desc *fd, int32_t *rows);
 /* The pixel loop of main.c:356-374 (fresh) / main.c:382-407 (accumulate) for
    the shard described by fd: writes the displayed RGBA8 colour of every pixel
    of the shard's rows, compacted in shard row order, to host memory `out`
-   (num_rows * width). Accumulation state lives on the device (per ctx). */
+   (num_rows * width). Accumulation state lives on the device (per ctx); with
+   fd->samples > 1 the frames are accumulated in order and `out` receives the
+   display after the last one. */
 int mirt_render_frame(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_desc *fd, mirt_rgba8 *out);
 
 /* Same, asynchronously on `stream` (a hipStream_t; NULL = the default stream),
-   into device memory: d_out = num_rows * width packed RGBA8. d_accum is a
-   device float buffer of num_rows * width * 3 (may be NULL when
-   fd->accumulate == 0). Inputs are already resident in HBM. */
+   into device memory: d_out = samples * num_rows * width packed RGBA8 (frame
+   j's slab at j * num_rows * width). d_accum is a device float buffer of
+   num_rows * width * 3 (may be NULL when fd->accumulate == 0); given with
+   samples > 1, the frames are folded into it and slab 0 receives the display
+   after the last. Inputs are already resident in HBM. */
 int mirt_render_frame_device(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_desc *fd,
                              uint32_t *d_out, float *d_accum, void *stream);
 

@@ -6,6 +6,10 @@ import sys
 
 import numpy as np
 import pytest
+# torch before libmirt.so: both need libamdhip64.so.7, and the process must
+# hold ONE HIP runtime (torch's) for device pointers and streams from torch
+# to be valid in libmirt -- as in bench.py, which imports torch first
+import torch  # noqa: F401
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:

@@ -153,6 +153,84 @@ def test_accumulate_matches_oracle(gpu, mirt, oracle, small):
     oracle.free(t)
 
 
+@pytest.mark.parametrize("depth,trav", [(5, 5), (1, 5), (5, 2)])
+def test_frames_in_flight_match_successive_frames(gpu, mirt, oracle, small, depth, trav):
+    """samples = 4 in one launch == 4 successive calls of the accumulating
+    loop (main.c:379-408): same display, same accumulation buffer; checked
+    against the oracle too, on a whole frame and on shard 1 of 3."""
+    s, b = _scene(mirt, "render", 1000)
+    gpu.upload(s, b)
+    cam = mirt.default_camera()
+    W, H = 160, 90
+    t = oracle.build(small["render_1000_1_pre"].copy())
+    old = gpu.get_option(mirt.abi.OPT_TRAVERSAL)
+    try:
+        gpu.set_option(mirt.abi.OPT_TRAVERSAL, trav)
+        for shard, world in ((0, 1), (1, 3)):
+            seq = None
+            for k in range(4):
+                seq = gpu.render_frame(cam, W, H, depth=depth, seed=4, sample=k, accumulate=k > 0, frames=k + 1,
+                                       shard=shard, num_shards=world)
+            acc_seq = gpu.accum(seq.shape[0] * W * 3)
+            one = gpu.render_frame(cam, W, H, depth=depth, seed=4, sample=0, samples=4, shard=shard,
+                                   num_shards=world)
+            assert (one == seq).all(), shard
+            assert gpu.accum(seq.shape[0] * W * 3).tobytes() == acc_seq.tobytes()
+            # continuing an accumulation: frames 4..6 after the 4 above
+            more = gpu.render_frame(cam, W, H, depth=depth, seed=4, sample=4, samples=3, accumulate=True, frames=5,
+                                    shard=shard, num_shards=world)
+            acc = np.zeros(W * H * 3, np.float32)
+            for k in range(7):
+                col = oracle.render(cam, W, H, s, t, depth=depth, mode=1, seed=4, sample=k)
+                ref = oracle.accumulate(col, acc, k == 0, k + 1).reshape(H, W, 4)
+            rows = mirt.shard_rows(mirt.frame_desc(W, H, shard=shard, num_shards=world))
+            assert (more == ref[rows]).all(), shard
+    finally:
+        gpu.set_option(mirt.abi.OPT_TRAVERSAL, old)
+        oracle.free(t)
+
+
+def test_frames_in_flight_raw_slabs(gpu, mirt):
+    """Without an accumulation buffer a launch of samples = 3 leaves frame j
+    (RNG sample j) in slab j: each equals the fresh single frame."""
+    import torch
+    s, b = _scene(mirt, "render", 10000)
+    gpu.upload(s, b)
+    cam = mirt.default_camera()
+    W, H = 320, 180
+    fd = mirt.frame_desc(W, H, depth=5, seed=2, sample=5, samples=3)
+    out = torch.zeros((3, H, W), dtype=torch.int32, device="cuda")
+    gpu.render_frame_device(cam, fd, out.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint8).reshape(3, H, W, 4)
+    for j in range(3):
+        ref = gpu.render_frame(cam, W, H, depth=5, seed=2, sample=5 + j)
+        assert (got[j] == ref).all(), j
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_weak_scaling_step_identical(gpu, mirt, world):
+    """The bench's weak-scaling step at N ranks (N frames in flight, rows
+    interleaved over N shards, display slabs gathered) shows the same bytes
+    as the same N frames accumulated on one GPU."""
+    from importlib import import_module
+    import torch
+    shard = import_module("cs201_sah-bvh_ray_tracer_amd.shard")
+    s, b = _scene(mirt, "render", 10000)
+    gpu.upload(s, b)
+    cam = mirt.default_camera()
+    W, H = 1920, 1080
+    full = gpu.render_frame(cam, W, H, depth=5, seed=1, samples=world)
+    rows = shard.slab_rows(H, 8, world)
+    slabs = np.zeros((world, rows, W, 4), np.uint8)
+    for r in range(world):
+        part = gpu.render_frame(cam, W, H, depth=5, seed=1, samples=world, shard=r, num_shards=world)
+        slabs[r, :len(part)] = part
+    st = torch.from_numpy(slabs.view(np.int32).reshape(world, rows, W))
+    frame = shard.as_rgba(shard.assemble(st, H, 8)).numpy()
+    assert (frame == full).all()
+
+
 def test_counts_match_oracle(gpu, mirt, oracle):
     s, b = _scene(mirt, "render", 10000)
     gpu.upload(s, b)
