@@ -12,13 +12,15 @@ Layout:
   lib.py       loader (no fallback: missing library -> MirtError)
   renderer.py  the reference's call surface (trace_ray, build_bvh_node, ...)
   shard.py     row-block sharding of a frame over ranks + RCCL gather
+  benchmark.py the reference's benchmark mode (benchmark.c) as batched launches
 """
 from . import abi
 from .lib import LIB_PATH, MirtError, build, load
 from .renderer import (Bvh, RandState, Renderer, build_bvh, build_bvh_node, camera_update,
-                       create_benchmark_spheres, create_random_spheres, default_camera, flatten_bvh,
+                       create_bench_rays, create_benchmark_spheres, create_random_spheres, default_camera,
+                       flatten_bvh,
                        frame_desc, free_bvh, shard_rows)
 
 __all__ = ["abi", "LIB_PATH", "MirtError", "build", "load", "Bvh", "RandState", "Renderer", "build_bvh",
-           "build_bvh_node", "camera_update", "create_benchmark_spheres", "create_random_spheres",
+           "build_bvh_node", "camera_update", "create_bench_rays", "create_benchmark_spheres", "create_random_spheres",
            "default_camera", "flatten_bvh", "frame_desc", "free_bvh", "shard_rows"]

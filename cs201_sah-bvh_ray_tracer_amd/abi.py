@@ -96,6 +96,7 @@ SIGNATURES = [
     ("mirt_rand", I, [P]),
     ("mirt_scene_random", I, [P, P, I]),
     ("mirt_scene_benchmark", I, [P, P, I, C.c_float]),
+    ("mirt_bench_rays", I, [P, P, I]),
     ("mirt_camera_default", None, [P]),
     ("mirt_camera_update", None, [P]),
     ("mirt_build_bvh_node", P, [P, I, I, I]),
@@ -114,6 +115,7 @@ SIGNATURES = [
     ("mirt_accum_download", I, [P, P, C.c_size_t]),
     ("mirt_trace_rays", I, [P, P, I, I, I, C.c_uint64, C.c_uint32, P]),
     ("mirt_intersect_rays", I, [P, P, I, I, P]),
+    ("mirt_any_hit_rays", I, [P, P, I, I, P]),
     ("mirt_sphere_pairs", I, [P, P, P, I, P]),
     ("mirt_aabb_pairs", I, [P, P, P, I, P]),
     ("mirt_camera_rays", I, [P, P, P, P]),

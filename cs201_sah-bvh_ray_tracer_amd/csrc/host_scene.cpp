@@ -190,6 +190,22 @@ void mirt_camera_update(mirt_camera* c)  // camera.c:10-18 (libm in double)
     c->up = v_norm(v_cross(c->right, c->forward));
 }
 
+// benchmark.c:176-185 / 228-237: direction = normalize((float)rand()/RAND_MAX
+// * 2 - 1 per axis, x then y then z), origin (0,0,0); n rays off the stream.
+int mirt_bench_rays(mirt_rand_state* st, mirt_ray* out, int n)
+{
+    if (!st || (!out && n > 0) || n < 0) return MIRT_E_INVALID;
+    for (int i = 0; i < n; i++) {
+        mirt_vec3 d;
+        d.x = (float)mirt_rand(st) / 2147483648.0f * 2 - 1;
+        d.y = (float)mirt_rand(st) / 2147483648.0f * 2 - 1;
+        d.z = (float)mirt_rand(st) / 2147483648.0f * 2 - 1;
+        out[i].origin = {0.0f, 0.0f, 0.0f};
+        out[i].direction = v_norm(d);
+    }
+    return MIRT_OK;
+}
+
 int mirt_shard_rows(const mirt_frame_desc* fd, int32_t* rows)
 {
     if (!mirt::frame_desc_valid(fd)) {

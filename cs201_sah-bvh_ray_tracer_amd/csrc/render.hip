@@ -670,11 +670,66 @@ __device__ __forceinline__ void store_hit(const Ray& ray, float t, int s, const 
     *o = h;
 }
 
-// ray_bvh_intersect (hit.c:91) / brute-force closest hit (renderer.c:36-43)
+// Brute force (renderer.c:36-43, benchmark.c:190-199) split over sphere
+// chunks so that a few thousand rays still fill the chip: workgroup (bx, by)
+// runs rays [256 bx, 256 bx + 256) against spheres [chunk by, chunk (by + 1)),
+// every lane reading the same sphere (scalar loads, one fetch per wave).
+// The chunk's best (t, index) joins keys[ray] by a 64-bit atomicMin of
+// (bits(t) << 32 | index) -- t > 0 orders as its bit pattern, and on equal t
+// the smaller index (the first sphere in array order) wins, as the loop's
+// strict `<` does. Any-hit flags are keys != ~0: every sphere is still
+// tested, as benchmark.c:190-199 does (an early exit measured slower: the
+// per-sphere vote costs more than the rare hit saves).
 template <bool FAST>
-__global__ __launch_bounds__(256) void intersect_kernel(DevScene sc, const mirt_ray* __restrict__ rays, int n,
-                                                        int use_bvh, mirt_hit* __restrict__ out)
+__global__ __launch_bounds__(256) void brute_chunk_kernel(DevScene sc, const mirt_ray* __restrict__ rays, int n,
+                                                          int chunk, unsigned long long* __restrict__ keys)
 {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool active = i < n;
+    const mirt_ray& rr = rays[active ? i : 0];
+    const Ray ray{rr.origin.x, rr.origin.y, rr.origin.z, rr.direction.x, rr.direction.y, rr.direction.z};
+    const SphRay sp = sph_ray(ray);
+    const int s0 = (int)blockIdx.y * chunk;
+    const int s1 = min(s0 + chunk, sc.num_spheres);
+    float best_t = INFINITY;
+    int best_s = -1;
+    if (s0 < s1 && __ballot(active)) {
+        float4 g = load_geo_uniform(sc.geo, s0);
+        for (int k = s0; k < s1; k++) {
+            const float4 gn = load_geo_uniform(sc.geo, k + 1);  // [num_spheres] is the sentinel: in bounds
+            if (active) {
+                const float t = sphere_t<FAST>(sp, g, best_t);
+                if (t > 0.0f && t < best_t) {
+                    best_t = t;
+                    best_s = k;
+                }
+            }
+            g = gn;
+        }
+    }
+    if (best_s >= 0) atomicMin(&keys[i], ((unsigned long long)__float_as_uint(best_t) << 32) | (unsigned)best_s);
+}
+
+// The hit records of brute_chunk_kernel (hit.c:32-33 for the winner).
+__global__ __launch_bounds__(256) void brute_finish_kernel(DevScene sc, const mirt_ray* __restrict__ rays, int n,
+                                                           const unsigned long long* __restrict__ keys,
+                                                           mirt_hit* __restrict__ out)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const mirt_ray& rr = rays[i];
+    const Ray ray{rr.origin.x, rr.origin.y, rr.origin.z, rr.direction.x, rr.direction.y, rr.direction.z};
+    const unsigned long long k = keys[i];
+    const bool hit = k != ~0ull;
+    store_hit(ray, hit ? __uint_as_float((uint32_t)(k >> 32)) : INFINITY, hit ? (int)(uint32_t)k : -1, sc, &out[i]);
+}
+
+// ray_bvh_intersect(...).hit_something per ray (benchmark.c:239-241).
+template <bool FAST>
+__global__ __launch_bounds__(256) void bvh_any_kernel(DevScene sc, const mirt_ray* __restrict__ rays, int n,
+                                                      int32_t* __restrict__ out)
+{
+    __shared__ uint32_t wstack[kWideStack * kWideStride];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool alive = i < n;
     const mirt_ray& rr = rays[alive ? i : 0];
@@ -682,8 +737,33 @@ __global__ __launch_bounds__(256) void intersect_kernel(DevScene sc, const mirt_
     Counters cnt{0, 0, 0, 0, 0};
     float t;
     int s;
+    closest_hit<false, FAST, false>(sc, ray, alive, t, s, cnt, wstack + threadIdx.x);
+    if (alive) out[i] = s >= 0 ? 1 : 0;
+}
+
+__global__ void keys_to_flags_kernel(const unsigned long long* __restrict__ keys, int n, int32_t* __restrict__ out)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = keys[i] != ~0ull ? 1 : 0;
+}
+
+// ray_bvh_intersect (hit.c:91) / brute-force closest hit (renderer.c:36-43)
+template <bool FAST>
+__global__ __launch_bounds__(256) void intersect_kernel(DevScene sc, const mirt_ray* __restrict__ rays, int n,
+                                                        int use_bvh, mirt_hit* __restrict__ out)
+{
+    __shared__ uint32_t wstack[kWideStack * kWideStride];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool alive = i < n;
+    const mirt_ray& rr = rays[alive ? i : 0];
+    const Ray ray{rr.origin.x, rr.origin.y, rr.origin.z, rr.direction.x, rr.direction.y, rr.direction.z};
+    Counters cnt{0, 0, 0, 0, 0};
+    float t;
+    int s;
+    // arbitrary rays are incoherent: per-lane walks (four-wide where the
+    // tree admits it, each lane with its LDS stack column), not packets
     if (use_bvh)
-        closest_hit<true, FAST, false>(sc, ray, alive, t, s, cnt);
+        closest_hit<false, FAST, false>(sc, ray, alive, t, s, cnt, wstack + threadIdx.x);
     else
         closest_brute<FAST, false>(sc, ray, alive, t, s, cnt);
     if (alive) store_hit(ray, t, s, sc, &out[i]);
@@ -786,6 +866,9 @@ struct mirt_ctx {
     size_t queue_cap = 0;
     uint32_t* d_defer = nullptr;  // [count, list...]
     size_t defer_cap = 0;
+    unsigned long long* d_keys = nullptr;  // chunked brute force: per-ray (t, index) keys
+    size_t keys_cap = 0;
+    int num_cus = 0;
 };
 
 namespace {
@@ -1134,6 +1217,38 @@ int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_ac
     return MIRT_OK;
 }
 
+// Workgroup size of a per-ray batch kernel: one wave per workgroup while the
+// batch is too small to give every CU a few waves (each walk is a chain of
+// dependent loads, so spreading the waves over CUs is what shortens it).
+int batch_threads(const mirt_ctx* c, int n)
+{
+    return n < 256 * 4 * std::max(1, c->num_cus) ? 64 : 256;
+}
+
+// brute_chunk_kernel over the rays in c->d_in: enough sphere chunks that the
+// grid has ~8 workgroups per CU whatever the ray count.
+int launch_brute(mirt_ctx* c, int n)
+{
+    int rc = ensure((void**)&c->d_keys, &c->keys_cap, sizeof(unsigned long long) * (size_t)n);
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(c->d_keys, 0xff, sizeof(unsigned long long) * (size_t)n, c->stream));
+    const int ns = c->num_spheres;
+    if (ns <= 0) return MIRT_OK;
+    const int bx = (n + 255) / 256;
+    const int want = std::max(1, 8 * std::max(1, c->num_cus) / bx);
+    const int chunks = std::min(std::min(want, (ns + 63) / 64), 65535);
+    const int chunk = (ns + chunks - 1) / chunks;
+    const dim3 grid(bx, (ns + chunk - 1) / chunk);
+    const DevScene sc = dev_scene(c);
+    const mirt_ray* d_rays = (const mirt_ray*)c->d_in;
+    if (c->fast_slab)
+        brute_chunk_kernel<true><<<grid, 256, 0, c->stream>>>(sc, d_rays, n, chunk, c->d_keys);
+    else
+        brute_chunk_kernel<false><<<grid, 256, 0, c->stream>>>(sc, d_rays, n, chunk, c->d_keys);
+    HIP_TRY(hipGetLastError());
+    return MIRT_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1164,6 +1279,7 @@ int mirt_create(int device, mirt_ctx** out)
         if (e == hipSuccess)
             e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bounce_kernel<true, 2>, 256, 0);
         c->bounce_blocks = std::max(1, cus) * std::max(1, per_cu);
+        c->num_cus = cus;
     }
     if (e != hipSuccess) {
         mirt_destroy(c);
@@ -1179,7 +1295,7 @@ void mirt_destroy(mirt_ctx* c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : {(void*)c->d_nodes, (void*)c->d_nodes32, (void*)c->d_geo, (void*)c->d_color, (void*)c->d_out, (void*)c->d_acc,
-                    c->d_in, c->d_res, (void*)c->d_counts, (void*)c->d_defer, c->d_queue, (void*)c->d_pnodes,
+                    c->d_in, c->d_res, (void*)c->d_counts, (void*)c->d_defer, c->d_queue, (void*)c->d_keys, (void*)c->d_pnodes,
                     (void*)c->d_hnodes, (void*)c->d_haux, (void*)c->d_leaves})
         if (p) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -1488,15 +1604,59 @@ int mirt_intersect_rays(mirt_ctx* c, const mirt_ray* rays, int n, int use_bvh, m
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(c->d_in, rays, sizeof(mirt_ray) * (size_t)n, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
-    if (c->fast_slab)
-        intersect_kernel<true><<<(n + 255) / 256, 256, 0, c->stream>>>(dev_scene(c), (const mirt_ray*)c->d_in, n,
+    const int bt = batch_threads(c, n);
+    if (!use_bvh) {
+        rc = launch_brute(c, n);
+        if (rc) return rc;
+        brute_finish_kernel<<<(n + 255) / 256, 256, 0, c->stream>>>(dev_scene(c), (const mirt_ray*)c->d_in, n,
+                                                                    c->d_keys, (mirt_hit*)c->d_res);
+    } else if (c->fast_slab) {
+        intersect_kernel<true><<<(n + bt - 1) / bt, bt, 0, c->stream>>>(dev_scene(c), (const mirt_ray*)c->d_in, n,
                                                                       use_bvh, (mirt_hit*)c->d_res);
-    else
-        intersect_kernel<false><<<(n + 255) / 256, 256, 0, c->stream>>>(dev_scene(c), (const mirt_ray*)c->d_in, n,
+    } else {
+        intersect_kernel<false><<<(n + bt - 1) / bt, bt, 0, c->stream>>>(dev_scene(c), (const mirt_ray*)c->d_in, n,
                                                                        use_bvh, (mirt_hit*)c->d_res);
+    }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev1, c->stream));
     HIP_TRY(hipMemcpyAsync(out, c->d_res, sizeof(mirt_hit) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+    return MIRT_OK;
+}
+
+int mirt_any_hit_rays(mirt_ctx* c, const mirt_ray* rays, int n, int use_bvh, int32_t* out)
+{
+    if (!ctx_ok(c, true, "mirt_any_hit_rays")) return MIRT_E_NOSCENE;
+    if (n < 0 || (n > 0 && (!rays || !out))) {
+        set_error("mirt_any_hit_rays: invalid arguments");
+        return MIRT_E_INVALID;
+    }
+    if (use_bvh && c->num_nodes == 0) {
+        set_error("mirt_any_hit_rays: use_bvh set but no tree uploaded");
+        return MIRT_E_NOSCENE;
+    }
+    if (n == 0) return MIRT_OK;
+    int rc = ensure(&c->d_in, &c->in_cap, sizeof(mirt_ray) * (size_t)n);
+    if (!rc) rc = ensure(&c->d_res, &c->res_cap, sizeof(int32_t) * (size_t)n);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(c->d_in, rays, sizeof(mirt_ray) * (size_t)n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipEventRecord(c->ev0, c->stream));
+    const int bt = batch_threads(c, n);
+    if (!use_bvh) {
+        rc = launch_brute(c, n);
+        if (rc) return rc;
+        keys_to_flags_kernel<<<(n + 255) / 256, 256, 0, c->stream>>>(c->d_keys, n, (int32_t*)c->d_res);
+    } else if (c->fast_slab) {
+        bvh_any_kernel<true><<<(n + bt - 1) / bt, bt, 0, c->stream>>>(dev_scene(c), (const mirt_ray*)c->d_in, n,
+                                                                    (int32_t*)c->d_res);
+    } else {
+        bvh_any_kernel<false><<<(n + bt - 1) / bt, bt, 0, c->stream>>>(dev_scene(c), (const mirt_ray*)c->d_in, n,
+                                                                     (int32_t*)c->d_res);
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev1, c->stream));
+    HIP_TRY(hipMemcpyAsync(out, c->d_res, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     HIP_TRY(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
     return MIRT_OK;

@@ -57,6 +57,14 @@ def create_benchmark_spheres(n, seed=1, world_size=1000.0, state=None):
     return out
 
 
+def create_bench_rays(n, state):
+    """n rays of benchmark.c:176-185 (origin 0, normalised random direction)
+    drawn from `state` (a RandState continuing the scene's glibc stream)."""
+    out = np.zeros(n, abi.RAY)
+    check(load().mirt_bench_rays(C.byref(state.st), ptr(out), n), "mirt_bench_rays")
+    return out
+
+
 def default_camera():
     cam = abi.Camera()
     load().mirt_camera_default(C.byref(cam))
@@ -271,6 +279,14 @@ class Renderer:
         out = np.zeros(len(rays), abi.HIT)
         check(self.L.mirt_intersect_rays(self.h, ptr(rays), len(rays), int(use_bvh), ptr(out)),
               "mirt_intersect_rays")
+        return out
+
+    def any_hit(self, rays, use_bvh=False):
+        """int32 per ray: 1 if it hits some sphere (benchmark.c:190-199
+        brute force; with use_bvh, ray_bvh_intersect's hit_something)."""
+        rays = np.ascontiguousarray(rays, abi.RAY)
+        out = np.zeros(len(rays), np.int32)
+        check(self.L.mirt_any_hit_rays(self.h, ptr(rays), len(rays), int(use_bvh), ptr(out)), "mirt_any_hit_rays")
         return out
 
     def ray_bvh_intersect(self, rays):

@@ -150,6 +150,9 @@ int mirt_rand(mirt_rand_state *st);
 int mirt_scene_random(mirt_rand_state *st, mirt_sphere *out, int n);
 /* n x benchmark centre + create_benchmark_sphere() (benchmark.c:307-314, sphere.c:34-41). */
 int mirt_scene_benchmark(mirt_rand_state *st, mirt_sphere *out, int n, float world_size);
+/* n benchmark rays (benchmark.c:176-185, 228-237): origin 0, direction
+   vec3_normalize of three (float)rand()/RAND_MAX*2-1 draws. */
+int mirt_bench_rays(mirt_rand_state *st, mirt_ray *out, int n);
 /* The default camera of main.c:203-211. */
 void mirt_camera_default(mirt_camera *cam);
 /* camera_update (camera.c:10-18): basis from yaw/pitch. */
@@ -220,6 +223,15 @@ int mirt_trace_rays(mirt_ctx *ctx, const mirt_ray *rays, int n, int depth, int u
 /* Closest hit: ray_bvh_intersect (hit.c:91-109) when use_bvh, else the brute
    force loop of renderer.c:36-43. */
 int mirt_intersect_rays(mirt_ctx *ctx, const mirt_ray *rays, int n, int use_bvh, mirt_hit *out);
+
+/* benchmark.c:172-255 as batches. Any hit: out[i] = 1 if ray i hits some
+   sphere (benchmark_no_bvh's hit_found, benchmark.c:190-199, when use_bvh =
+   0; ray_bvh_intersect(...).hit_something, benchmark.c:239-241, when 1).
+   Both intersect calls split the brute-force loop over sphere chunks across
+   the chip (64-bit atomicMin of (t, index): the first sphere wins ties as in
+   renderer.c:39; every sphere is tested, as the reference does). The device
+   time of the call's kernels is mirt_last_kernel_ms(). */
+int mirt_any_hit_rays(mirt_ctx *ctx, const mirt_ray *rays, int n, int use_bvh, int32_t *out);
 
 /* Element-wise ray_sphere_intersect (hit.c:19-39) / ray_aabb_intersect
    (hit.c:49-82) on pairs; need no scene. */

@@ -165,11 +165,27 @@ class Reference:
             "h_render": (None, [P, P, I, P, I, I, I, C.c_uint64, C.c_uint32, I, I, I, P, I]),
             "h_trace_rays": (None, [P, I, P, I, P, I, I, I, C.c_uint64, C.c_uint32, P]),
             "h_camera_update": (None, [P]),
+            "h_bench_point": (None, [I, I, C.c_float, P, P, P, P, P, P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
             f.restype, f.argtypes = res, args
         assert (L.h_width(), L.h_height()) == (W, H)
+
+    def bench_point(self, n, num_rays, world=1000.0):
+        """One sweep point of benchmark.c's run_benchmark_with_plotting on the
+        current rand() stream (srand first): spheres, rays and hit flags of
+        both loops, and their clock() seconds."""
+        s = np.zeros(n, abi.SPHERE)
+        ra, rb = np.zeros(num_rays, abi.RAY), np.zeros(num_rays, abi.RAY)
+        ha, hb = np.zeros(num_rays, np.int32), np.zeros(num_rays, np.int32)
+        secs = np.zeros(2, np.float64)
+        self.L.h_bench_point(n, num_rays, world, _p(s), _p(ra), _p(rb), _p(ha), _p(hb), _p(secs))
+        return {"spheres": s, "rays_no_bvh": ra, "rays_bvh": rb, "hit_no_bvh": ha, "hit_bvh": hb,
+                "secs": (float(secs[0]), float(secs[1]))}
+
+    def srand(self, seed):
+        self.L.h_srand(seed)
 
     def render_scene(self, seed, n):
         out = np.zeros(n, abi.SPHERE)

@@ -19,6 +19,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "Custom/constants.h"
 #include "Custom/bvh.h"
@@ -136,6 +137,63 @@ void h_intersect_bvh(void *root, const Sphere *base, const Ray *rays, int n, mir
         HitRecord h = ray_bvh_intersect(rays[i], (BVHNode *)root);
         put_hit(&h, base, &out[i]);
     }
+}
+
+/* One point of run_benchmark_with_plotting (benchmark.c:283-332) on the
+   CURRENT rand() stream (h_srand once, then the points in sweep order):
+   n spheres (benchmark.c:307-314), build_bvh_node(s, 0, n - 1, 20)
+   (benchmark.c:317), then the loops of benchmark_no_bvh (benchmark.c:
+   172-222) and benchmark_with_bvh (benchmark.c:224-255) around the
+   reference's own vec3_normalize / ray_sphere_intersect / ray_bvh_intersect,
+   timed with clock() as there. Out: the spheres (post-build order), the two
+   ray sets, per-ray hit flags, seconds of each loop. */
+void h_bench_point(int n, int num_rays, float world_size, Sphere *s_out, Ray *rays_a, Ray *rays_b,
+                   int32_t *hit_a, int32_t *hit_b, double *secs)
+{
+    g_mode = 0;
+    Sphere *s = malloc((size_t)n * sizeof(Sphere));
+    for (int j = 0; j < n; j++) {
+        Vec3 c = {
+            (float)rand() / RAND_MAX * world_size - world_size / 2,
+            (float)rand() / RAND_MAX * world_size - world_size / 2,
+            (float)rand() / RAND_MAX * world_size - world_size / 2};
+        s[j] = create_benchmark_sphere(c);
+    }
+    BVHNode *root = build_bvh_node(s, 0, n - 1, 20);
+    clock_t t0 = clock();
+    for (int i = 0; i < num_rays; i++) {
+        Vec3 dir = {
+            (float)rand() / RAND_MAX * 2 - 1,
+            (float)rand() / RAND_MAX * 2 - 1,
+            (float)rand() / RAND_MAX * 2 - 1};
+        dir = vec3_normalize(dir);
+        Ray ray = {{0, 0, 0}, dir};
+        int found = 0;
+        for (int j = 0; j < n; j++) {
+            HitRecord h = ray_sphere_intersect(ray, &s[j]);
+            if (h.hit_something) found = 1;
+        }
+        rays_a[i] = ray;
+        hit_a[i] = found;
+    }
+    clock_t t1 = clock();
+    for (int i = 0; i < num_rays; i++) {
+        Vec3 dir = {
+            (float)rand() / RAND_MAX * 2 - 1,
+            (float)rand() / RAND_MAX * 2 - 1,
+            (float)rand() / RAND_MAX * 2 - 1};
+        dir = vec3_normalize(dir);
+        Ray ray = {{0, 0, 0}, dir};
+        HitRecord h = ray_bvh_intersect(ray, root);
+        rays_b[i] = ray;
+        hit_b[i] = h.hit_something;
+    }
+    clock_t t2 = clock();
+    secs[0] = (double)(t1 - t0) / CLOCKS_PER_SEC;
+    secs[1] = (double)(t2 - t1) / CLOCKS_PER_SEC;
+    memcpy(s_out, s, (size_t)n * sizeof(Sphere));
+    free_tree(root);
+    free(s);
 }
 
 void h_sphere_pairs(const Ray *rays, Sphere *s, int n, mirt_hit *out)
