@@ -121,6 +121,7 @@ SIGNATURES = [
     ("mirt_camera_rays", I, [P, P, P, P]),
     ("mirt_count_frame", I, [P, P, P, P]),
     ("mirt_wave_stats", I, [P, P, P, P, I]),
+    ("mirt_ctx_stream", P, [P]),
     ("mirt_last_kernel_ms", C.c_float, [P]),
     ("mirt_last_phase_ms", I, [P, C.POINTER(C.c_float)]),
     ("mirt_bounce_stats", I, [P, P, P, P, I]),

@@ -1710,6 +1710,11 @@ int mirt_aabb_pairs(mirt_ctx* c, const mirt_ray* rays, const mirt_aabb* boxes, i
 
 float mirt_last_kernel_ms(mirt_ctx* c) { return c ? c->last_ms : 0.0f; }
 
+void* mirt_ctx_stream(mirt_ctx* c)
+{
+    return c ? (void*)c->stream : nullptr;
+}
+
 int mirt_last_phase_ms(mirt_ctx* c, float* phase)
 {
     if (!c || !phase) return MIRT_E_INVALID;

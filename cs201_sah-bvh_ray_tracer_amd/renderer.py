@@ -250,6 +250,11 @@ class Renderer:
         return out
 
     @property
+    def stream_handle(self):
+        """The ctx's own hipStream_t (int)."""
+        return self.L.mirt_ctx_stream(self.h) or 0
+
+    @property
     def last_kernel_ms(self):
         return self.L.mirt_last_kernel_ms(self.h)
 

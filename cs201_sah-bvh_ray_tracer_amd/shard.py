@@ -74,14 +74,21 @@ def as_rgba(frame_i32):
 
 
 class ShardedFrame:
-    """Renders one frame with this rank's mirt Renderer and gathers it.
+    """Renders frames with this rank's mirt Renderer(s) and gathers them.
 
     renderer: a renderer.Renderer bound to this rank's GPU with the scene
-    uploaded. Uses torch's current stream for both the kernel and RCCL.
+    uploaded. With `renderers` (two or more contexts on the same GPU, the
+    same scene uploaded to each) successive frames alternate between them,
+    each on its own stream with its own slabs and queue: frame k + 1's
+    launches are enqueued while frame k's bounce pass is still draining its
+    last chains, so the GPU fills the slots those waves free (double
+    buffering; each frame's bytes are unchanged). Otherwise torch's current
+    stream carries the kernel and RCCL.
     """
 
-    def __init__(self, renderer, width, height, row_block=8, group=None, samples=1):
-        self.r = renderer
+    def __init__(self, renderer, width, height, row_block=8, group=None, samples=1, renderers=None):
+        self.rs = list(renderers) if renderers else [renderer]
+        self.r = self.rs[0]
         self.width, self.height, self.row_block = width, height, row_block
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -89,10 +96,20 @@ class ShardedFrame:
         self.samples = samples
         dev = torch.device("cuda", torch.cuda.current_device())
         self.rows = slab_rows(height, row_block, self.world)
-        # one slab per frame in flight; slab 0 is the display that is gathered
-        self.slabs = torch.zeros((samples, self.rows, width), dtype=torch.int32, device=dev)
-        self.slab = self.slabs[0]
-        self.acc = torch.zeros((self.rows, width, 3), dtype=torch.float32, device=dev) if samples > 1 else None
+        # per context: one slab per frame in flight (slab 0 is the display
+        # that is gathered) and the accumulation buffer of a multi-frame launch
+        self.bufs = []
+        for _ in self.rs:
+            slabs = torch.zeros((samples, self.rows, width), dtype=torch.int32, device=dev)
+            acc = torch.zeros((self.rows, width, 3), dtype=torch.float32, device=dev) if samples > 1 else None
+            self.bufs.append((slabs, acc))
+        # each context's own stream (created by mirt_create), seen by torch as
+        # an external stream
+        self.streams = ([torch.cuda.ExternalStream(x.stream_handle) for x in self.rs] if len(self.rs) > 1
+                        else [None])
+        self.k = 0
+        self.slab = self.bufs[0][0][0]
+        self.stream = None
 
     def desc(self, depth=5, use_bvh=True, seed=1, sample=0, accumulate=False, frames=1):
         from .renderer import frame_desc
@@ -100,14 +117,24 @@ class ShardedFrame:
                           self.rank, self.world, self.samples)
 
     def render_local(self, cam, fd):
-        stream = torch.cuda.current_stream().cuda_stream
-        self.r.render_frame_device(cam, fd, self.slabs.data_ptr(),
-                                   self.acc.data_ptr() if self.acc is not None else None, stream)
+        """Enqueue this rank's rows of the next frame; returns its display slab."""
+        i = self.k % len(self.rs)
+        self.k += 1
+        slabs, acc = self.bufs[i]
+        self.stream = self.streams[i] or torch.cuda.current_stream()
+        self.rs[i].render_frame_device(cam, fd, slabs.data_ptr(), acc.data_ptr() if acc is not None else None,
+                                       self.stream.cuda_stream)
+        self.slab = slabs[0]
         return self.slab
+
+    def gather(self):
+        """Gather the last rendered slab (on its stream); the frame on rank 0."""
+        with torch.cuda.stream(self.stream):
+            if self.world == 1:
+                return assemble(self.slab.unsqueeze(0), self.height, self.row_block)
+            return gather_frame(self.slab, self.height, self.row_block, self.group)
 
     def render(self, cam, fd):
         """Render this rank's rows and gather; the (H, W) int32 frame on rank 0."""
         self.render_local(cam, fd)
-        if self.world == 1:
-            return assemble(self.slab.unsqueeze(0), self.height, self.row_block)
-        return gather_frame(self.slab, self.height, self.row_block, self.group)
+        return self.gather()

@@ -260,6 +260,10 @@ int mirt_wave_stats(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_desc
    (or -waves if cap is too small). */
 int mirt_bounce_stats(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_desc *fd, uint64_t *out, int cap);
 
+/* The ctx's own stream (a hipStream_t, non-blocking): the blocking calls run
+   on it; a caller may pass it to mirt_render_frame_device. */
+void *mirt_ctx_stream(mirt_ctx *ctx);
+
 /* Device time (ms) of the last render kernel launched by a blocking call. */
 float mirt_last_kernel_ms(mirt_ctx *ctx);
 

@@ -19,7 +19,8 @@ mirt = importlib.import_module("cs201_sah-bvh_ray_tracer_amd")
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--spheres", type=int, default=10000)
-    ap.add_argument("--threshold", type=int, default=40)
+    ap.add_argument("--threshold", type=int, default=32)
+    ap.add_argument("--dump", default=None, help="save the raw per-wave records (.npy)")
     a = ap.parse_args()
     s = mirt.create_random_spheres(a.spheres, 1)
     b = mirt.build_bvh(s)
@@ -29,6 +30,8 @@ def main():
     cam = mirt.default_camera()
     r.bounce_stats(cam, 1920, 1080)
     d = r.bounce_stats(cam, 1920, 1080).astype(np.float64)
+    if a.dump:
+        np.save(a.dump, d)
     t0 = d[:, 4].min()
     end = (d[:, 6] - t0) / 100.0
     dry = d[:, 5][d[:, 5] > 0]

@@ -23,9 +23,10 @@ for s in $STEPS; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()";;
     tests) step pytest_gpu 1200 python -m pytest tests -m gpu -x -q;;
     bench) step bench 600 python bench.py;;
-    prof)  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu;;
-    pmc)   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --no-cpu --no-host --steps 5 --warmup 1
-           step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --no-cpu --no-host --steps 5 --warmup 1;;
+    # one launch at a time (--pipeline 1): per-kernel durations as bench.py's serial measurement loop sees them
+    prof)  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu --pipeline 1;;
+    pmc)   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --no-cpu --no-host --steps 5 --warmup 1 --pipeline 1
+           step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --no-cpu --no-host --steps 5 --warmup 1 --pipeline 1;;
   esac
 done
 echo "done"
