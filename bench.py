@@ -44,6 +44,22 @@ mirt = importlib.import_module("cs201_sah-bvh_ray_tracer_amd")
 shard = importlib.import_module("cs201_sah-bvh_ray_tracer_amd.shard")
 
 W, H, NSPH, DEPTH, SEED, ROW_BLOCK = 1920, 1080, 10000, 5, 1, 8
+KIND, SPP, JITTER = "render", 1, False
+# --workload: BASELINE.json configs (the default is configs[1], the metric's
+# own configuration; the others are measured on request, one GPU or more)
+WORKLOADS = {
+    "1080p_10k": dict(W=1920, H=1080, KIND="render", NSPH=10000, SPP=1, JITTER=False,
+                      desc="1920x1080, 10000 random spheres, 1 primary ray/pixel, diffuse shading depth 5 "
+                           "(BASELINE configs[1])"),
+    "1080p_100k": dict(W=1920, H=1080, KIND="render", NSPH=100000, SPP=1, JITTER=False,
+                       desc="1920x1080, 100000 random spheres (deep BVH, LDS-stack stress), depth 5 "
+                            "(BASELINE configs[2])"),
+    "4k_10k": dict(W=3840, H=2160, KIND="render", NSPH=10000, SPP=1, JITTER=False,
+                   desc="3840x2160, 10000 random spheres, depth 5 (BASELINE configs[3])"),
+    "4k_1m_4spp": dict(W=3840, H=2160, KIND="bench", NSPH=1000000, SPP=4, JITTER=True,
+                       desc="3840x2160, 1000000 benchmark spheres (benchmark.c:307-314, built over [0, N)), "
+                            "4 spp jittered, depth 5 (BASELINE configs[4])"),
+}
 PEAK_HBM_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 NODE_B, SPHERE_B, COLOR_B, PIXEL_B = 32, 16, 4, 4
 KERNEL = "bounce_kernel<true, 2, false>"   # dominant kernel of the default (wavefront, four-wide) schedule
@@ -76,7 +92,8 @@ def cpu_baseline(target_s=12.0):
     except (FileNotFoundError, OSError):
         ref, kind = None, "port"
     o = Oracle()
-    s = o.render_scene(SEED, NSPH)                 # same scene (bit-identical generator)
+    # same scene (bit-identical generator), same tree ([0, N), depth 0)
+    s = o.render_scene(SEED, NSPH) if KIND == "render" else o.bench_scene(SEED, NSPH)
     cam = mirt.default_camera()
     if ref is not None:
         s_ref = s.copy()
@@ -85,7 +102,7 @@ def cpu_baseline(target_s=12.0):
         def run(step, nthreads):
             t0 = time.perf_counter()
             img = ref.render(cam, s_ref, tree, depth=DEPTH, mode=1, seed=SEED, row0=0, step=step,
-                             threads=nthreads)
+                             threads=nthreads, jitter=JITTER)
             return time.perf_counter() - t0, img.shape[0]
     else:
         tree = o.build(s)
@@ -93,7 +110,7 @@ def cpu_baseline(target_s=12.0):
         def run(step, nthreads):
             rows = np.arange(0, H, step, dtype=np.int32)
             t0 = time.perf_counter()
-            o.render(cam, W, H, s, tree, depth=DEPTH, mode=1, seed=SEED, rows=rows, threads=nthreads)
+            o.render(cam, W, H, s, tree, depth=DEPTH, mode=1, seed=SEED, rows=rows, threads=nthreads, jitter=JITTER)
             return time.perf_counter() - t0, len(rows)
 
     def sample(step, nthreads, budget):
@@ -118,8 +135,9 @@ def cpu_baseline(target_s=12.0):
     else:
         o.free(tree)
     return {"value": round(value, 5), "unit": "Mrays/s", "cores": threads, "kind": kind,
-            "sample": f"every {step}th row of the 1920x1080 frame x {reps} ({rows} rows, {rows * W} primary rays, "
-                      f"depth {DEPTH}, {threads} OpenMP threads, row-dynamic schedule) in {t:.1f} s",
+            "sample": f"every {step}th row of the {W}x{H} frame (sample 0{', jittered' if JITTER else ''}) x {reps} "
+                      f"({rows} rows, {rows * W} primary rays, depth {DEPTH}, {threads} OpenMP threads, "
+                      f"row-dynamic schedule) in {t:.1f} s",
             "single_core_value": round(value1, 5),
             "single_core_sample": f"every {step1}th row x {reps1} ({rows1} rows) in {t1:.1f} s"}
 
@@ -146,11 +164,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-host", action="store_true", help="skip the host-inclusive (D2H) leg")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="1080p_10k")
     ap.add_argument("--pipeline", type=int, default=3,
                     help="device contexts alternating successive steps on their own streams (1 = serial)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
                     help="weak: N frames in flight per step at N GPUs (default); strong: one frame split N ways")
     args = ap.parse_args()
+    global W, H, NSPH, KIND, SPP, JITTER
+    wl = WORKLOADS[args.workload]
+    W, H, NSPH, KIND, SPP, JITTER = wl["W"], wl["H"], wl["NSPH"], wl["KIND"], wl["SPP"], wl["JITTER"]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -163,7 +185,8 @@ def main():
         torch.cuda.set_device(0)
     assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
 
-    spheres = mirt.create_random_spheres(NSPH, SEED)
+    spheres = (mirt.create_random_spheres(NSPH, SEED) if KIND == "render"
+               else mirt.create_benchmark_spheres(NSPH, SEED))
     t0 = time.perf_counter()
     bvh = mirt.build_bvh(spheres)
     build_s = time.perf_counter() - t0
@@ -173,18 +196,19 @@ def main():
         x.upload(spheres, bvh)
     r = rs[0]
     cam = mirt.default_camera()
-    frames = world if args.scaling == "weak" else 1   # frames in flight per step
+    # frames (accumulated samples) in flight per step: SPP per frame x N at N GPUs (weak scaling)
+    frames = SPP * (world if args.scaling == "weak" else 1)
     sf = shard.ShardedFrame(r, W, H, ROW_BLOCK, samples=frames, renderers=rs)
-    fd = sf.desc(depth=DEPTH, seed=SEED)
+    fd = sf.desc(depth=DEPTH, seed=SEED, jitter=JITTER)
     my_rows = shard.shard_row_count(H, ROW_BLOCK, world, rank)
 
     # algorithmic work of this rank's launch (instrumented build, untimed):
     # the walk as configured (pruned), and the reference's exhaustive DFS
     counts = r.count_frame(cam, W, H, depth=DEPTH, seed=SEED, row_block=ROW_BLOCK, shard=rank, num_shards=world,
-                           samples=frames)
+                           samples=frames, jitter=JITTER)
     r.set_option(mirt.abi.OPT_PRUNE, 0)
     ref_counts = r.count_frame(cam, W, H, depth=DEPTH, seed=SEED, row_block=ROW_BLOCK, shard=rank,
-                               num_shards=world, samples=frames)
+                               num_shards=world, samples=frames, jitter=JITTER)
     r.set_option(mirt.abi.OPT_PRUNE, 1)
     alg_bytes = algorithmic_bytes(counts, my_rows * W * frames)
 
@@ -211,6 +235,24 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
+    # depth 1 alongside (camera rays and their shading only),
+    # same pipeline, same step
+    fd1 = sf.desc(depth=1, seed=SEED, jitter=JITTER)
+    for _ in range(2):
+        sf.render_local(cam, fd1)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    for k in range(args.steps):
+        sf.render_local(cam, fd1)
+        if world > 1:
+            sf.gather()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed_d1 = time.perf_counter() - t1
+
     # per-kernel split of the same launch, one context, serial (untimed loop:
     # each launch waits for its events): torch events around the launch and
     # the HIP events the library records around the primary and bounce passes
@@ -229,13 +271,13 @@ def main():
     primary_ms, bounce_ms = (float(v) for v in np.mean(np.array(phases), axis=0))
     kernel_ms = float(np.mean(launch))
 
-    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
+    t = torch.tensor([elapsed, kernel_ms, elapsed_d1], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kernel_ms_max = float(t[0]), float(t[1])
+    elapsed, kernel_ms_max, elapsed_d1 = float(t[0]), float(t[1]), float(t[2])
 
     if rank == 0:
-        value = W * H * frames * args.steps / elapsed / 1e6
+        value = W * H * frames * args.steps / elapsed / 1e6   # primary rays: W*H per sample
         frame_gbs = alg_bytes / (kernel_ms / 1e3) / 1e9
         b_bytes = bounce_bytes(counts)
         achieved = b_bytes / (bounce_ms / 1e3) / 1e9
@@ -243,11 +285,11 @@ def main():
         # the same frame through the blocking host API (kernel + D2H over PCIe)
         host = None
         if world == 1 and not args.no_host:
-            img = r.render_frame(cam, W, H, depth=DEPTH, seed=SEED)
+            img = r.render_frame(cam, W, H, depth=DEPTH, seed=SEED, samples=SPP, jitter=JITTER)
             t1 = time.perf_counter()
             for _ in range(5):
-                img = r.render_frame(cam, W, H, depth=DEPTH, seed=SEED)
-            host = W * H * 5 / (time.perf_counter() - t1) / 1e6
+                img = r.render_frame(cam, W, H, depth=DEPTH, seed=SEED, samples=SPP, jitter=JITTER)
+            host = W * H * SPP * 5 / (time.perf_counter() - t1) / 1e6
         line = {
             "metric": "Mrays/s at 1080p, 10k spheres; 1/2/4/8 GPU + CPU baseline",
             "value": round(value, 3),
@@ -261,9 +303,9 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (create_random_sphere scene, srand(1); default camera main.c:203-211)",
-            "config": {"workload": "1920x1080, 10000 random spheres, 1 primary ray/pixel, diffuse shading "
-                                   "depth 5 (BASELINE configs[1])",
-                       "width": W, "height": H, "spheres": NSPH, "max_depth": DEPTH, "spp": 1,
+            "config": {"workload": wl["desc"], "name": args.workload,
+                       "width": W, "height": H, "spheres": NSPH, "scene": KIND, "max_depth": DEPTH, "spp": SPP,
+                       "jitter": JITTER,
                        "frames_per_step": frames, "pipeline": len(rs), "bvh_nodes": len(bvh),
                        "row_block": ROW_BLOCK,
                        "parallelism": f"row-block shard x{world}" + (" + RCCL gather" if world > 1 else "")
@@ -284,6 +326,7 @@ def main():
             "work": {k: int(v) for k, v in counts.items()},
             "work_reference_dfs": {k: int(v) for k, v in ref_counts.items() if k != "lane_steps"},
             "traced_rays_per_s_M": round(counts["rays"] * world / (kernel_ms_max / 1e3) / 1e6, 3),
+            "depth1_mrays_s": round(W * H * frames * args.steps / elapsed_d1 / 1e6, 3),
             "host_inclusive_mrays_s": None if host is None else round(host, 3),
             "bvh_build_s": round(build_s, 4),
         }

@@ -54,7 +54,8 @@ class FrameDesc(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("max_depth", C.c_int32),
                 ("use_bvh", C.c_int32), ("seed", C.c_uint64), ("sample", C.c_uint32),
                 ("accumulate", C.c_int32), ("frames", C.c_int32), ("row_block", C.c_int32),
-                ("shard", C.c_int32), ("num_shards", C.c_int32), ("samples", C.c_int32)]
+                ("shard", C.c_int32), ("num_shards", C.c_int32), ("samples", C.c_int32),
+                ("jitter", C.c_int32)]
 
 
 class Counts(C.Structure):

@@ -34,6 +34,7 @@ struct FrameConst {
     int accumulate;
     float frames;
     int row_block, shard, num_shards;
+    int jitter;        // sub-pixel jitter of camera rays from the RNG contract (camera_ray)
     int num_rows;      // rows of this launch: shard_rows x samples (frame j's rows follow frame j-1's)
     int shard_rows;    // rows of one frame of this shard
     int samples;       // frames in this launch (RNG samples sample .. sample + samples - 1)
@@ -67,6 +68,7 @@ FrameConst make_frame_const(const mirt_camera* cam, const mirt_frame_desc* fd)
     f.num_shards = fd->num_shards;
     f.shard_rows = shard_row_count(fd);
     f.samples = fd->samples > 1 ? fd->samples : 1;
+    f.jitter = fd->jitter != 0;
     f.num_rows = f.shard_rows * f.samples;
     return f;
 }
@@ -85,11 +87,21 @@ __device__ __forceinline__ uint32_t row_sample(const FrameConst& f, int r)
     return f.samples > 1 ? f.sample + (uint32_t)(r / f.shard_rows) : f.sample;
 }
 
-// main.c:362-365 + ray.c:26-31 for pixel (x, y).
-__device__ __forceinline__ Ray camera_ray(const FrameConst& f, int x, int y)
+// main.c:362-365 + ray.c:26-31 for pixel (x, y) of RNG sample `sample`.
+// Jittered frames (mirt_frame_desc.jitter; BASELINE configs[4] "4 spp
+// jittered" -- the reference has no jitter, so the build defines it): the
+// sample point moves by (jx, jy) in [0, 1)^2, two draws of the pixel's RNG
+// contract stream at indices its bounce sampling never reaches (rng.h).
+__device__ __forceinline__ Ray camera_ray(const FrameConst& f, int x, int y, uint32_t sample)
 {
-    const float u = ((float)x / f.wf - 0.5f) * f.aspect;
-    const float v = -((float)y / f.hf - 0.5f);
+    float xf = (float)x, yf = (float)y;
+    if (f.jitter) {
+        const uint64_t key = pixel_key(f.seed, (uint32_t)(y * f.width + x), sample);
+        xf = xf + (float)draw(key, kJitterDrawX) / 2147483648.0f;
+        yf = yf + (float)draw(key, kJitterDrawY) / 2147483648.0f;
+    }
+    const float u = (xf / f.wf - 0.5f) * f.aspect;
+    const float v = -(yf / f.hf - 0.5f);
     float dx = f.fx + f.hx * u, dy = f.fy + f.hy * u, dz = f.fz + f.hz * u;
     dx = dx + f.vx * v;
     dy = dy + f.vy * v;
@@ -132,7 +144,7 @@ __device__ __forceinline__ void render_pixel(const DevScene& sc, const FrameCons
                                              uint32_t* wstk = nullptr)
 {
     const int y = alive ? shard_row_to_y(f, r) : 0;
-    const Ray ray = camera_ray(f, alive ? x : 0, y);
+    const Ray ray = camera_ray(f, alive ? x : 0, y, row_sample(f, r));
     if (skip_generic && alive && slab_ray(ray).generic) alive = false;  // a deferred wave traces it
     const uint64_t key = pixel_key(f.seed, (uint32_t)(y * f.width + x), row_sample(f, r));
     const uint32_t c = trace_path<TRAV, FAST, COUNT>(sc, ray, alive, f.depth, f.use_bvh != 0, key, cnt, cstack,
@@ -209,7 +221,7 @@ __global__ void mark_deferred_kernel(FrameConst f, uint32_t* __restrict__ list, 
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int r = blockIdx.y;
     if (x >= f.width || r >= f.num_rows) return;
-    const Ray ray = camera_ray(f, x, shard_row_to_y(f, r));
+    const Ray ray = camera_ray(f, x, shard_row_to_y(f, r), row_sample(f, r));
     if (slab_ray(ray).generic) list[atomicAdd(count, 1u)] = (uint32_t)(r * f.width + x);
 }
 
@@ -318,7 +330,7 @@ __global__ __launch_bounds__(256) void primary_kernel(DevScene sc, FrameConst f,
     const int r = (tile / tiles_x) * 8 + (lane >> 3);
     bool alive = x < f.width && r < f.num_rows;
     const int y = alive ? shard_row_to_y(f, r) : 0;
-    const Ray ray = camera_ray(f, alive ? x : 0, y);
+    const Ray ray = camera_ray(f, alive ? x : 0, y, row_sample(f, r));
     if (!ORD && dfr.blocks > 0 && alive && slab_ray(ray).generic) alive = false;  // traced by a deferred wave
     float t;
     int s;
@@ -811,7 +823,7 @@ __global__ void camera_rays_kernel(FrameConst f, mirt_ray* __restrict__ out)
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int r = blockIdx.y;
     if (x >= f.width || r >= f.num_rows) return;
-    const Ray ray = camera_ray(f, x, shard_row_to_y(f, r));
+    const Ray ray = camera_ray(f, x, shard_row_to_y(f, r), row_sample(f, r));
     out[(size_t)r * f.width + x] = {{ray.ox, ray.oy, ray.oz}, {ray.dx, ray.dy, ray.dz}};
 }
 

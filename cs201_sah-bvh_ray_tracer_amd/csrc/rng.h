@@ -39,4 +39,9 @@ MIRT_HD int draw(uint64_t key, uint32_t k)
     return (int)(mix64(key + (uint64_t)(k + 1u) * 0x9E3779B97F4A7C15ull) >> 33);
 }
 
+// Jittered frames: the camera ray's sample point is (x + jx, y + jy) with
+// j = (float)draw(key, kJitterDraw*) / 2^31 in [0, 1) -- draws at indices the
+// bounce sampling (k = 0, 1, ...; a few dozen per pixel) never reaches.
+constexpr uint32_t kJitterDrawX = 0x7ffffff0u, kJitterDrawY = 0x7ffffff1u;
+
 }  // namespace mirt

@@ -127,12 +127,13 @@ def flatten_bvh(root, spheres):
 
 
 def frame_desc(width, height, depth=5, use_bvh=True, seed=1, sample=0, accumulate=False, frames=1,
-               row_block=8, shard=0, num_shards=1, samples=1):
+               row_block=8, shard=0, num_shards=1, samples=1, jitter=False):
     fd = abi.FrameDesc()
     fd.width, fd.height, fd.max_depth, fd.use_bvh = width, height, depth, int(use_bvh)
     fd.seed, fd.sample, fd.accumulate, fd.frames = seed, sample, int(accumulate), frames
     fd.row_block, fd.shard, fd.num_shards = row_block, shard, num_shards
     fd.samples = samples
+    fd.jitter = int(jitter)
     return fd
 
 
@@ -188,13 +189,13 @@ class Renderer:
 
     # ---- frames
     def render_frame(self, cam, width, height, depth=5, use_bvh=True, seed=1, sample=0, accumulate=False,
-                     frames=1, row_block=8, shard=0, num_shards=1, samples=1):
+                     frames=1, row_block=8, shard=0, num_shards=1, samples=1, jitter=False):
         """main.c:356-374 (fresh) or main.c:379-408 (accumulate) for one shard;
         returns (rows, width, 4) uint8 in the shard's row order. samples > 1:
         that many successive frames (RNG samples sample, sample + 1, ...) in
         one launch, accumulated; returns the display after the last."""
         fd = frame_desc(width, height, depth, use_bvh, seed, sample, accumulate, frames, row_block, shard,
-                        num_shards, samples)
+                        num_shards, samples, jitter)
         n = check(self.L.mirt_shard_rows(C.byref(fd), None), "mirt_shard_rows")
         out = np.zeros((n, width, 4), np.uint8)
         check(self.L.mirt_render_frame(self.h, C.byref(cam), C.byref(fd), ptr(out)), "mirt_render_frame")
@@ -212,10 +213,10 @@ class Renderer:
         return out
 
     def count_frame(self, cam, width, height, depth=5, use_bvh=True, seed=1, sample=0, row_block=8, shard=0,
-                    num_shards=1, samples=1):
+                    num_shards=1, samples=1, jitter=False):
         """Work of one launch (samples frames): rays, node tests, sphere tests, hits."""
         fd = frame_desc(width, height, depth, use_bvh, seed, sample, False, 1, row_block, shard, num_shards,
-                        samples)
+                        samples, jitter)
         c = abi.Counts()
         check(self.L.mirt_count_frame(self.h, C.byref(cam), C.byref(fd), C.byref(c)), "mirt_count_frame")
         return {k: getattr(c, k) for k, _ in abi.Counts._fields_}

@@ -111,10 +111,10 @@ class ShardedFrame:
         self.slab = self.bufs[0][0][0]
         self.stream = None
 
-    def desc(self, depth=5, use_bvh=True, seed=1, sample=0, accumulate=False, frames=1):
+    def desc(self, depth=5, use_bvh=True, seed=1, sample=0, accumulate=False, frames=1, jitter=False):
         from .renderer import frame_desc
         return frame_desc(self.width, self.height, depth, use_bvh, seed, sample, accumulate, frames, self.row_block,
-                          self.rank, self.world, self.samples)
+                          self.rank, self.world, self.samples, jitter)
 
     def render_local(self, cam, fd):
         """Enqueue this rank's rows of the next frame; returns its display slab."""

@@ -108,6 +108,9 @@ typedef struct mirt_frame_desc {
                                 accumulation buffer, the frames are folded into it in order (as
                                 `samples` successive calls would: frame j has divisor frames + j)
                                 and slab 0 holds the display after the last one (main.c:379-408) */
+    int32_t jitter;          /* 1: camera rays through (x + jx, y + jy), j in [0, 1)^2 from the pixel's
+                                RNG contract stream (rng.h; BASELINE configs[4] "4 spp jittered" --
+                                the reference samples pixel corners only); 0: main.c:362-363 */
 } mirt_frame_desc;
 
 /* Work counters of the walk as configured; with MIRT_OPT_PRUNE = 0 they are

@@ -50,7 +50,7 @@ class Oracle:
             "o_intersect": (None, [P, P, I, P, I, I, P]),
             "o_sphere_pairs": (None, [P, P, I, P]), "o_aabb_pairs": (None, [P, P, I, P]),
             "o_camera_ray_px": (None, [P, I, I, I, I, P]),
-            "o_render_rows": (None, [P, I, I, P, I, P, I, I, I, C.c_uint64, C.c_uint32, P, I, P, I, P]),
+            "o_render_rows": (None, [P, I, I, P, I, P, I, I, I, C.c_uint64, C.c_uint32, P, I, P, I, P, I]),
             "o_trace_rays": (None, [P, I, P, I, P, I, I, I, C.c_uint64, C.c_uint32, P]),
             "o_accumulate": (None, [P, I, P, I, I, P]),
         }
@@ -115,7 +115,7 @@ class Oracle:
 
     # ---- shading
     def render(self, cam, W, H, spheres, tree, depth=5, use_bvh=True, mode=1, seed=1, sample=0,
-               rows=None, threads=None, counts=False):
+               rows=None, threads=None, counts=False, jitter=False):
         """Fresh frame (main.c:358-374) of the given rows -> (nrows, W, 4) u8."""
         rows = np.arange(H, dtype=np.int32) if rows is None else np.ascontiguousarray(rows, np.int32)
         out = np.zeros((len(rows), W, 4), np.uint8)
@@ -124,7 +124,7 @@ class Oracle:
         if mode == 0:
             self.L.o_srand(seed)
         self.L.o_render_rows(C.byref(cam), W, H, _p(spheres), len(spheres), tree, depth, int(use_bvh),
-                             mode, seed, sample, _p(rows), len(rows), _p(out), threads, _p(cnt))
+                             mode, seed, sample, _p(rows), len(rows), _p(out), threads, _p(cnt), int(jitter))
         return (out, cnt) if counts else out
 
     def trace_rays(self, rays, spheres, tree, depth=5, use_bvh=True, mode=1, seed=1, sample=0):
@@ -162,7 +162,7 @@ class Reference:
             "h_intersect_bvh": (None, [P, P, P, I, P]),
             "h_sphere_pairs": (None, [P, P, I, P]), "h_aabb_pairs": (None, [P, P, I, P]),
             "h_camera_ray": (None, [P, I, I, P]),
-            "h_render": (None, [P, P, I, P, I, I, I, C.c_uint64, C.c_uint32, I, I, I, P, I]),
+            "h_render": (None, [P, P, I, P, I, I, I, C.c_uint64, C.c_uint32, I, I, I, P, I, I]),
             "h_trace_rays": (None, [P, I, P, I, P, I, I, I, C.c_uint64, C.c_uint32, P]),
             "h_camera_update": (None, [P]),
             "h_bench_point": (None, [I, I, C.c_float, P, P, P, P, P, P]),
@@ -243,7 +243,7 @@ class Reference:
         return out
 
     def render(self, cam, spheres, tree, depth=5, use_bvh=True, mode=1, seed=1, sample=0,
-               row0=0, step=1, nrows=None, threads=1):
+               row0=0, step=1, nrows=None, threads=1, jitter=False):
         """mode 0: call srand(seed) then render with the glibc stream (the
         unmodified reference); mode 1: the per-pixel contract."""
         nrows = (self.H - row0 + step - 1) // step if nrows is None else nrows
@@ -251,7 +251,7 @@ class Reference:
         if mode == 0:
             self.L.h_srand(seed)
         self.L.h_render(C.byref(cam), _p(spheres), len(spheres), tree, depth, int(use_bvh), mode, seed, sample,
-                        row0, step, nrows, _p(out), threads)
+                        row0, step, nrows, _p(out), threads, int(jitter))
         return out
 
     def trace_rays(self, rays, spheres, tree, depth=5, use_bvh=True, mode=1, seed=1, sample=0):

@@ -475,12 +475,25 @@ void o_camera_ray_px(const mirt_camera *cam, int W, int H, int x, int y, mirt_ra
     *out = o_camera_ray(cam, W, H, u, -v);                 /* main.c:365 */
 }
 
+/* main.c:362-365 with the build's jitter (rng_contract.h OC_JITTER_*): the
+   sample point (x + jx, y + jy) of the pixel's contract stream */
+static void o_camera_ray_jittered(const mirt_camera *cam, int W, int H, int x, int y, uint64_t key, mirt_ray *out)
+{
+    float aspect = (float)W / (float)H;
+    float xf = (float)x + (float)oc_draw(key, OC_JITTER_X) / 2147483648.0f;
+    float yf = (float)y + (float)oc_draw(key, OC_JITTER_Y) / 2147483648.0f;
+    float u = (xf / (float)W - 0.5f) * aspect;
+    float v = yf / (float)H - 0.5f;
+    *out = o_camera_ray(cam, W, H, u, -v);
+}
+
 /* main.c:358-374 (fresh frame) over a list of rows. mode 0 must run with one
    thread (serial glibc stream in pixel order); mode 1 is thread-count
-   independent. counts (nullable) receives {rays traced, node tests, sphere tests}. */
+   independent; jitter (mode 1 only) moves each camera ray's sample point.
+   counts (nullable) receives {rays traced, node tests, sphere tests}. */
 void o_render_rows(const mirt_camera *cam, int W, int H, const mirt_sphere *s, int ns, void *root,
                    int depth, int use_bvh, int mode, uint64_t seed, uint32_t sample,
-                   const int *rows, int nrows, mirt_rgba8 *out, int nthreads, long long *counts)
+                   const int *rows, int nrows, mirt_rgba8 *out, int nthreads, long long *counts, int jitter)
 {
     o_mode = mode;
     long long c_rays = 0, c_nodes = 0, c_sph = 0;
@@ -494,8 +507,11 @@ void o_render_rows(const mirt_camera *cam, int W, int H, const mirt_sphere *s, i
         long long nr = 0;
         for (int x = 0; x < W; x++) {
             mirt_ray r;
-            o_camera_ray_px(cam, W, H, x, y, &r);
             if (mode == 1) { o_key = oc_pixel_key(seed, (uint32_t)(y * W + x), sample); o_draws = 0; }
+            if (mode == 1 && jitter)
+                o_camera_ray_jittered(cam, W, H, x, y, o_key, &r);
+            else
+                o_camera_ray_px(cam, W, H, x, y, &r);
             out[(size_t)ri * W + x] = o_trace(r, s, ns, depth, use_bvh ? (const ONode *)root : NULL,
                                               counts ? &cnt : NULL, counts ? &nr : NULL);
         }

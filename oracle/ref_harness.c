@@ -223,7 +223,8 @@ void h_camera_ray(Camera *cam, int x, int y, Ray *out)
    mode 0 = the unmodified glibc stream (call h_srand first), single thread;
    mode 1 = rng contract, any thread count. */
 void h_render(const Camera *cam_in, Sphere *spheres, int n, void *root, int depth, int use_bvh, int mode,
-              uint64_t seed, uint32_t sample, int row0, int step, int nrows, uint8_t *rgba, int nthreads)
+              uint64_t seed, uint32_t sample, int row0, int step, int nrows, uint8_t *rgba, int nthreads,
+              int jitter)
 {
     g_mode = mode;
     if (mode == 0) nthreads = 1;
@@ -236,6 +237,12 @@ void h_render(const Camera *cam_in, Sphere *spheres, int n, void *root, int dept
             float u = ((float)x / WIDTH - 0.5f) * aspect_ratio;
             float v = (float)y / HEIGHT - 0.5f;
             if (mode == 1) { g_key = oc_pixel_key(seed, (uint32_t)(y * WIDTH + x), sample); g_k = 0; }
+            if (mode == 1 && jitter) {  /* the build's jitter (rng_contract.h), not main.c */
+                float xf = (float)x + (float)oc_draw(g_key, OC_JITTER_X) / 2147483648.0f;
+                float yf = (float)y + (float)oc_draw(g_key, OC_JITTER_Y) / 2147483648.0f;
+                u = (xf / WIDTH - 0.5f) * aspect_ratio;
+                v = yf / HEIGHT - 0.5f;
+            }
             Ray ray = get_camera_ray(&cam, u, -v);
             SDL_Color c = trace_ray(ray, spheres, n, depth, use_bvh ? (BVHNode *)root : NULL);
             uint8_t *p = rgba + ((size_t)ri * WIDTH + x) * 4;

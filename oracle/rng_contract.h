@@ -42,4 +42,10 @@ static inline int oc_draw(uint64_t key, uint32_t k)
     return (int)(oc_mix64(key + (uint64_t)(k + 1u) * 0x9E3779B97F4A7C15ULL) >> 33);
 }
 
+/* Jittered frames (the build's definition; the reference has no jitter):
+   pixel (x, y) samples at (x + jx, y + jy), j = (float)draw(key, OC_JITTER_*)
+   / 2^31 in [0, 1), draws at indices the bounce sampling never reaches. */
+#define OC_JITTER_X 0x7ffffff0u
+#define OC_JITTER_Y 0x7ffffff1u
+
 #endif
