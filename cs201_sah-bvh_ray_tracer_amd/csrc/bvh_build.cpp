@@ -16,10 +16,22 @@
 //  * the in-place partition (bvh.c:172-201) is the reference's swap loop.
 // No FMA contraction (-ffp-contract=off): bvh.c:54-56,96,150-158 are
 // contraction-sensitive.
+//
+// Threads: after a node's partition its two children own disjoint ranges of
+// the sphere array and their builds are independent, so above kParMin
+// spheres (and up to kParDepth levels deep: at most 2^kParDepth tasks) both
+// children are built concurrently by child builders. The parent keeps a
+// marker node per child and counts the child's nodes in its own indices, so
+// every skip is final relative to the builder's origin; emit() then writes
+// the pre-order array once, each node copied once, skips offset by the
+// builder's position. Every node is computed by the same sequence of
+// operations as in one thread: the tree is the same bits.
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <future>
+#include <memory>
 #include <vector>
 
 #include "internal.h"
@@ -71,10 +83,59 @@ inline float centre(const mirt_sphere& s, int axis)
     return axis == 0 ? s.center.x : (axis == 1 ? s.center.y : s.center.z);
 }
 
+constexpr int kParMin = 32768;  // spheres below which a subtree is built on one thread
+constexpr int kParDepth = 4;    // levels that may fork (<= 16 concurrent builds)
+
+// MIRT_BVH_FORK_LEVELS overrides kParDepth (0 = one thread)
+int fork_levels()
+{
+    const char* e = std::getenv("MIRT_BVH_FORK_LEVELS");
+    return e ? std::atoi(e) : kParDepth;
+}
+
 struct FlatBuilder {
     mirt_sphere* s;
-    std::vector<mirt_node> nodes;
-    std::vector<int32_t> counts;  // sphere_count of leaves (bvh.c:134), 0 for inner nodes
+    std::vector<mirt_node> nodes;  // own nodes, plus one marker (sphere = -2 - k) per child builder k
+    std::vector<int32_t> counts;   // sphere_count of leaves (bvh.c:134), 0 for inner nodes
+    int par = 0;                   // fork levels left
+    uint32_t total = 0;            // nodes of the finished subtree (children's included)
+    std::vector<std::unique_ptr<FlatBuilder>> kids;
+
+    // the pre-order array of this subtree at out[base..base + total)
+    void emit(mirt_node* out, int32_t* cnt, uint32_t base) const
+    {
+        uint32_t pos = base;
+        for (size_t i = 0; i < nodes.size(); i++) {
+            const mirt_node& n = nodes[i];
+            if (n.sphere <= -2) {
+                const FlatBuilder& k = *kids[(size_t)(-2 - n.sphere)];
+                k.emit(out, cnt, pos);
+                pos += k.total;
+                continue;
+            }
+            mirt_node o = n;
+            o.skip = ((n.skip & ~MIRT_NODE_EMPTY) + base) | (n.skip & MIRT_NODE_EMPTY);
+            out[pos] = o;
+            if (cnt) cnt[pos] = counts[i];
+            pos++;
+        }
+    }
+
+    std::vector<mirt_node> flat(std::vector<int32_t>* cnt) const
+    {
+        std::vector<mirt_node> out(total);
+        if (cnt) cnt->assign(total, 0);
+        emit(out.data(), cnt ? cnt->data() : nullptr, 0);
+        return out;
+    }
+
+    void run(int lo, int hi, int depth)
+    {
+        build(lo, hi, depth);
+        total = cur;
+    }
+
+    uint32_t cur = 0;  // final-array index (relative to this builder) of the next node
 
     void emit_box(mirt_node& n, const Box& b)
     {
@@ -86,7 +147,8 @@ struct FlatBuilder {
 
     void build(int lo, int hi, int depth)
     {
-        const int me = (int)nodes.size();
+        const int me = (int)nodes.size();  // slot in `nodes`
+        const uint32_t at = cur++;         // index in the final array (relative)
         nodes.push_back(mirt_node{});
         counts.push_back(0);
         Box bounds = box_empty();
@@ -95,7 +157,7 @@ struct FlatBuilder {
         const int n = hi - lo;
         if (n <= 1 || depth >= 40) {  // bvh.c:131-137 (n == 0 leaves too)
             nodes[me].sphere = lo;
-            nodes[me].skip = (uint32_t)(me + 1) | (n == 0 ? MIRT_NODE_EMPTY : 0u);
+            nodes[me].skip = (at + 1) | (n == 0 ? MIRT_NODE_EMPTY : 0u);
             counts[me] = n;
             return;
         }
@@ -157,10 +219,28 @@ struct FlatBuilder {
                 mid++;
             }
         }
-        build(lo, mid, depth + 1);
-        build(mid, hi, depth + 1);
+        if (par > 0 && n >= kParMin) {
+            auto l = std::make_unique<FlatBuilder>(), r = std::make_unique<FlatBuilder>();
+            l->s = r->s = s;
+            l->par = r->par = par - 1;
+            FlatBuilder *lp = l.get(), *rp = r.get();
+            auto fl = std::async(std::launch::async, [=] { lp->run(lo, mid, depth + 1); });
+            rp->run(mid, hi, depth + 1);
+            fl.get();
+            for (auto* k : {&l, &r}) {
+                mirt_node mk{};
+                mk.sphere = -2 - (int32_t)kids.size();
+                cur += (*k)->total;
+                kids.push_back(std::move(*k));
+                nodes.push_back(mk);
+                counts.push_back(0);
+            }
+        } else {
+            build(lo, mid, depth + 1);
+            build(mid, hi, depth + 1);
+        }
         nodes[me].sphere = -1;
-        nodes[me].skip = (uint32_t)nodes.size();
+        nodes[me].skip = cur;
     }
 };
 
@@ -219,17 +299,18 @@ int mirt_bvh_build_flat(mirt_sphere* spheres, int start, int end, int depth, mir
         mirt::set_error("mirt_bvh_build_flat: invalid arguments");
         return MIRT_E_INVALID;
     }
-    FlatBuilder b{spheres, {}, {}};
-    b.nodes.reserve((size_t)(end - start) * 3 + 1);
-    b.build(start, end, depth);
-    mirt_node* out = (mirt_node*)std::malloc(b.nodes.size() * sizeof(mirt_node));
+    FlatBuilder b;
+    b.s = spheres;
+    b.par = fork_levels();
+    b.run(start, end, depth);
+    mirt_node* out = (mirt_node*)std::malloc((size_t)b.total * sizeof(mirt_node));
     if (!out) {
         mirt::set_error("mirt_bvh_build_flat: out of host memory");
         return MIRT_E_NOMEM;
     }
-    std::memcpy(out, b.nodes.data(), b.nodes.size() * sizeof(mirt_node));
+    b.emit(out, nullptr, 0);
     *out_nodes = out;
-    *out_count = (int)b.nodes.size();
+    *out_count = (int)b.total;
     return MIRT_OK;
 }
 
@@ -241,10 +322,14 @@ mirt_bvh_node* mirt_build_bvh_node(mirt_sphere* spheres, int start, int end, int
         mirt::set_error("mirt_build_bvh_node: invalid arguments");
         return nullptr;
     }
-    FlatBuilder b{spheres, {}, {}};
-    b.build(start, end, depth);
+    FlatBuilder b;
+    b.s = spheres;
+    b.par = fork_levels();
+    b.run(start, end, depth);
+    std::vector<int32_t> counts;
+    const std::vector<mirt_node> flat = b.flat(&counts);
     int i = 0;
-    return to_pointer_tree(b.nodes, b.counts, spheres, i);
+    return to_pointer_tree(flat, counts, spheres, i);
 }
 
 void mirt_free_bvh(mirt_bvh_node* node)  // benchmark.c:81-88

@@ -159,3 +159,25 @@ def test_no_gpu_create_fails_loudly(mirt):
         pytest.skip("GPU present")
     with pytest.raises(mirt.MirtError):
         mirt.Renderer(0)
+
+
+@pytest.mark.parametrize("levels", ["0", "1", "4", "6"])
+def test_threaded_build_same_tree(mirt, golden, levels, monkeypatch):
+    """The build forks child subtrees onto threads (MIRT_BVH_FORK_LEVELS);
+    any number of fork levels gives the reference's tree, bit for bit."""
+    monkeypatch.setenv("MIRT_BVH_FORK_LEVELS", levels)
+    g = golden["scenes"]["render_100000_1"]
+    s = mirt.create_random_spheres(100000, 1)
+    b = mirt.build_bvh(s)
+    assert sha(b.nodes) == g["tree_sha"]
+    s = mirt.create_random_spheres(70000, 3)
+    ref = s.copy()
+    monkeypatch.setenv("MIRT_BVH_FORK_LEVELS", "0")
+    one = mirt.build_bvh(ref)
+    monkeypatch.setenv("MIRT_BVH_FORK_LEVELS", levels)
+    root = mirt.build_bvh_node(s)
+    try:
+        assert (s == ref).all()
+        assert mirt.flatten_bvh(root, s).nodes.tobytes() == one.nodes.tobytes()
+    finally:
+        mirt.free_bvh(root)
