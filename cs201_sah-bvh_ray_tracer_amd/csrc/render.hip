@@ -367,7 +367,8 @@ __global__ __launch_bounds__(256) void primary_kernel(DevScene sc, FrameConst f,
 }
 
 // The walk of one bounce ray: WALK 0 = reference DFS order, 1 = ordered
-// binary (PNode, register stack), 2 = ordered four-wide (QNode, LDS stack).
+// binary (PNode, register stack), 2 = ordered four-wide (HNode, LDS stack),
+// 3 = four-wide with one ray per quad, 4 = WALK 2 over the 48-B QNodes.
 template <int WALK>
 struct BounceWalk;
 template <>
@@ -407,6 +408,19 @@ struct BounceWalk<2> {
                          float& bt, int& bs, Counters& cnt)
     {
         wide_lane_step<FAST, false>(sc, sr, sp, pr, w, stk, bt, bs, cnt);
+    }
+};
+template <>
+struct BounceWalk<4> {  // BounceWalk<2> over the 48-B QNodes (MIRT_OPT_QUANT)
+    WideWalk w;
+    __device__ void start(const DevScene&) { w = wide_walk_start(true); }
+    __device__ void stop() { w = wide_walk_start(false); }
+    __device__ bool walking() const { return wide_walking(w); }
+    template <bool FAST>
+    __device__ void step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr, uint32_t* stk,
+                         float& bt, int& bs, Counters& cnt)
+    {
+        wide_lane_step<FAST, false, true>(sc, sr, sp, pr, w, stk, bt, bs, cnt);
     }
 };
 
@@ -479,10 +493,11 @@ __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, 
     // WALK 3: one ray per quad of lanes -- its colour stack and walk stack are
     // per ray (quad); the ray's state is replicated in the quad's lanes
     constexpr bool QUAD = WALK == 3;
+    constexpr bool LANE4 = WALK == 2 || WALK == 4;  // four-wide, one ray per lane (HNode / QNode)
     constexpr int cstride = QUAD ? kQuadStride : 256;
     __shared__ uint32_t cstack[kMaxDepth * cstride];
-    __shared__ uint32_t wstack[WALK == 2 ? kWideStack * kWideStride : QUAD ? kQuadStack * kQuadStride : 1];
-    __shared__ uint32_t qsrc[WALK == 2 ? 4 * 16 : 1];  // quad drain: source lane of each quad, per wave
+    __shared__ uint32_t wstack[LANE4 ? kWideStack * kWideStride : QUAD ? kQuadStack * kQuadStride : 1];
+    __shared__ uint32_t qsrc[LANE4 ? 4 * 16 : 1];  // quad drain: source lane of each quad, per wave
     const uint32_t slot = QUAD ? threadIdx.x >> 2 : threadIdx.x;
     uint32_t* cs = cstack + slot;
     uint32_t* stk = wstack + (WALK >= 2 ? slot : 0);
@@ -533,7 +548,7 @@ __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, 
         }
         if (!__ballot(has)) break;
         if (DIAG && exhausted && !dg_tx) dg_tx = __builtin_amdgcn_s_memrealtime();
-        if (WALK == 2 && quad_drain && exhausted && __popcll(__ballot(has)) <= 16) break;  // -> quad drain
+        if (LANE4 && quad_drain && exhausted && __popcll(__ballot(has)) <= 16) break;  // -> quad drain
         // walk until few lanes are still walking and the others can make progress
         for (;;) {
             const uint64_t walking = __ballot(has && w.walking());
@@ -576,8 +591,8 @@ __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, 
             }
         }
     }
-    if constexpr (WALK == 2) {
-        // quad drain (uniform control flow here: every lane is active)
+    if constexpr (LANE4) {
+        // quad drain (over the HNodes: QNode and HNode indices agree) (uniform control flow here: every lane is active)
         const uint64_t busy = __ballot(has);
         if (busy) {
             const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -874,6 +889,9 @@ struct mirt_ctx {
     int bounce_blocks_opt = 0;  // MIRT_OPT_BOUNCE_BLOCKS override (0: occupancy x CUs)
     int quad = 0;               // four-wide bounce walk with one ray per quad of lanes
     int quad_drain = 1;         // four-wide bounce walk: finish the drain four lanes per ray
+    QNode* d_qnodes = nullptr;  // the four-wide layout in 48 B (null: the tree does not admit it)
+    int quant = 0;              // bounce walk over d_qnodes
+    int bounce_blocks_q = 0;    // persistent workgroups of the QNode bounce kernel
     void* d_queue = nullptr;    // wavefront: {count, head} + bounce records
     size_t queue_cap = 0;
     uint32_t* d_defer = nullptr;  // [count, list...]
@@ -1039,13 +1057,16 @@ uint16_t half_up(float v)
 // grandchildren (a leaf child standing in for its own); one LeafRec per
 // leaf slot. Used only when the PNode conditions hold and the boxes nest.
 void build_hnodes(const mirt_node* nd, int nn, const mirt_sphere* sp, int ns, std::vector<HNode>& hn,
-                  std::vector<HAux>& aux, std::vector<LeafRec>& leaves)
+                  std::vector<HAux>& aux, std::vector<LeafRec>& leaves, std::vector<uint32_t>& src)
 {
     hn.assign(1, HNode{});
+    src.assign(4, kPNone);  // src[4 h + k]: the flat node slot k of HNode h stands for
     aux.assign(1, HAux{0xffffffffu, (uint32_t)nn});  // flat + 1 == 0: the whole tree
     leaves.clear();
     std::vector<uint32_t> todo;  // inner nodes waiting for their HNode: HNode 1 + i is todo[i]
-    auto fill = [&](HNode& h, int k, uint32_t ci) {
+    auto fill = [&](size_t hi, int k, uint32_t ci) {
+        HNode& h = hn[hi];
+        src[4 * hi + k] = ci;
         const mirt_node& n = nd[ci];
         for (int a = 0; a < 3; a++)
             h.slot[k].box[a] = (uint32_t)half_down(n.bmin[a]) | ((uint32_t)half_up(n.bmax[a]) << 16);
@@ -1073,24 +1094,103 @@ void build_hnodes(const mirt_node* nd, int nn, const mirt_sphere* sp, int ns, st
     };
     for (int k = 0; k < 4; k++) hn[0].slot[k].ref = kPNone;
     if (nn == 0) return;
-    fill(hn[0], 0, 0);
+    fill(0, 0, 0);
     for (size_t next = 0; next < todo.size(); next++) {
         const uint32_t y = todo[next];
         HNode h{};
         for (int k = 0; k < 4; k++) h.slot[k].ref = kPNone;
         hn.push_back(h);
+        src.resize(4 * hn.size(), kPNone);
         aux.push_back(HAux{y, nd[y].skip & MIRT_SKIP_MASK});
         const uint32_t kids[2] = {y + 1, nd[y + 1].skip & MIRT_SKIP_MASK};
         int k = 0;
         for (uint32_t c : kids) {
             if (nd[c].sphere < 0 && !(nd[c].skip & MIRT_NODE_EMPTY)) {
-                fill(hn.back(), k++, c + 1);
-                fill(hn.back(), k++, nd[c + 1].skip & MIRT_SKIP_MASK);
+                fill(hn.size() - 1, k++, c + 1);
+                fill(hn.size() - 1, k++, nd[c + 1].skip & MIRT_SKIP_MASK);
             } else {
-                fill(hn.back(), k++, c);
+                fill(hn.size() - 1, k++, c);
             }
         }
     }
+}
+
+// QNode i of HNode i (trace.h): per axis, the origin is the least lo of the
+// node's live slots and the step the least power of two with which 255 steps
+// reach the greatest hi; each slot's lo / hi rounds down / up to a multiple
+// of the step, checked with the fp32 arithmetic the kernel decodes with
+// (q_dec). Returns false -- the walk keeps the 64-B nodes -- if a node's
+// inner or leaf references are not consecutive, a bound is not finite, or a
+// decoded bound would be subnormal.
+float q_dec_host(float org, uint32_t q, uint32_t e)
+{
+    const uint32_t bits = e << 23;
+    float step;
+    std::memcpy(&step, &bits, 4);
+    return org + (float)q * step;
+}
+
+bool build_qnodes(const mirt_node* nd, const std::vector<HNode>& hn, const std::vector<uint32_t>& src,
+                  std::vector<QNode>& qn)
+{
+    qn.assign(hn.size(), QNode{});
+    for (size_t i = 0; i < hn.size(); i++) {
+        QNode& q = qn[i];
+        uint32_t im = 0, lk = 0, ni = 0, nl = 0;
+        for (int k = 0; k < 4; k++) {
+            const uint32_t r = hn[i].slot[k].ref;
+            if (r == kPNone) continue;
+            if (r & kPLeaf) {
+                if (nl == 0) q.leaf = r & ~kPLeaf;
+                if ((r & ~kPLeaf) != q.leaf + nl) return false;
+                nl++;
+                lk |= 1u << k;
+            } else {
+                if (ni == 0) q.inner = r;
+                if (r != q.inner + ni) return false;
+                ni++;
+                im |= 1u << k;
+            }
+        }
+        const uint32_t live = im | lk;
+        uint32_t ex[3] = {127, 127, 127};
+        for (int a = 0; a < 3 && live; a++) {
+            float lo = INFINITY, hi = -INFINITY;
+            for (int k = 0; k < 4; k++)
+                if ((live >> k) & 1u) {
+                    lo = std::min(lo, nd[src[4 * i + k]].bmin[a]);
+                    hi = std::max(hi, nd[src[4 * i + k]].bmax[a]);
+                }
+            if (!std::isfinite(lo) || !std::isfinite(hi) || !(lo <= hi)) return false;
+            q.org[a] = lo;
+            const double need = ((double)hi - (double)lo) / 255.0;
+            int e = need > 0.0 ? std::max(1, std::ilogb(need) + 127) : 1;
+            while (e <= 254 && q_dec_host(lo, 255, (uint32_t)e) < hi) e++;
+            if (e > 254) return false;
+            while (e > 1 && q_dec_host(lo, 255, (uint32_t)(e - 1)) >= hi) e--;
+            ex[a] = (uint32_t)e;
+        }
+        for (int k = 0; k < 4; k++) {
+            if (!((live >> k) & 1u)) continue;
+            const mirt_node& n = nd[src[4 * i + k]];
+            for (int a = 0; a < 3; a++) {
+                const float o = q.org[a];
+                const double step = std::ldexp(1.0, (int)ex[a] - 127);
+                int ql = (int)std::clamp(std::floor(((double)n.bmin[a] - o) / step), 0.0, 255.0);
+                while (ql > 0 && q_dec_host(o, (uint32_t)ql, ex[a]) > n.bmin[a]) ql--;
+                int qh = (int)std::clamp(std::ceil(((double)n.bmax[a] - o) / step), 0.0, 255.0);
+                while (qh < 255 && q_dec_host(o, (uint32_t)qh, ex[a]) < n.bmax[a]) qh++;
+                const float dl = q_dec_host(o, (uint32_t)ql, ex[a]), dh = q_dec_host(o, (uint32_t)qh, ex[a]);
+                if (!(dl <= n.bmin[a]) || !(dh >= n.bmax[a])) return false;
+                if ((dl != 0.0f && std::fabs(dl) < 0x1p-126f) || (dh != 0.0f && std::fabs(dh) < 0x1p-126f))
+                    return false;
+                q.q[a] |= (uint32_t)ql << (8 * k);
+                q.q[3 + a] |= (uint32_t)qh << (8 * k);
+            }
+        }
+        q.meta = ex[0] | ex[1] << 8 | ex[2] << 16 | im << 24 | lk << 28;
+    }
+    return true;
 }
 
 DevScene dev_scene(const mirt_ctx* c)
@@ -1099,7 +1199,8 @@ DevScene dev_scene(const mirt_ctx* c)
     return DevScene{c->d_nodes, c->d_nodes32, c->d_geo, c->d_color, (uint32_t)c->num_nodes, c->num_spheres,
                     prune, c->r_max, c->c_max, c->d_pnodes, prune && c->ordered && c->ordered_ok && c->fast_slab,
                     c->d_hnodes, c->d_haux, c->d_leaves,
-                    prune && c->ordered && c->ordered_ok && c->fast_slab && c->wide};
+                    prune && c->ordered && c->ordered_ok && c->fast_slab && c->wide,
+                    c->quant ? c->d_qnodes : nullptr};
 }
 
 bool ctx_ok(mirt_ctx* c, bool need_scene, const char* fn)
@@ -1205,6 +1306,9 @@ int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_ac
             bounce_kernel<true, 0, true><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, d_bdiag);
         else if (c->fast_slab && sc.wide && c->quad)
             bounce_kernel<true, 3><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain);
+        else if (c->fast_slab && sc.wide && sc.qnodes)
+            bounce_kernel<true, 4><<<c->bounce_blocks_opt ? c->bounce_blocks_opt : c->bounce_blocks_q, 256, 0, s>>>(
+                sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain);
         else if (c->fast_slab && sc.wide)
             bounce_kernel<true, 2><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain);
         else if (c->fast_slab && sc.ordered)
@@ -1291,6 +1395,10 @@ int mirt_create(int device, mirt_ctx** out)
         if (e == hipSuccess)
             e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bounce_kernel<true, 2>, 256, 0);
         c->bounce_blocks = std::max(1, cus) * std::max(1, per_cu);
+        int per_cu_q = 0;
+        if (e == hipSuccess)
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_q, bounce_kernel<true, 4>, 256, 0);
+        c->bounce_blocks_q = std::max(1, cus) * std::max(1, per_cu_q);
         c->num_cus = cus;
     }
     if (e != hipSuccess) {
@@ -1308,7 +1416,7 @@ void mirt_destroy(mirt_ctx* c)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : {(void*)c->d_nodes, (void*)c->d_nodes32, (void*)c->d_geo, (void*)c->d_color, (void*)c->d_out, (void*)c->d_acc,
                     c->d_in, c->d_res, (void*)c->d_counts, (void*)c->d_defer, c->d_queue, (void*)c->d_keys, (void*)c->d_pnodes,
-                    (void*)c->d_hnodes, (void*)c->d_haux, (void*)c->d_leaves})
+                    (void*)c->d_hnodes, (void*)c->d_haux, (void*)c->d_leaves, (void*)c->d_qnodes})
         if (p) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -1350,8 +1458,9 @@ int mirt_scene_upload_flat(mirt_ctx* c, const mirt_sphere* spheres, int ns, cons
     geo[ns] = make_float4(NAN, NAN, NAN, NAN);  // &spheres[N] sentinel: never hits
     col[ns] = 0xff000000u;
     for (void* p : {(void*)c->d_nodes, (void*)c->d_nodes32, (void*)c->d_geo, (void*)c->d_color, (void*)c->d_pnodes,
-                    (void*)c->d_hnodes, (void*)c->d_haux, (void*)c->d_leaves})
+                    (void*)c->d_hnodes, (void*)c->d_haux, (void*)c->d_leaves, (void*)c->d_qnodes})
         if (p) (void)hipFree(p);
+    c->d_qnodes = nullptr;
     c->d_pnodes = nullptr;
     c->d_hnodes = nullptr;
     c->d_haux = nullptr;
@@ -1387,7 +1496,13 @@ int mirt_scene_upload_flat(mirt_ctx* c, const mirt_sphere* spheres, int ns, cons
     std::vector<HNode> hn;
     std::vector<HAux> hx;
     std::vector<LeafRec> lr;
-    build_hnodes(nodes, nn, spheres, ns, hn, hx, lr);
+    std::vector<uint32_t> src;
+    build_hnodes(nodes, nn, spheres, ns, hn, hx, lr, src);
+    std::vector<QNode> qn;
+    if (build_qnodes(nodes, hn, src, qn)) {
+        HIP_TRY(hipMalloc((void**)&c->d_qnodes, sizeof(QNode) * qn.size()));
+        HIP_TRY(hipMemcpy(c->d_qnodes, qn.data(), sizeof(QNode) * qn.size(), hipMemcpyHostToDevice));
+    }
     HIP_TRY(hipMalloc((void**)&c->d_hnodes, sizeof(HNode) * hn.size()));
     HIP_TRY(hipMalloc((void**)&c->d_haux, sizeof(HAux) * hx.size()));
     HIP_TRY(hipMalloc((void**)&c->d_leaves, sizeof(LeafRec) * std::max<size_t>(lr.size(), 1)));
@@ -1778,6 +1893,9 @@ int mirt_set_option(mirt_ctx* c, int option, int value)
     case MIRT_OPT_QUAD_DRAIN:
         c->quad_drain = value != 0;
         return MIRT_OK;
+    case MIRT_OPT_QUANT:
+        c->quant = value != 0;
+        return MIRT_OK;
     case MIRT_OPT_BLOCK_WAVES:
         if (value != 1 && value != 2 && value != 4 && value != 8) break;
         c->block_waves = value;
@@ -1803,6 +1921,7 @@ int mirt_get_option(mirt_ctx* c, int option)
     if (option == MIRT_OPT_BOUNCE_BLOCKS) return c->bounce_blocks_opt;
     if (option == MIRT_OPT_QUAD) return c->quad;
     if (option == MIRT_OPT_QUAD_DRAIN) return c->quad_drain;
+    if (option == MIRT_OPT_QUANT) return c->quant;
     set_error("mirt_get_option: bad option %d", option);
     return MIRT_E_INVALID;
 }

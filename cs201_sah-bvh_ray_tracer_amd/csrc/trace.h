@@ -86,6 +86,22 @@ static_assert(sizeof(HNode) == 64, "wide node is 64 B");
 struct HAux {
     uint32_t flat, end;
 };
+// The same four-wide node in 48 B (QNode i <-> HNode i, same slots): each
+// slot box as 8-bit offsets from a per-node origin in steps of a per-axis
+// power of two, lo rounded down and hi up (decoded as org + q * step in
+// fp32, exactly the arithmetic the host checked the fp32 box against).
+// References are implicit: the build gives a node's inner slots consecutive
+// HNode indices and its leaf slots consecutive LeafRec indices, so a slot's
+// reference is a base plus the count of same-kind slots before it.
+struct __attribute__((aligned(16))) QNode {
+    float org[3];
+    uint32_t meta;   // biased fp32 exponent of the x / y / z step (bits 0-23),
+                     // inner-slot mask (24-27), leaf-slot mask (28-31)
+    uint32_t inner;  // HNode index of the first inner slot
+    uint32_t leaf;   // LeafRec index of the first leaf slot
+    uint32_t q[6];   // lo x, lo y, lo z, hi x, hi y, hi z: byte k = slot k
+};
+static_assert(sizeof(QNode) == 48, "quantised wide node is 48 B");
 struct __attribute__((aligned(16))) LeafRec {
     float lo[3], hi[3];  // the leaf's exact box (bvh.c bounds)
     int32_t sphere;
@@ -117,6 +133,9 @@ struct DevScene {
     const HAux* haux;
     const LeafRec* leaves;
     int wide;
+    // the four-wide nodes in 48 B (QNode): set when MIRT_OPT_QUANT is on and
+    // the tree admits them
+    const QNode* qnodes;
 };
 
 struct Ray {
@@ -1049,7 +1068,15 @@ __device__ __forceinline__ void wide_leaf(const DevScene& sc, const SlabRay& sr,
     }
 }
 
-template <bool FAST, bool COUNT>
+// A QNode slot bound: org + q * step in fp32 (q * step is exact), the
+// arithmetic build_qnodes checked against the node's fp32 box.
+__device__ __forceinline__ float q_dec(float org, uint32_t q, int k, float step)
+{
+    return org + (float)((q >> (8 * k)) & 0xffu) * step;
+}
+
+// Q: read the 48-B QNodes instead of the 64-B HNodes (same walk, same stack).
+template <bool FAST, bool COUNT, bool Q = false>
 __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
                                                WideWalk& w, uint32_t* stk, float& best_t, int& best_s, Counters& cnt)
 {
@@ -1062,21 +1089,51 @@ __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay
         }
         return;
     }
-    const uint4* p = (const uint4*)(sc.hnodes + w.cur);
-    const uint4 s0 = p[0], s1 = p[1], s2 = p[2], s3 = p[3];
     // 1. the four conservative slot tests, computed for every slot (no branch
     // for the compiler to sink a load into); COUNT: a slot test is a node test
     float e0 = 0.0f, e1 = 0.0f, e2 = 0.0f, e3 = 0.0f;
-    auto test = [&](const uint4& q, float& e) {
-        if (COUNT && q.w != kPNone) cnt.nodes++;
-        const bool pass = slab_cons(sr, pr, h_lo(q.x), h_lo(q.y), h_lo(q.z), h_hi(q.x), h_hi(q.y), h_hi(q.z), e);
-        return pass & (q.w != kPNone);
-    };
-    bool h0 = test(s0, e0);
-    bool h1 = test(s1, e1);
-    bool h2 = test(s2, e2);
-    bool h3 = test(s3, e3);
-    const uint4 q3 = make_uint4(s0.w, s1.w, s2.w, s3.w);  // the slots' references
+    bool h0, h1, h2, h3;
+    uint4 q3;  // the slots' references
+    if constexpr (Q) {
+        const uint4* p = (const uint4*)(sc.qnodes + w.cur);
+        const uint4 a = p[0], b = p[1], c = p[2];
+        const float ox = __uint_as_float(a.x), oy = __uint_as_float(a.y), oz = __uint_as_float(a.z);
+        const float sx = __uint_as_float((a.w & 0xffu) << 23);
+        const float sy = __uint_as_float(((a.w >> 8) & 0xffu) << 23);
+        const float sz = __uint_as_float(((a.w >> 16) & 0xffu) << 23);
+        const uint32_t im = (a.w >> 24) & 0xfu, lk = a.w >> 28;
+        auto test = [&](int k, float& e) {
+            const bool live = ((im | lk) >> k) & 1u;
+            if (COUNT && live) cnt.nodes++;
+            const bool pass = slab_cons(sr, pr, q_dec(ox, b.z, k, sx), q_dec(oy, b.w, k, sy), q_dec(oz, c.x, k, sz),
+                                        q_dec(ox, c.y, k, sx), q_dec(oy, c.z, k, sy), q_dec(oz, c.w, k, sz), e);
+            return pass & live;
+        };
+        h0 = test(0, e0);
+        h1 = test(1, e1);
+        h2 = test(2, e2);
+        h3 = test(3, e3);
+        auto ref = [&](int k) {
+            const uint32_t below = (1u << k) - 1u;
+            return (im >> k) & 1u   ? b.x + (uint32_t)__builtin_popcount(im & below)
+                   : (lk >> k) & 1u ? kPLeaf | (b.y + (uint32_t)__builtin_popcount(lk & below))
+                                    : kPNone;
+        };
+        q3 = make_uint4(ref(0), ref(1), ref(2), ref(3));
+    } else {
+        const uint4* p = (const uint4*)(sc.hnodes + w.cur);
+        const uint4 s0 = p[0], s1 = p[1], s2 = p[2], s3 = p[3];
+        auto test = [&](const uint4& q, float& e) {
+            if (COUNT && q.w != kPNone) cnt.nodes++;
+            const bool pass = slab_cons(sr, pr, h_lo(q.x), h_lo(q.y), h_lo(q.z), h_hi(q.x), h_hi(q.y), h_hi(q.z), e);
+            return pass & (q.w != kPNone);
+        };
+        h0 = test(s0, e0);
+        h1 = test(s1, e1);
+        h2 = test(s2, e2);
+        h3 = test(s3, e3);
+        q3 = make_uint4(s0.w, s1.w, s2.w, s3.w);
+    }
     // 2. passing leaf slots (the node's boxes are dead here): each lane works
     // through its own list, so the gate code runs max-over-lanes times
     // instead of once per slot that any lane passes
@@ -1268,8 +1325,14 @@ __device__ __forceinline__ void closest_hit(const DevScene& sc, const Ray& ray, 
         best_t = INFINITY;
         best_s = -1;
         WideWalk w = wide_walk_start(active && !gen);
-        while (__ballot(wide_walking(w)))
-            if (wide_walking(w)) wide_lane_step<FAST, COUNT>(sc, sr, sp, pr, w, wstk, best_t, best_s, cnt);
+        while (__ballot(wide_walking(w))) {
+            if (!wide_walking(w)) continue;
+            // counts follow the bounce kernel's node format (MIRT_OPT_QUANT)
+            if (COUNT && sc.qnodes)
+                wide_lane_step<FAST, COUNT, true>(sc, sr, sp, pr, w, wstk, best_t, best_s, cnt);
+            else
+                wide_lane_step<FAST, COUNT>(sc, sr, sp, pr, w, wstk, best_t, best_s, cnt);
+        }
     } else if (!UNIFORM && FAST && sc.ordered) {
         const SlabRay sr = slab_ray(ray);
         const SphRay sp = sph_ray(ray);

@@ -307,8 +307,11 @@ enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3,
        MIRT_OPT_BOUNCE_BLOCKS = 9,  /* wavefront: persistent bounce workgroups, 0 = occupancy x CUs */
        MIRT_OPT_QUAD = 10,          /* four-wide bounce walk: 1 = one ray per quad of lanes throughout,
                                        the four slot tests side by side; 0 (default) = one ray per lane */
-       MIRT_OPT_QUAD_DRAIN = 11     /* four-wide, one ray per lane: 1 (default) = once the queue is dry
-                                       and <= 16 lanes of a wave are busy, finish them as quads */ };
+       MIRT_OPT_QUAD_DRAIN = 11,    /* four-wide, one ray per lane: 1 (default) = once the queue is dry
+                                       and <= 16 lanes of a wave are busy, finish them as quads */
+       MIRT_OPT_QUANT = 12          /* four-wide, one ray per lane: 1 = the bounce walk reads 48-B nodes
+                                       whose slot boxes are 8-bit offsets from a per-node origin
+                                       (rounded outward); 0 = the 64-B fp16 nodes */ };
 enum { MIRT_TRAV_UNIFORM = 0, MIRT_TRAV_LANE = 1, MIRT_TRAV_HYBRID = 2, MIRT_TRAV_LANE_NP = 3,
        MIRT_TRAV_HYBRID_NP = 4,  /* *_NP: per-lane walk without successor prefetch */
        MIRT_TRAV_WAVEFRONT = 5   /* default: camera-ray packets, then persistent per-lane
