@@ -892,6 +892,8 @@ struct mirt_ctx {
     QNode* d_qnodes = nullptr;  // the four-wide layout in 48 B (null: the tree does not admit it)
     int quant = 0;              // bounce walk over d_qnodes
     int bounce_blocks_q = 0;    // persistent workgroups of the QNode bounce kernel
+    size_t hnode_count = 0;     // HNodes per order: d_hnodes / d_haux hold two orders
+    int hdfs = 0;               // walks use the depth-first HNode order
     void* d_queue = nullptr;    // wavefront: {count, head} + bounce records
     size_t queue_cap = 0;
     uint32_t* d_defer = nullptr;  // [count, list...]
@@ -1193,14 +1195,51 @@ bool build_qnodes(const mirt_node* nd, const std::vector<HNode>& hn, const std::
     return true;
 }
 
+// The HNodes renumbered depth-first (slot order) for MIRT_OPT_HNODE_DFS: a
+// node's first inner child follows it in memory, in the other half of its
+// 128-B cache line. Returns false (order kept) if some node is unreachable.
+bool hnodes_dfs_order(std::vector<HNode>& hn, std::vector<HAux>& hx)
+{
+    const size_t n = hn.size();
+    std::vector<uint32_t> nw(n, kPNone);
+    std::vector<uint32_t> stk{0};
+    uint32_t next = 0;
+    while (!stk.empty()) {
+        const uint32_t h = stk.back();
+        stk.pop_back();
+        if (h >= n || nw[h] != kPNone) return false;
+        nw[h] = next++;
+        for (int k = 3; k >= 0; k--) {
+            const uint32_t r = hn[h].slot[k].ref;
+            if (r != kPNone && !(r & kPLeaf)) stk.push_back(r);
+        }
+    }
+    if (next != n) return false;
+    std::vector<HNode> h2(n);
+    std::vector<HAux> x2(n);
+    for (size_t i = 0; i < n; i++) {
+        HNode t = hn[i];
+        for (auto& s : t.slot)
+            if (s.ref != kPNone && !(s.ref & kPLeaf)) s.ref = nw[s.ref];
+        h2[nw[i]] = t;
+        x2[nw[i]] = hx[i];
+    }
+    hn.swap(h2);
+    hx.swap(x2);
+    return true;
+}
+
 DevScene dev_scene(const mirt_ctx* c)
 {
+    // MIRT_OPT_HNODE_DFS: the depth-first copy in the second half of the
+    // HNode / HAux buffers (QNodes follow the first order only)
+    const size_t ho = c->hdfs ? c->hnode_count : 0;
     const bool prune = c->prune && c->prune_ok;
     return DevScene{c->d_nodes, c->d_nodes32, c->d_geo, c->d_color, (uint32_t)c->num_nodes, c->num_spheres,
                     prune, c->r_max, c->c_max, c->d_pnodes, prune && c->ordered && c->ordered_ok && c->fast_slab,
-                    c->d_hnodes, c->d_haux, c->d_leaves,
+                    c->d_hnodes + ho, c->d_haux + ho, c->d_leaves,
                     prune && c->ordered && c->ordered_ok && c->fast_slab && c->wide,
-                    c->quant ? c->d_qnodes : nullptr};
+                    c->quant && !ho ? c->d_qnodes : nullptr};
 }
 
 bool ctx_ok(mirt_ctx* c, bool need_scene, const char* fn)
@@ -1502,6 +1541,17 @@ int mirt_scene_upload_flat(mirt_ctx* c, const mirt_sphere* spheres, int ns, cons
     if (build_qnodes(nodes, hn, src, qn)) {
         HIP_TRY(hipMalloc((void**)&c->d_qnodes, sizeof(QNode) * qn.size()));
         HIP_TRY(hipMemcpy(c->d_qnodes, qn.data(), sizeof(QNode) * qn.size(), hipMemcpyHostToDevice));
+    }
+    {  // second half: the depth-first copy (MIRT_OPT_HNODE_DFS); the first order if that fails
+        std::vector<HNode> h2 = hn;
+        std::vector<HAux> x2 = hx;
+        if (!hnodes_dfs_order(h2, x2)) {
+            h2 = hn;
+            x2 = hx;
+        }
+        c->hnode_count = hn.size();
+        hn.insert(hn.end(), h2.begin(), h2.end());
+        hx.insert(hx.end(), x2.begin(), x2.end());
     }
     HIP_TRY(hipMalloc((void**)&c->d_hnodes, sizeof(HNode) * hn.size()));
     HIP_TRY(hipMalloc((void**)&c->d_haux, sizeof(HAux) * hx.size()));
@@ -1896,6 +1946,9 @@ int mirt_set_option(mirt_ctx* c, int option, int value)
     case MIRT_OPT_QUANT:
         c->quant = value != 0;
         return MIRT_OK;
+    case MIRT_OPT_HNODE_DFS:
+        c->hdfs = value != 0;
+        return MIRT_OK;
     case MIRT_OPT_BLOCK_WAVES:
         if (value != 1 && value != 2 && value != 4 && value != 8) break;
         c->block_waves = value;
@@ -1922,6 +1975,7 @@ int mirt_get_option(mirt_ctx* c, int option)
     if (option == MIRT_OPT_QUAD) return c->quad;
     if (option == MIRT_OPT_QUAD_DRAIN) return c->quad_drain;
     if (option == MIRT_OPT_QUANT) return c->quant;
+    if (option == MIRT_OPT_HNODE_DFS) return c->hdfs;
     set_error("mirt_get_option: bad option %d", option);
     return MIRT_E_INVALID;
 }

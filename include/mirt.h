@@ -309,9 +309,11 @@ enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3,
                                        the four slot tests side by side; 0 (default) = one ray per lane */
        MIRT_OPT_QUAD_DRAIN = 11,    /* four-wide, one ray per lane: 1 (default) = once the queue is dry
                                        and <= 16 lanes of a wave are busy, finish them as quads */
-       MIRT_OPT_QUANT = 12          /* four-wide, one ray per lane: 1 = the bounce walk reads 48-B nodes
+       MIRT_OPT_QUANT = 12,         /* four-wide, one ray per lane: 1 = the bounce walk reads 48-B nodes
                                        whose slot boxes are 8-bit offsets from a per-node origin
-                                       (rounded outward); 0 = the 64-B fp16 nodes */ };
+                                       (rounded outward); 0 = the 64-B fp16 nodes */
+       MIRT_OPT_HNODE_DFS = 13      /* four-wide walks: 1 = the 64-B nodes numbered depth-first (a node's
+                                       first inner child next to it in memory); 0 = breadth-first */ };
 enum { MIRT_TRAV_UNIFORM = 0, MIRT_TRAV_LANE = 1, MIRT_TRAV_HYBRID = 2, MIRT_TRAV_LANE_NP = 3,
        MIRT_TRAV_HYBRID_NP = 4,  /* *_NP: per-lane walk without successor prefetch */
        MIRT_TRAV_WAVEFRONT = 5   /* default: camera-ray packets, then persistent per-lane

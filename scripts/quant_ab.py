@@ -1,10 +1,11 @@
-"""A/B of the bounce walk's node format: 64-B fp16 HNodes vs 48-B 8-bit
-QNodes (MIRT_OPT_QUANT), one context, serial launches on one stream.
+"""A/B of a bounce-walk node option (default MIRT_OPT_QUANT: 64-B fp16
+HNodes vs 48-B 8-bit QNodes; --opt HNODE_DFS: breadth- vs depth-first HNode
+numbering), one context, serial launches on one stream.
 
 Prints per setting: primary / bounce pass ms (HIP events the library records
 around them), the bounce-level node/sphere tests (mirt_count_frame) and the
 frame's SHA-256, which must agree between the settings.
-usage: python scripts/quant_ab.py [--workload 1080p_10k] [--reps 20]
+usage: python scripts/quant_ab.py [--workload 1080p_10k] [--reps 20] [--opt QUANT]
 """
 import argparse
 import hashlib
@@ -32,6 +33,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="1080p_10k")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--opt", default="QUANT", choices=["QUANT", "HNODE_DFS"])
     a = ap.parse_args()
     W, H, kind, n = WORKLOADS[a.workload]
     s = mirt.create_random_spheres(n, 1) if kind == "render" else mirt.create_benchmark_spheres(n, 1)
@@ -41,7 +43,7 @@ def main():
     with mirt.Renderer(0) as r:
         r.upload(s, b)
         for q in (0, 1, 0, 1):
-            r.set_option(mirt.abi.OPT_QUANT, q)
+            r.set_option(getattr(mirt.abi, "OPT_" + a.opt), q)
             img = r.render_frame(cam, W, H, depth=5, seed=1)
             ph = []
             for _ in range(a.reps):
@@ -57,7 +59,7 @@ def main():
                 "spheres_bounce": int(c["spheres"] - c["spheres_primary"]),
                 "sha": hashlib.sha256(np.ascontiguousarray(img).tobytes()).hexdigest()[:16],
             }
-            print(a.workload, f"quant={q}", json.dumps(out[f"quant{q}"]), flush=True)
+            print(a.workload, f"{a.opt}={q}", json.dumps(out[f"quant{q}"]), flush=True)
     assert out["quant0"]["sha"] == out["quant1"]["sha"], "node formats disagree"
 
 
