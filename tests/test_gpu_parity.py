@@ -488,9 +488,10 @@ def test_ordered_walk_stays_within_its_lanes(gpu, mirt):
     assert ordered[:, 1].sum() < dfs[:, 1].sum()
 
 
-@pytest.mark.parametrize("quad,drain,quant", [(0, 0, 0), (0, 1, 0), (1, 0, 0), (0, 0, 1), (0, 1, 1)])
+@pytest.mark.parametrize("quad,drain,quant,dfs", [(0, 0, 0, 0), (0, 1, 0, 0), (1, 0, 0, 0), (0, 0, 1, 0), (0, 1, 1, 0),
+                                                  (0, 1, 0, 1), (1, 0, 0, 1)])
 @pytest.mark.parametrize("threshold,blocks", [(40, 0), (8, 0), (56, 64)])
-def test_bounce_modes_identical(gpu, mirt, golden, quad, drain, quant, threshold, blocks):
+def test_bounce_modes_identical(gpu, mirt, golden, quad, drain, quant, dfs, threshold, blocks):
     """The bounce pass's modes (one ray per lane, quad drain, one ray per
     quad), node formats (fp16 / 8-bit), refill thresholds and grid sizes give
     the golden 1080p frame."""
@@ -498,9 +499,10 @@ def test_bounce_modes_identical(gpu, mirt, golden, quad, drain, quant, threshold
     s, b = _scene(mirt, "render", 10000)
     gpu.upload(s, b)
     cam = mirt.default_camera()
-    q0 = gpu.get_option(abi.OPT_QUANT)
+    q0, d0 = gpu.get_option(abi.OPT_QUANT), gpu.get_option(abi.OPT_HNODE_DFS)
     try:
         gpu.set_option(abi.OPT_QUANT, quant)
+        gpu.set_option(abi.OPT_HNODE_DFS, dfs)
         gpu.set_option(abi.OPT_QUAD, quad)
         gpu.set_option(abi.OPT_QUAD_DRAIN, drain)
         gpu.set_option(abi.OPT_BOUNCE_THRESHOLD, threshold)
@@ -512,18 +514,20 @@ def test_bounce_modes_identical(gpu, mirt, golden, quad, drain, quant, threshold
         gpu.set_option(abi.OPT_BOUNCE_THRESHOLD, 32)
         gpu.set_option(abi.OPT_BOUNCE_BLOCKS, 0)
         gpu.set_option(abi.OPT_QUANT, q0)
+        gpu.set_option(abi.OPT_HNODE_DFS, d0)
     key = "1920x1080_render10000_d5_m1_b1_s1_c0_step1"
     assert sha(img) == golden["frames"][key]["sha"]
 
 
-@pytest.mark.parametrize("quant", [0, 1])
-def test_node_formats_match_golden_depth5(gpu, mirt, golden, small, quant):
+@pytest.mark.parametrize("quant,dfs", [(0, 0), (1, 0), (0, 1)])
+def test_node_formats_match_golden_depth5(gpu, mirt, golden, small, quant, dfs):
     """Both bounce-walk node formats (64-B fp16 / 48-B 8-bit) give every
     golden depth-5 BVH frame (100 .. 1M spheres, both cameras)."""
     abi = mirt.abi
     cs = cams(mirt, small)
-    q0 = gpu.get_option(abi.OPT_QUANT)
+    q0, d0 = gpu.get_option(abi.OPT_QUANT), gpu.get_option(abi.OPT_HNODE_DFS)
     gpu.set_option(abi.OPT_QUANT, quant)
+    gpu.set_option(abi.OPT_HNODE_DFS, dfs)
     try:
         for key, g in golden["frames"].items():
             p = parse_frame_key(key)
@@ -535,3 +539,4 @@ def test_node_formats_match_golden_depth5(gpu, mirt, golden, small, quant):
             assert sha(img[::p["step"]]) == g["sha"], key
     finally:
         gpu.set_option(abi.OPT_QUANT, q0)
+        gpu.set_option(abi.OPT_HNODE_DFS, d0)
