@@ -10,6 +10,7 @@ Reference call surface -> here (all compute goes through libmirt.so):
   camera init (main.c:203-211) / camera_update default_camera() / camera_update(cam)
     (camera.c:10-18)
   build_bvh_node (bvh.c:117-209)               build_bvh(spheres, start, end, depth) -> Bvh
+                                               build_bvh_cached(path, spheres, ...) (tree cache file)
                                                build_bvh_node(...) -> pointer tree (drop-in)
   get_camera_ray (ray.c:17-32) per pixel       Renderer.get_camera_rays(cam, W, H)
   trace_ray (renderer.c:21-77) per ray         Renderer.trace_ray(rays, depth, ...)
@@ -21,6 +22,7 @@ Reference call surface -> here (all compute goes through libmirt.so):
 Errors raise MirtError (the reference only printf's); there is no CPU path.
 """
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -101,6 +103,27 @@ def build_bvh(spheres, start=0, end=None, depth=0):
     finally:
         L.mirt_bvh_free_flat(out)
     return Bvh(nodes)
+
+
+def build_bvh_cached(path, spheres, start=0, end=None, depth=0):
+    """build_bvh through a flattened-tree cache file (mirt_bvh_build_flat_cached):
+    returns (Bvh, cached) with cached 1 = loaded from `path`, 0 = built and
+    written, -1 = built, file not written. `spheres` ends up reordered exactly
+    as build_bvh leaves it either way."""
+    assert spheres.dtype == abi.SPHERE and spheres.flags["C_CONTIGUOUS"]
+    end = len(spheres) if end is None else end
+    out = C.c_void_p()
+    cnt = C.c_int()
+    cached = C.c_int()
+    L = load()
+    check(L.mirt_bvh_build_flat_cached(os.fsencode(path), ptr(spheres), start, end, depth, C.byref(out),
+                                       C.byref(cnt), C.byref(cached)), "mirt_bvh_build_flat_cached")
+    try:
+        buf = (C.c_char * (cnt.value * abi.NODE.itemsize)).from_address(out.value)
+        nodes = np.frombuffer(bytes(buf), dtype=abi.NODE).copy()
+    finally:
+        L.mirt_bvh_free_flat(out)
+    return Bvh(nodes), cached.value
 
 
 def build_bvh_node(spheres, start=0, end=None, depth=0):

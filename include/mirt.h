@@ -181,6 +181,17 @@ int mirt_bvh_flatten(const mirt_bvh_node *root, const mirt_sphere *base, mirt_no
 int mirt_bvh_build_flat(mirt_sphere *spheres, int start, int end, int depth,
                         mirt_node **out_nodes, int *out_count);
 void mirt_bvh_free_flat(mirt_node *nodes);
+/* mirt_bvh_build_flat through a flattened-tree cache file (SURVEY.md §8(f)
+   rank 3; replaces the build_bvh_node call at main.c:225 / benchmark.c:317 on
+   a rerun). If `path` holds the tree of exactly these input spheres
+   (FNV-1a 64 of spheres[start,end) + start, end, depth; payload hash checked)
+   the reordered spheres are copied into spheres[start,end), the nodes are
+   returned and *out_cached = 1. Otherwise the tree is built, written to
+   `path` (temp file + rename) and *out_cached = 0, or -1 if the file could
+   not be written (the build result is still returned; mirt_last_error says
+   why). Same outputs as mirt_bvh_build_flat, bit for bit. */
+int mirt_bvh_build_flat_cached(const char *path, mirt_sphere *spheres, int start, int end, int depth,
+                               mirt_node **out_nodes, int *out_count, int *out_cached);
 
 /* ------------------------------------------------------ device context */
 

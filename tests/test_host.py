@@ -181,3 +181,39 @@ def test_threaded_build_same_tree(mirt, golden, levels, monkeypatch):
         assert mirt.flatten_bvh(root, s).nodes.tobytes() == one.nodes.tobytes()
     finally:
         mirt.free_bvh(root)
+
+
+def test_tree_cache_file(mirt, small, tmp_path):
+    """mirt_bvh_build_flat_cached: a miss builds and
+    writes the file, a hit loads the same reordered spheres and nodes bit for
+    bit; a file for other spheres, a corrupted or truncated file is rebuilt."""
+    path = tmp_path / "scene.bvh"
+    for attempt, want in [(0, 0), (1, 1)]:
+        s = small["render_1000_1_pre"].copy()
+        b, cached = mirt.build_bvh_cached(path, s)
+        assert cached == want, attempt
+        assert s.tobytes() == small["render_1000_1_post"].tobytes()
+        assert b.nodes.tobytes() == small["render_1000_1_tree"].tobytes()
+    # other spheres (and other build arguments) miss and overwrite
+    s = small["bench_1000_1_pre"].copy()
+    b, cached = mirt.build_bvh_cached(path, s, 0, 999, 20)  # benchmark.c:317
+    assert cached == 0 and b.nodes.tobytes() == small["bench_1000_1_tree"].tobytes()
+    s = small["bench_1000_1_pre"].copy()
+    assert mirt.build_bvh_cached(path, s, 0, 1000, 20)[1] == 0
+    assert mirt.build_bvh_cached(path, small["bench_1000_1_pre"].copy(), 0, 1000, 20)[1] == 1
+    # corrupt one payload byte, then truncate: both rebuild the same tree
+    raw = bytearray(path.read_bytes())
+    raw[len(raw) // 2] ^= 0x40
+    path.write_bytes(bytes(raw))
+    s = small["render_1000_1_pre"].copy()
+    b, cached = mirt.build_bvh_cached(path, s)
+    assert cached == 0 and b.nodes.tobytes() == small["render_1000_1_tree"].tobytes()
+    path.write_bytes(path.read_bytes()[:-7])
+    s = small["render_1000_1_pre"].copy()
+    assert mirt.build_bvh_cached(path, s)[1] == 0
+    assert s.tobytes() == small["render_1000_1_post"].tobytes()
+    # an unwritable path still returns the built tree, flagged -1
+    s = small["render_1000_1_pre"].copy()
+    b, cached = mirt.build_bvh_cached(tmp_path / "no_such_dir" / "x.bvh", s)
+    assert cached == -1 and b.nodes.tobytes() == small["render_1000_1_tree"].tobytes()
+    assert not list(tmp_path.glob("*.tmp.*"))
