@@ -540,3 +540,16 @@ def test_node_formats_match_golden_depth5(gpu, mirt, golden, small, quant, dfs):
     finally:
         gpu.set_option(abi.OPT_QUANT, q0)
         gpu.set_option(abi.OPT_HNODE_DFS, d0)
+
+
+def test_cached_tree_renders_golden_frame(gpu, mirt, golden, tmp_path):
+    """A scene uploaded from the tree cache file (mirt_bvh_build_flat_cached,
+    second call = a load) renders the golden 1080p depth-5 frame."""
+    path = tmp_path / "render10000.bvh"
+    for want in (0, 1):
+        s = mirt.create_random_spheres(10000, 1)
+        b, cached = mirt.build_bvh_cached(path, s)
+        assert cached == want
+    gpu.upload(s, b)
+    img = gpu.render_frame(mirt.default_camera(), 1920, 1080, depth=5, seed=1)
+    assert sha(img) == golden["frames"]["1920x1080_render10000_d5_m1_b1_s1_c0_step1"]["sha"]
