@@ -286,10 +286,12 @@ def main():
         host = None
         if world == 1 and not args.no_host:
             img = r.render_frame(cam, W, H, depth=DEPTH, seed=SEED, samples=SPP, jitter=JITTER)
-            t1 = time.perf_counter()
-            for _ in range(5):
+            dts = []
+            for _ in range(11):   # median call: pageable-buffer page faults make single calls noisy
+                t1 = time.perf_counter()
                 img = r.render_frame(cam, W, H, depth=DEPTH, seed=SEED, samples=SPP, jitter=JITTER)
-            host = W * H * SPP * 5 / (time.perf_counter() - t1) / 1e6
+                dts.append(time.perf_counter() - t1)
+            host = W * H * SPP / sorted(dts)[len(dts) // 2] / 1e6
         line = {
             "metric": "Mrays/s at 1080p, 10k spheres; 1/2/4/8 GPU + CPU baseline",
             "value": round(value, 3),
