@@ -131,7 +131,7 @@ SIGNATURES = [
     ("mirt_get_option", I, [P, I]),
 ]
 
-OPT_TRAVERSAL, OPT_FAST_SLAB, OPT_BLOCK_WAVES, OPT_DEFER, OPT_BOUNCE_THRESHOLD, OPT_PRUNE, OPT_ORDERED, OPT_WIDE = (
-    1, 2, 3, 4, 5, 6, 7, 8)
-OPT_BOUNCE_BLOCKS, OPT_QUAD, OPT_QUAD_DRAIN, OPT_QUANT, OPT_HNODE_DFS = 9, 10, 11, 12, 13
-TRAV_UNIFORM, TRAV_LANE, TRAV_HYBRID, TRAV_LANE_NP, TRAV_HYBRID_NP, TRAV_WAVEFRONT = 0, 1, 2, 3, 4, 5
+OPT_TRAVERSAL, OPT_FAST_SLAB, OPT_BLOCK_WAVES, OPT_DEFER, OPT_BOUNCE_THRESHOLD, OPT_PRUNE, OPT_ORDERED = (
+    1, 2, 3, 4, 5, 6, 7)
+OPT_BOUNCE_BLOCKS, OPT_QUAD_DRAIN = 9, 11
+TRAV_TILE, TRAV_WAVEFRONT = 0, 1

@@ -137,7 +137,7 @@ struct Deferred {
 
 // One pixel of the pixel loop: main.c:362-366 ray, trace_ray, then the
 // display/accumulation of main.c:368-372 (fresh) or main.c:394-405.
-template <int TRAV, bool FAST, bool COUNT>
+template <bool FAST, bool COUNT>
 __device__ __forceinline__ void render_pixel(const DevScene& sc, const FrameConst& f, int x, int r, bool alive,
                                              bool skip_generic, uint32_t* __restrict__ out, float* __restrict__ acc,
                                              Counters& cnt, uint32_t* cstack, int cstride,
@@ -147,7 +147,7 @@ __device__ __forceinline__ void render_pixel(const DevScene& sc, const FrameCons
     const Ray ray = camera_ray(f, alive ? x : 0, y, row_sample(f, r));
     if (skip_generic && alive && slab_ray(ray).generic) alive = false;  // a deferred wave traces it
     const uint64_t key = pixel_key(f.seed, (uint32_t)(y * f.width + x), row_sample(f, r));
-    const uint32_t c = trace_path<TRAV, FAST, COUNT>(sc, ray, alive, f.depth, f.use_bvh != 0, key, cnt, cstack,
+    const uint32_t c = trace_path<FAST, COUNT>(sc, ray, alive, f.depth, f.use_bvh != 0, key, cnt, cstack,
                                                      cstride, wstk);
     if (!alive) return;
     const size_t i = (size_t)r * f.width + x;
@@ -170,7 +170,7 @@ __device__ __forceinline__ void render_pixel(const DevScene& sc, const FrameCons
 }
 
 // The pixel loop of main.c:358-374 (fresh) / main.c:382-407 (accumulate).
-template <int TRAV, bool FAST, bool COUNT>
+template <bool FAST, bool COUNT>
 __global__ __launch_bounds__(512) void render_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
                                                       float* __restrict__ acc, mirt_counts* counts,
                                                       uint32_t* wave_stats, Deferred dfr)
@@ -189,7 +189,7 @@ __global__ __launch_bounds__(512) void render_kernel(DevScene sc, FrameConst f, 
         const uint32_t stride = (uint32_t)(dfr.blocks * bw);
         for (uint32_t j = blockIdx.x * bw + wave; j < n; j += stride) {
             const uint32_t p = __builtin_amdgcn_readfirstlane(dfr.list[j]);
-            render_pixel<TRAV, FAST, COUNT>(sc, f, (int)(p % f.width), (int)(p / f.width), (threadIdx.x & 63) == 0,
+            render_pixel<FAST, COUNT>(sc, f, (int)(p % f.width), (int)(p / f.width), (threadIdx.x & 63) == 0,
                                             false, out, acc, cnt, cstack + threadIdx.x, blockDim.x, wstk);
         }
         if (COUNT) add_counts(counts, cnt);
@@ -200,7 +200,7 @@ __global__ __launch_bounds__(512) void render_kernel(DevScene sc, FrameConst f, 
     const int tiles_x = (f.width + 7) >> 3;
     const int x = (tile % tiles_x) * 8 + (lane & 7);
     const int r = (tile / tiles_x) * 8 + (lane >> 3);
-    render_pixel<TRAV, FAST, COUNT>(sc, f, x, r, x < f.width && r < f.num_rows, dfr.blocks > 0, out, acc, cnt,
+    render_pixel<FAST, COUNT>(sc, f, x, r, x < f.width && r < f.num_rows, dfr.blocks > 0, out, acc, cnt,
                                     cstack + threadIdx.x, blockDim.x, wstk);
     if (COUNT) {
         add_counts(counts, cnt);
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(256) void primary_kernel(DevScene sc, FrameConst f,
         const uint32_t stride = (uint32_t)(dfr.blocks * 4);
         for (uint32_t j = blockIdx.x * 4 + wave; j < n; j += stride) {
             const uint32_t p = __builtin_amdgcn_readfirstlane(dfr.list[j]);
-            render_pixel<kTravHybridNP, FAST, false>(sc, f, (int)(p % f.width), (int)(p / f.width), lane == 0, false,
+            render_pixel<FAST, false>(sc, f, (int)(p % f.width), (int)(p / f.width), lane == 0, false,
                                                      out, acc, cnt, cstack + threadIdx.x, 256);
         }
         return;
@@ -366,35 +366,22 @@ __global__ __launch_bounds__(256) void primary_kernel(DevScene sc, FrameConst f,
     }
 }
 
-// The walk of one bounce ray: WALK 0 = reference DFS order, 1 = ordered
-// binary (PNode, register stack), 2 = ordered four-wide (HNode, LDS stack),
-// 3 = four-wide with one ray per quad, 4 = WALK 2 over the 48-B QNodes.
+// The walk of one bounce ray: WALK 0 = reference DFS order (any tree),
+// 2 = ordered four-wide (HNode, LDS stack).
 template <int WALK>
 struct BounceWalk;
 template <>
 struct BounceWalk<0> {
-    LaneWalk w;
-    __device__ void start(const DevScene& sc) { w = lane_walk_dfs(sc.num_nodes); }
-    __device__ void stop() { w = lane_walk_start(false); }
-    __device__ bool walking() const { return lane_walking(w); }
+    DfsWalk w;
+    __device__ void start(const DevScene& sc) { w = DfsWalk{0u, sc.num_nodes}; }
+    __device__ void stop() { w = DfsWalk{kPNone, 0u}; }
+    __device__ bool walking() const { return w.cur != kPNone; }
     template <bool FAST>
     __device__ void step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr, uint32_t*, float& bt,
                          int& bs, Counters& cnt)
     {
-        ordered_lane_step<FAST, false, false>(sc, sr, sp, pr, w, bt, bs, cnt);
-    }
-};
-template <>
-struct BounceWalk<1> {
-    LaneWalk w;
-    __device__ void start(const DevScene&) { w = lane_walk_start(true); }
-    __device__ void stop() { w = lane_walk_start(false); }
-    __device__ bool walking() const { return lane_walking(w); }
-    template <bool FAST>
-    __device__ void step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr, uint32_t*, float& bt,
-                         int& bs, Counters& cnt)
-    {
-        ordered_lane_step<FAST, false, true>(sc, sr, sp, pr, w, bt, bs, cnt);
+        lane_step<FAST, false>(sc, sr, sp, pr, w.cur, bt, bs, cnt);
+        if (w.cur >= w.end) w.cur = kPNone;
     }
 };
 template <>
@@ -410,36 +397,10 @@ struct BounceWalk<2> {
         wide_lane_step<FAST, false>(sc, sr, sp, pr, w, stk, bt, bs, cnt);
     }
 };
-template <>
-struct BounceWalk<4> {  // BounceWalk<2> over the 48-B QNodes (MIRT_OPT_QUANT)
-    WideWalk w;
-    __device__ void start(const DevScene&) { w = wide_walk_start(true); }
-    __device__ void stop() { w = wide_walk_start(false); }
-    __device__ bool walking() const { return wide_walking(w); }
-    template <bool FAST>
-    __device__ void step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr, uint32_t* stk,
-                         float& bt, int& bs, Counters& cnt)
-    {
-        wide_lane_step<FAST, false, true>(sc, sr, sp, pr, w, stk, bt, bs, cnt);
-    }
-};
 
 // DIAG (mirt_bounce_stats): per wave {loop iterations, walking lanes summed
 // over them, the same two after the queue ran dry, start / queue-dry / end
 // time (100 MHz clock), longest chain << 32 | longest walk (in steps)}.
-template <>
-struct BounceWalk<3> {
-    QuadWalk w;
-    __device__ void start(const DevScene&) { w = QuadWalk{0u, 0u, 0u}; }
-    __device__ void stop() { w = QuadWalk{kPNone, 0u, 0u}; }
-    __device__ bool walking() const { return w.cur != kPNone; }
-    template <bool FAST>
-    __device__ void step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr, uint32_t* stk,
-                         float& bt, int& bs, Counters&)
-    {
-        quad_step<FAST>(sc, sr, sp, pr, w, stk, bt, bs);
-    }
-};
 
 // The shading of one lane whose walk for this level is done (renderer.c:46-77
 // for that level): returns true if the chain goes on (ray re-aimed); else the
@@ -473,9 +434,9 @@ __device__ __forceinline__ bool shade_level(const DevScene& sc, const FrameConst
     return false;
 }
 
-// Persistent bounce pass: each lane (WALK 3: each quad of lanes) owns one
-// pixel's chain of bounces, refilled from the primary pass's queue. WALK 2
-// (default) ends with a QUAD DRAIN: once the queue is dry and at most 16 of
+// Persistent bounce pass: each lane owns one pixel's chain of bounces,
+// refilled from the primary pass's queue. WALK 2 (default) ends with a QUAD
+// DRAIN: once the queue is dry and at most 16 of
 // a wave's lanes are still busy, their chains move to quads (registers by
 // ds_bpermute; the LDS stacks stay in the source lane's columns) and are
 // finished four lanes per ray -- a sparse wave costs full issue slots per
@@ -490,17 +451,13 @@ __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, 
     uint64_t dg_it = 0, dg_lanes = 0, dg_it_x = 0, dg_lanes_x = 0, dg_tx = 0;
     const uint64_t dg_t0 = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
     uint32_t dg_steps = 0, dg_chain = 0, dg_walk_max = 0, dg_chain_max = 0;
-    // WALK 3: one ray per quad of lanes -- its colour stack and walk stack are
-    // per ray (quad); the ray's state is replicated in the quad's lanes
-    constexpr bool QUAD = WALK == 3;
-    constexpr bool LANE4 = WALK == 2 || WALK == 4;  // four-wide, one ray per lane (HNode / QNode)
-    constexpr int cstride = QUAD ? kQuadStride : 256;
+    constexpr bool LANE4 = WALK == 2;  // four-wide, one ray per lane
+    constexpr int cstride = 256;
     __shared__ uint32_t cstack[kMaxDepth * cstride];
-    __shared__ uint32_t wstack[LANE4 ? kWideStack * kWideStride : QUAD ? kQuadStack * kQuadStride : 1];
+    __shared__ uint32_t wstack[LANE4 ? kWideStack * kWideStride : 1];
     __shared__ uint32_t qsrc[LANE4 ? 4 * 16 : 1];  // quad drain: source lane of each quad, per wave
-    const uint32_t slot = QUAD ? threadIdx.x >> 2 : threadIdx.x;
-    uint32_t* cs = cstack + slot;
-    uint32_t* stk = wstack + (WALK >= 2 ? slot : 0);
+    uint32_t* cs = cstack + threadIdx.x;
+    uint32_t* stk = wstack + (LANE4 ? threadIdx.x : 0);
     Counters cnt{0, 0, 0, 0, 0};
     const uint32_t n = __builtin_amdgcn_readfirstlane(qctl[0]);
     bool has = false, exhausted = false;
@@ -516,8 +473,7 @@ __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, 
     uint64_t key = 0;
     for (;;) {
         // refill lanes that own no chain (one atomic per wave, tile order kept)
-        const uint64_t need_all = __ballot(!has);
-        const uint64_t need = QUAD ? (need_all & 0x1111111111111111ull) : need_all;  // one per ray
+        const uint64_t need = __ballot(!has);
         if (need && !exhausted) {
             const int leader = __builtin_ctzll(need);
             uint32_t b = 0;
@@ -525,7 +481,7 @@ __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, 
             b = __builtin_amdgcn_readlane(b, leader);
             if (b + (uint32_t)__popcll(need) >= n) exhausted = true;
             if (!has) {
-                const uint32_t lane0 = QUAD ? (threadIdx.x & 60) : (threadIdx.x & 63);
+                const uint32_t lane0 = threadIdx.x & 63;
                 const uint32_t idx = b + (uint32_t)__popcll(need & ((1ull << lane0) - 1));
                 if (idx < n) {
                     const BounceRec rec = queue[idx];
@@ -574,8 +530,7 @@ __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, 
                 dg_chain += dg_steps;
                 dg_steps = 0;
             }
-            if (shade_level(sc, f, ray, best_t, best_s, level, k, key, cs, cstride, base0, pixel, out, acc,
-                            !QUAD || (threadIdx.x & 3) == 0)) {
+            if (shade_level(sc, f, ray, best_t, best_s, level, k, key, cs, cstride, base0, pixel, out, acc, true)) {
                 sr = slab_ray(ray);
                 sp = sph_ray(ray);
                 w.start(sc);
@@ -592,7 +547,7 @@ __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, 
         }
     }
     if constexpr (LANE4) {
-        // quad drain (over the HNodes: QNode and HNode indices agree) (uniform control flow here: every lane is active)
+        // quad drain (uniform control flow here: every lane is active)
         const uint64_t busy = __ballot(has);
         if (busy) {
             const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -662,7 +617,7 @@ __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, 
 }
 
 // trace_ray on explicit rays (renderer.c:21); ray i uses contract pixel i.
-template <int TRAV, bool FAST>
+template <bool FAST>
 __global__ __launch_bounds__(256) void trace_rays_kernel(DevScene sc, const mirt_ray* __restrict__ rays, int n,
                                                          int depth, int use_bvh, uint64_t seed, uint32_t sample,
                                                          uint32_t* __restrict__ out)
@@ -674,7 +629,7 @@ __global__ __launch_bounds__(256) void trace_rays_kernel(DevScene sc, const mirt
     Counters cnt{0, 0, 0, 0, 0};
     __shared__ uint32_t cstack[kMaxDepth * 256];
     __shared__ uint32_t wstack[kWideStack * kWideStride];
-    const uint32_t c = trace_path<TRAV, FAST, false>(sc, ray, alive, depth, use_bvh != 0,
+    const uint32_t c = trace_path<FAST, false>(sc, ray, alive, depth, use_bvh != 0,
                                                   pixel_key(seed, (uint32_t)i, sample), cnt, cstack + threadIdx.x, 256,
                                                   wstack + threadIdx.x);
     if (alive) out[i] = c;
@@ -882,18 +837,11 @@ struct mirt_ctx {
     HNode* d_hnodes = nullptr;  // four-wide layout (per-lane walks)
     HAux* d_haux = nullptr;
     LeafRec* d_leaves = nullptr;
-    int wide = 1;               // four-wide per-lane walks where the tree admits them
     float r_max = 0.0f, c_max = 0.0f;
     int bounce_threshold = 32;  // wavefront: shade finished rays once fewer lanes walk
     int bounce_blocks = 0;      // wavefront: persistent workgroups (set in mirt_create)
     int bounce_blocks_opt = 0;  // MIRT_OPT_BOUNCE_BLOCKS override (0: occupancy x CUs)
-    int quad = 0;               // four-wide bounce walk with one ray per quad of lanes
     int quad_drain = 1;         // four-wide bounce walk: finish the drain four lanes per ray
-    QNode* d_qnodes = nullptr;  // the four-wide layout in 48 B (null: the tree does not admit it)
-    int quant = 0;              // bounce walk over d_qnodes
-    int bounce_blocks_q = 0;    // persistent workgroups of the QNode bounce kernel
-    size_t hnode_count = 0;     // HNodes per order: d_hnodes / d_haux hold two orders
-    int hdfs = 0;               // walks use the depth-first HNode order
     void* d_queue = nullptr;    // wavefront: {count, head} + bounce records
     size_t queue_cap = 0;
     uint32_t* d_defer = nullptr;  // [count, list...]
@@ -1117,129 +1065,12 @@ void build_hnodes(const mirt_node* nd, int nn, const mirt_sphere* sp, int ns, st
     }
 }
 
-// QNode i of HNode i (trace.h): per axis, the origin is the least lo of the
-// node's live slots and the step the least power of two with which 255 steps
-// reach the greatest hi; each slot's lo / hi rounds down / up to a multiple
-// of the step, checked with the fp32 arithmetic the kernel decodes with
-// (q_dec). Returns false -- the walk keeps the 64-B nodes -- if a node's
-// inner or leaf references are not consecutive, a bound is not finite, or a
-// decoded bound would be subnormal.
-float q_dec_host(float org, uint32_t q, uint32_t e)
-{
-    const uint32_t bits = e << 23;
-    float step;
-    std::memcpy(&step, &bits, 4);
-    return org + (float)q * step;
-}
-
-bool build_qnodes(const mirt_node* nd, const std::vector<HNode>& hn, const std::vector<uint32_t>& src,
-                  std::vector<QNode>& qn)
-{
-    qn.assign(hn.size(), QNode{});
-    for (size_t i = 0; i < hn.size(); i++) {
-        QNode& q = qn[i];
-        uint32_t im = 0, lk = 0, ni = 0, nl = 0;
-        for (int k = 0; k < 4; k++) {
-            const uint32_t r = hn[i].slot[k].ref;
-            if (r == kPNone) continue;
-            if (r & kPLeaf) {
-                if (nl == 0) q.leaf = r & ~kPLeaf;
-                if ((r & ~kPLeaf) != q.leaf + nl) return false;
-                nl++;
-                lk |= 1u << k;
-            } else {
-                if (ni == 0) q.inner = r;
-                if (r != q.inner + ni) return false;
-                ni++;
-                im |= 1u << k;
-            }
-        }
-        const uint32_t live = im | lk;
-        uint32_t ex[3] = {127, 127, 127};
-        for (int a = 0; a < 3 && live; a++) {
-            float lo = INFINITY, hi = -INFINITY;
-            for (int k = 0; k < 4; k++)
-                if ((live >> k) & 1u) {
-                    lo = std::min(lo, nd[src[4 * i + k]].bmin[a]);
-                    hi = std::max(hi, nd[src[4 * i + k]].bmax[a]);
-                }
-            if (!std::isfinite(lo) || !std::isfinite(hi) || !(lo <= hi)) return false;
-            q.org[a] = lo;
-            const double need = ((double)hi - (double)lo) / 255.0;
-            int e = need > 0.0 ? std::max(1, std::ilogb(need) + 127) : 1;
-            while (e <= 254 && q_dec_host(lo, 255, (uint32_t)e) < hi) e++;
-            if (e > 254) return false;
-            while (e > 1 && q_dec_host(lo, 255, (uint32_t)(e - 1)) >= hi) e--;
-            ex[a] = (uint32_t)e;
-        }
-        for (int k = 0; k < 4; k++) {
-            if (!((live >> k) & 1u)) continue;
-            const mirt_node& n = nd[src[4 * i + k]];
-            for (int a = 0; a < 3; a++) {
-                const float o = q.org[a];
-                const double step = std::ldexp(1.0, (int)ex[a] - 127);
-                int ql = (int)std::clamp(std::floor(((double)n.bmin[a] - o) / step), 0.0, 255.0);
-                while (ql > 0 && q_dec_host(o, (uint32_t)ql, ex[a]) > n.bmin[a]) ql--;
-                int qh = (int)std::clamp(std::ceil(((double)n.bmax[a] - o) / step), 0.0, 255.0);
-                while (qh < 255 && q_dec_host(o, (uint32_t)qh, ex[a]) < n.bmax[a]) qh++;
-                const float dl = q_dec_host(o, (uint32_t)ql, ex[a]), dh = q_dec_host(o, (uint32_t)qh, ex[a]);
-                if (!(dl <= n.bmin[a]) || !(dh >= n.bmax[a])) return false;
-                if ((dl != 0.0f && std::fabs(dl) < 0x1p-126f) || (dh != 0.0f && std::fabs(dh) < 0x1p-126f))
-                    return false;
-                q.q[a] |= (uint32_t)ql << (8 * k);
-                q.q[3 + a] |= (uint32_t)qh << (8 * k);
-            }
-        }
-        q.meta = ex[0] | ex[1] << 8 | ex[2] << 16 | im << 24 | lk << 28;
-    }
-    return true;
-}
-
-// The HNodes renumbered depth-first (slot order) for MIRT_OPT_HNODE_DFS: a
-// node's first inner child follows it in memory, in the other half of its
-// 128-B cache line. Returns false (order kept) if some node is unreachable.
-bool hnodes_dfs_order(std::vector<HNode>& hn, std::vector<HAux>& hx)
-{
-    const size_t n = hn.size();
-    std::vector<uint32_t> nw(n, kPNone);
-    std::vector<uint32_t> stk{0};
-    uint32_t next = 0;
-    while (!stk.empty()) {
-        const uint32_t h = stk.back();
-        stk.pop_back();
-        if (h >= n || nw[h] != kPNone) return false;
-        nw[h] = next++;
-        for (int k = 3; k >= 0; k--) {
-            const uint32_t r = hn[h].slot[k].ref;
-            if (r != kPNone && !(r & kPLeaf)) stk.push_back(r);
-        }
-    }
-    if (next != n) return false;
-    std::vector<HNode> h2(n);
-    std::vector<HAux> x2(n);
-    for (size_t i = 0; i < n; i++) {
-        HNode t = hn[i];
-        for (auto& s : t.slot)
-            if (s.ref != kPNone && !(s.ref & kPLeaf)) s.ref = nw[s.ref];
-        h2[nw[i]] = t;
-        x2[nw[i]] = hx[i];
-    }
-    hn.swap(h2);
-    hx.swap(x2);
-    return true;
-}
-
 DevScene dev_scene(const mirt_ctx* c)
 {
-    // MIRT_OPT_HNODE_DFS: the depth-first copy in the second half of the
-    // HNode / HAux buffers (QNodes follow the first order only)
-    const size_t ho = c->hdfs ? c->hnode_count : 0;
     const bool prune = c->prune && c->prune_ok;
+    const bool ordered = prune && c->ordered && c->ordered_ok && c->fast_slab;
     return DevScene{c->d_nodes, c->d_nodes32, c->d_geo, c->d_color, (uint32_t)c->num_nodes, c->num_spheres,
-                    prune, c->r_max, c->c_max, c->d_pnodes, prune && c->ordered && c->ordered_ok && c->fast_slab,
-                    c->d_hnodes + ho, c->d_haux + ho, c->d_leaves,
-                    prune && c->ordered && c->ordered_ok && c->fast_slab && c->wide,
-                    c->quant && !ho ? c->d_qnodes : nullptr};
+                    prune, c->r_max, c->c_max, c->d_pnodes, ordered, c->d_hnodes, c->d_haux, c->d_leaves, ordered};
 }
 
 bool ctx_ok(mirt_ctx* c, bool need_scene, const char* fn)
@@ -1255,31 +1086,14 @@ bool ctx_ok(mirt_ctx* c, bool need_scene, const char* fn)
     return hipSetDevice(c->device) == hipSuccess;
 }
 
-template <int TRAV, bool FAST, bool COUNT>
-void launch_render_t(const DevScene& sc, const FrameConst& f, uint32_t* d_out, float* d_acc, hipStream_t s,
+template <bool COUNT>
+void dispatch_render(bool fast, const DevScene& sc, const FrameConst& f, uint32_t* d_out, float* d_acc, hipStream_t s,
                      int blocks, int bw, mirt_counts* d_counts, uint32_t* d_ws, Deferred dfr)
 {
-    render_kernel<TRAV, FAST, COUNT><<<blocks + dfr.blocks, 64 * bw, 0, s>>>(sc, f, d_out, d_acc, d_counts, d_ws, dfr);
-}
-
-template <bool COUNT>
-void dispatch_render(int trav, bool fast, const DevScene& sc, const FrameConst& f, uint32_t* d_out, float* d_acc,
-                     hipStream_t s, int blocks, int bw, mirt_counts* d_counts, uint32_t* d_ws, Deferred dfr)
-{
-#define MIRT_LAUNCH_TRAV(T)                                                                              \
-    case T:                                                                                            \
-        fast ? launch_render_t<T, true, COUNT>(sc, f, d_out, d_acc, s, blocks, bw, d_counts, d_ws, dfr)   \
-             : launch_render_t<T, false, COUNT>(sc, f, d_out, d_acc, s, blocks, bw, d_counts, d_ws, dfr); \
-        break;
-    switch (trav) {
-        MIRT_LAUNCH_TRAV(kTravUniform)
-        MIRT_LAUNCH_TRAV(kTravLane)
-        MIRT_LAUNCH_TRAV(kTravHybrid)
-        MIRT_LAUNCH_TRAV(kTravLaneNP)
-    default:
-        MIRT_LAUNCH_TRAV(kTravHybridNP)
-    }
-#undef MIRT_LAUNCH_TRAV
+    if (fast)
+        render_kernel<true, COUNT><<<blocks + dfr.blocks, 64 * bw, 0, s>>>(sc, f, d_out, d_acc, d_counts, d_ws, dfr);
+    else
+        render_kernel<false, COUNT><<<blocks + dfr.blocks, 64 * bw, 0, s>>>(sc, f, d_out, d_acc, d_counts, d_ws, dfr);
 }
 
 int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_acc, hipStream_t s, bool timed,
@@ -1339,19 +1153,10 @@ int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_ac
         HIP_TRY(hipEventRecord(c->ph1, s));
         if (d_bdiag && sc.wide)
             bounce_kernel<true, 2, true><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, d_bdiag);
-        else if (d_bdiag && sc.ordered)
-            bounce_kernel<true, 1, true><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, d_bdiag);
         else if (d_bdiag)
             bounce_kernel<true, 0, true><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, d_bdiag);
-        else if (c->fast_slab && sc.wide && c->quad)
-            bounce_kernel<true, 3><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain);
-        else if (c->fast_slab && sc.wide && sc.qnodes)
-            bounce_kernel<true, 4><<<c->bounce_blocks_opt ? c->bounce_blocks_opt : c->bounce_blocks_q, 256, 0, s>>>(
-                sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain);
-        else if (c->fast_slab && sc.wide)
+        else if (sc.wide)
             bounce_kernel<true, 2><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain);
-        else if (c->fast_slab && sc.ordered)
-            bounce_kernel<true, 1><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain);
         else if (c->fast_slab)
             bounce_kernel<true, 0><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain);
         else
@@ -1363,9 +1168,9 @@ int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_ac
         return MIRT_OK;
     }
     if (d_counts)
-        dispatch_render<true>(c->trav, true, sc, f, d_out, d_acc, s, blocks, bw, d_counts, d_wave_stats, dfr);
+        dispatch_render<true>(true, sc, f, d_out, d_acc, s, blocks, bw, d_counts, d_wave_stats, dfr);
     else
-        dispatch_render<false>(c->trav, c->fast_slab != 0, sc, f, d_out, d_acc, s, blocks, bw, nullptr, nullptr, dfr);
+        dispatch_render<false>(c->fast_slab != 0, sc, f, d_out, d_acc, s, blocks, bw, nullptr, nullptr, dfr);
     HIP_TRY(hipGetLastError());
     if (int rc = fold()) return rc;
     if (timed) HIP_TRY(hipEventRecord(c->ev1, s));
@@ -1434,10 +1239,6 @@ int mirt_create(int device, mirt_ctx** out)
         if (e == hipSuccess)
             e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bounce_kernel<true, 2>, 256, 0);
         c->bounce_blocks = std::max(1, cus) * std::max(1, per_cu);
-        int per_cu_q = 0;
-        if (e == hipSuccess)
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_q, bounce_kernel<true, 4>, 256, 0);
-        c->bounce_blocks_q = std::max(1, cus) * std::max(1, per_cu_q);
         c->num_cus = cus;
     }
     if (e != hipSuccess) {
@@ -1455,7 +1256,7 @@ void mirt_destroy(mirt_ctx* c)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : {(void*)c->d_nodes, (void*)c->d_nodes32, (void*)c->d_geo, (void*)c->d_color, (void*)c->d_out, (void*)c->d_acc,
                     c->d_in, c->d_res, (void*)c->d_counts, (void*)c->d_defer, c->d_queue, (void*)c->d_keys, (void*)c->d_pnodes,
-                    (void*)c->d_hnodes, (void*)c->d_haux, (void*)c->d_leaves, (void*)c->d_qnodes})
+                    (void*)c->d_hnodes, (void*)c->d_haux, (void*)c->d_leaves})
         if (p) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -1497,9 +1298,8 @@ int mirt_scene_upload_flat(mirt_ctx* c, const mirt_sphere* spheres, int ns, cons
     geo[ns] = make_float4(NAN, NAN, NAN, NAN);  // &spheres[N] sentinel: never hits
     col[ns] = 0xff000000u;
     for (void* p : {(void*)c->d_nodes, (void*)c->d_nodes32, (void*)c->d_geo, (void*)c->d_color, (void*)c->d_pnodes,
-                    (void*)c->d_hnodes, (void*)c->d_haux, (void*)c->d_leaves, (void*)c->d_qnodes})
+                    (void*)c->d_hnodes, (void*)c->d_haux, (void*)c->d_leaves})
         if (p) (void)hipFree(p);
-    c->d_qnodes = nullptr;
     c->d_pnodes = nullptr;
     c->d_hnodes = nullptr;
     c->d_haux = nullptr;
@@ -1537,22 +1337,6 @@ int mirt_scene_upload_flat(mirt_ctx* c, const mirt_sphere* spheres, int ns, cons
     std::vector<LeafRec> lr;
     std::vector<uint32_t> src;
     build_hnodes(nodes, nn, spheres, ns, hn, hx, lr, src);
-    std::vector<QNode> qn;
-    if (build_qnodes(nodes, hn, src, qn)) {
-        HIP_TRY(hipMalloc((void**)&c->d_qnodes, sizeof(QNode) * qn.size()));
-        HIP_TRY(hipMemcpy(c->d_qnodes, qn.data(), sizeof(QNode) * qn.size(), hipMemcpyHostToDevice));
-    }
-    {  // second half: the depth-first copy (MIRT_OPT_HNODE_DFS); the first order if that fails
-        std::vector<HNode> h2 = hn;
-        std::vector<HAux> x2 = hx;
-        if (!hnodes_dfs_order(h2, x2)) {
-            h2 = hn;
-            x2 = hx;
-        }
-        c->hnode_count = hn.size();
-        hn.insert(hn.end(), h2.begin(), h2.end());
-        hx.insert(hx.end(), x2.begin(), x2.end());
-    }
     HIP_TRY(hipMalloc((void**)&c->d_hnodes, sizeof(HNode) * hn.size()));
     HIP_TRY(hipMalloc((void**)&c->d_haux, sizeof(HAux) * hx.size()));
     HIP_TRY(hipMalloc((void**)&c->d_leaves, sizeof(LeafRec) * std::max<size_t>(lr.size(), 1)));
@@ -1745,16 +1529,10 @@ int mirt_trace_rays(mirt_ctx* c, const mirt_ray* rays, int n, int depth, int use
         const DevScene sc = dev_scene(c);
         const mirt_ray* in = (const mirt_ray*)c->d_in;
         uint32_t* res = (uint32_t*)c->d_res;
-        const bool fast = c->fast_slab != 0;
-        if (c->trav == kTravUniform)
-            fast ? trace_rays_kernel<kTravUniform, true><<<g, b, 0, c->stream>>>(sc, in, n, depth, use_bvh, seed, sample, res)
-                 : trace_rays_kernel<kTravUniform, false><<<g, b, 0, c->stream>>>(sc, in, n, depth, use_bvh, seed, sample, res);
-        else if (c->trav == kTravLane)
-            fast ? trace_rays_kernel<kTravLane, true><<<g, b, 0, c->stream>>>(sc, in, n, depth, use_bvh, seed, sample, res)
-                 : trace_rays_kernel<kTravLane, false><<<g, b, 0, c->stream>>>(sc, in, n, depth, use_bvh, seed, sample, res);
+        if (c->fast_slab)
+            trace_rays_kernel<true><<<g, b, 0, c->stream>>>(sc, in, n, depth, use_bvh, seed, sample, res);
         else
-            fast ? trace_rays_kernel<kTravHybrid, true><<<g, b, 0, c->stream>>>(sc, in, n, depth, use_bvh, seed, sample, res)
-                 : trace_rays_kernel<kTravHybrid, false><<<g, b, 0, c->stream>>>(sc, in, n, depth, use_bvh, seed, sample, res);
+            trace_rays_kernel<false><<<g, b, 0, c->stream>>>(sc, in, n, depth, use_bvh, seed, sample, res);
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev1, c->stream));
@@ -1911,7 +1689,7 @@ int mirt_set_option(mirt_ctx* c, int option, int value)
     if (!c) return MIRT_E_INVALID;
     switch (option) {
     case MIRT_OPT_TRAVERSAL:
-        if (value < MIRT_TRAV_UNIFORM || value > MIRT_TRAV_WAVEFRONT) break;
+        if (value != MIRT_TRAV_TILE && value != MIRT_TRAV_WAVEFRONT) break;
         c->trav = value;
         return MIRT_OK;
     case MIRT_OPT_FAST_SLAB:
@@ -1930,24 +1708,12 @@ int mirt_set_option(mirt_ctx* c, int option, int value)
     case MIRT_OPT_ORDERED:
         c->ordered = value != 0;
         return MIRT_OK;
-    case MIRT_OPT_WIDE:
-        c->wide = value != 0;
-        return MIRT_OK;
     case MIRT_OPT_BOUNCE_BLOCKS:
         if (value < 0) break;
         c->bounce_blocks_opt = value;
         return MIRT_OK;
-    case MIRT_OPT_QUAD:
-        c->quad = value != 0;
-        return MIRT_OK;
     case MIRT_OPT_QUAD_DRAIN:
         c->quad_drain = value != 0;
-        return MIRT_OK;
-    case MIRT_OPT_QUANT:
-        c->quant = value != 0;
-        return MIRT_OK;
-    case MIRT_OPT_HNODE_DFS:
-        c->hdfs = value != 0;
         return MIRT_OK;
     case MIRT_OPT_BLOCK_WAVES:
         if (value != 1 && value != 2 && value != 4 && value != 8) break;
@@ -1970,12 +1736,8 @@ int mirt_get_option(mirt_ctx* c, int option)
     if (option == MIRT_OPT_BOUNCE_THRESHOLD) return c->bounce_threshold;
     if (option == MIRT_OPT_PRUNE) return c->prune;
     if (option == MIRT_OPT_ORDERED) return c->ordered;
-    if (option == MIRT_OPT_WIDE) return c->wide;
     if (option == MIRT_OPT_BOUNCE_BLOCKS) return c->bounce_blocks_opt;
-    if (option == MIRT_OPT_QUAD) return c->quad;
     if (option == MIRT_OPT_QUAD_DRAIN) return c->quad_drain;
-    if (option == MIRT_OPT_QUANT) return c->quant;
-    if (option == MIRT_OPT_HNODE_DFS) return c->hdfs;
     set_error("mirt_get_option: bad option %d", option);
     return MIRT_E_INVALID;
 }

@@ -86,22 +86,6 @@ static_assert(sizeof(HNode) == 64, "wide node is 64 B");
 struct HAux {
     uint32_t flat, end;
 };
-// The same four-wide node in 48 B (QNode i <-> HNode i, same slots): each
-// slot box as 8-bit offsets from a per-node origin in steps of a per-axis
-// power of two, lo rounded down and hi up (decoded as org + q * step in
-// fp32, exactly the arithmetic the host checked the fp32 box against).
-// References are implicit: the build gives a node's inner slots consecutive
-// HNode indices and its leaf slots consecutive LeafRec indices, so a slot's
-// reference is a base plus the count of same-kind slots before it.
-struct __attribute__((aligned(16))) QNode {
-    float org[3];
-    uint32_t meta;   // biased fp32 exponent of the x / y / z step (bits 0-23),
-                     // inner-slot mask (24-27), leaf-slot mask (28-31)
-    uint32_t inner;  // HNode index of the first inner slot
-    uint32_t leaf;   // LeafRec index of the first leaf slot
-    uint32_t q[6];   // lo x, lo y, lo z, hi x, hi y, hi z: byte k = slot k
-};
-static_assert(sizeof(QNode) == 48, "quantised wide node is 48 B");
 struct __attribute__((aligned(16))) LeafRec {
     float lo[3], hi[3];  // the leaf's exact box (bvh.c bounds)
     int32_t sphere;
@@ -133,9 +117,6 @@ struct DevScene {
     const HAux* haux;
     const LeafRec* leaves;
     int wide;
-    // the four-wide nodes in 48 B (QNode): set when MIRT_OPT_QUANT is on and
-    // the tree admits them
-    const QNode* qnodes;
 };
 
 struct Ray {
@@ -496,6 +477,40 @@ __device__ __forceinline__ float sphere_t(const SphRay& r, float4 s, float best)
     return (t > kEps && t <= best) ? t : -1.0f;
 }
 
+// One step of the per-lane DFS walk with on-demand loads (the body of
+// closest_bvh's per-lane loop), for kernels that interleave walking with
+// other per-lane work.
+// TIEKEY: inside an ordered walk the best so far may come from a later DFS
+// leaf, so a tie replaces it only for a larger sphere index (the DFS key).
+template <bool FAST, bool COUNT, bool TIEKEY = false>
+__device__ __forceinline__ void lane_step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
+                                          uint32_t& next, float& best_t, int& best_s, Counters& cnt)
+{
+    const float4* p = (const float4*)(sc.nodes32 + next);
+    const float4 a = p[0], b = p[1];
+    NodeV nd;
+    nd.b0 = a.x; nd.b1 = a.y; nd.b2 = a.z; nd.b3 = a.w; nd.b4 = b.x; nd.b5 = b.y;
+    nd.sphere = __float_as_int(b.z);
+    nd.skip = __float_as_uint(b.w);
+    const bool inner = nd.sphere < 0;
+    const bool pass = (nd.skip & MIRT_NODE_EMPTY) || slab<FAST>(sr, pr, nd);
+    if (COUNT) cnt.nodes++;
+    if (pass && inner) {
+        next = next + 1;
+    } else {
+        if (pass) {
+            if (COUNT) cnt.spheres++;
+            const float t = sphere_t<FAST>(sp, sc.geo[nd.sphere], best_t);
+            if (t > 0.0f && (!TIEKEY || t < best_t || nd.sphere > best_s)) {
+                best_t = t;
+                best_s = nd.sphere;
+                if (sc.prune) prune_update(pr, sc, sr.ox, sr.oy, sr.oz, sp.a4, t);
+            }
+        }
+        next = nd.skip & MIRT_SKIP_MASK;
+    }
+}
+
 // Closest hit over the flattened tree in the reference's DFS order
 // (hit.c:91-109: left before right; the later leaf wins a tie on t, so the
 // scan keeps `t <= best`). Each lane keeps only `next`, the index of the
@@ -508,12 +523,12 @@ __device__ __forceinline__ float sphere_t(const SphRay& r, float4 s, float best)
 // without visiting its root), so the cursor advances to i + 1 if any lane
 // descended and to skip(i) otherwise -- no stack, no reduction, and every
 // node load is a scalar load.
-// Otherwise (LANE): every lane walks its own sequence with vector loads.
+// Otherwise every lane walks its own sequence with vector loads (lane_step).
 //
-// Both walks are latency-bound chains (load -> test -> next index), so each
-// step issues the loads of BOTH possible successors (i + 1 and skip(i))
+// The uniform walk is a latency-bound chain (load -> test -> next index), so
+// each step issues the loads of BOTH possible successors (i + 1 and skip(i))
 // before testing node i; the test then overlaps the load latency.
-template <bool UNIFORM, bool FAST, bool COUNT, bool LPF = true>
+template <bool UNIFORM, bool FAST, bool COUNT>
 __device__ __forceinline__ void closest_bvh(const DevScene& sc, const Ray& ray, bool active, float& best_t,
                                             int& best_s, Counters& cnt)
 {
@@ -566,103 +581,12 @@ __device__ __forceinline__ void closest_bvh(const DevScene& sc, const Ray& ray, 
             }
         }
     } else {
-      if constexpr (!LPF) {
-        // no prefetch: 32 B of box/links per step, the leaf sphere only when
-        // the leaf's box passes
+        // per lane: 32 B of box/links per step, the leaf sphere only when the
+        // leaf's box passes
         while (__ballot(next < end)) {
             if (COUNT) cnt.steps++;
-            if (next < end) {
-                const float4* p = (const float4*)(sc.nodes32 + next);
-                const float4 a = p[0], b = p[1];
-                NodeV nd;
-                nd.b0 = a.x; nd.b1 = a.y; nd.b2 = a.z; nd.b3 = a.w; nd.b4 = b.x; nd.b5 = b.y;
-                nd.sphere = __float_as_int(b.z);
-                nd.skip = __float_as_uint(b.w);
-                const bool inner = nd.sphere < 0;
-                const bool pass = (nd.skip & MIRT_NODE_EMPTY) || slab<FAST>(sr, pr, nd);
-                if (COUNT) cnt.nodes++;
-                if (pass && inner) {
-                    next = next + 1;
-                } else {
-                    if (pass) {
-                        if (COUNT) cnt.spheres++;
-                        const float t = sphere_t<FAST>(sp, sc.geo[nd.sphere], best_t);
-                        if (t > 0.0f) {
-                            best_t = t;
-                            best_s = nd.sphere;
-                            if (sc.prune) prune_update(pr, sc, ray.ox, ray.oy, ray.oz, sp.a4, t);
-                        }
-                    }
-                    next = nd.skip & MIRT_SKIP_MASK;
-                }
-            }
+            if (next < end) lane_step<FAST, COUNT>(sc, sr, sp, pr, next, best_t, best_s, cnt);
         }
-        return;
-      }
-        NodeV nd;
-        if (next < end) nd = load_node_lane(sc.nodes, next);
-        while (__ballot(next < end)) {
-            if (COUNT) cnt.steps++;
-            if (next < end) {
-                const uint32_t skip = nd.skip & MIRT_SKIP_MASK;
-                const bool inner = nd.sphere < 0;
-                const NodeV na = load_node_lane(sc.nodes, min(next + 1, last));
-                NodeV nb = na;
-                if (inner) nb = load_node_lane(sc.nodes, min(skip, last));
-                const bool pass = (nd.skip & MIRT_NODE_EMPTY) || slab<FAST>(sr, pr, nd);
-                if (COUNT) cnt.nodes++;
-                if (pass && inner) {
-                    next = next + 1;
-                    nd = na;
-                } else {
-                    if (pass) {
-                        if (COUNT) cnt.spheres++;
-                        const float t = sphere_t<FAST>(sp, nd.g, best_t);
-                        if (t > 0.0f) {
-                            best_t = t;
-                            best_s = nd.sphere;
-                            if (sc.prune) prune_update(pr, sc, ray.ox, ray.oy, ray.oz, sp.a4, t);
-                        }
-                    }
-                    next = skip;
-                    nd = nb;
-                }
-            }
-        }
-    }
-}
-
-// One step of the per-lane walk with on-demand loads (the body of
-// closest_bvh's LANE_NP loop), for kernels that interleave walking with
-// other per-lane work.
-// TIEKEY: inside an ordered walk the best so far may come from a later DFS
-// leaf, so a tie replaces it only for a larger sphere index (the DFS key).
-template <bool FAST, bool COUNT, bool TIEKEY = false>
-__device__ __forceinline__ void lane_step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
-                                          uint32_t& next, float& best_t, int& best_s, Counters& cnt)
-{
-    const float4* p = (const float4*)(sc.nodes32 + next);
-    const float4 a = p[0], b = p[1];
-    NodeV nd;
-    nd.b0 = a.x; nd.b1 = a.y; nd.b2 = a.z; nd.b3 = a.w; nd.b4 = b.x; nd.b5 = b.y;
-    nd.sphere = __float_as_int(b.z);
-    nd.skip = __float_as_uint(b.w);
-    const bool inner = nd.sphere < 0;
-    const bool pass = (nd.skip & MIRT_NODE_EMPTY) || slab<FAST>(sr, pr, nd);
-    if (COUNT) cnt.nodes++;
-    if (pass && inner) {
-        next = next + 1;
-    } else {
-        if (pass) {
-            if (COUNT) cnt.spheres++;
-            const float t = sphere_t<FAST>(sp, sc.geo[nd.sphere], best_t);
-            if (t > 0.0f && (!TIEKEY || t < best_t || nd.sphere > best_s)) {
-                best_t = t;
-                best_s = nd.sphere;
-                if (sc.prune) prune_update(pr, sc, sr.ox, sr.oy, sr.oz, sp.a4, t);
-            }
-        }
-        next = nd.skip & MIRT_SKIP_MASK;
     }
 }
 
@@ -922,96 +846,11 @@ __device__ __forceinline__ void closest_packet_ordered(const DevScene& sc, const
     }
 }
 
-// Per-lane ordered walk state (bounce rays): `cur` is the PNode to visit
-// (kPNone: done), or, while `end` != 0, the next flat node of a DFS segment
-// that ends at `end`. The far children still to visit sit in an 8-entry
-// shift-register stack; when it is full and both children pass, the node's
-// children are walked as the flat DFS segment [flat + 1, end) instead (the
-// reference order, pruned, no stack). 8 entries: on the 10k scene a 4-entry
-// stack costs little on average but doubles the longest walks (p99 147 ->
-// 210 steps, max 258 -> 492), which set the bounce pass's tail.
-constexpr int kLaneStack = 8;
-struct LaneWalk {
+// Per-lane DFS walk (any tree, the reference order): `cur` is the next flat
+// node, the walk ends at `end` (kPNone: done).
+struct DfsWalk {
     uint32_t cur, end;
-    uint32_t top;
-    uint32_t s0, s1, s2, s3, s4, s5, s6, s7;
 };
-
-__device__ __forceinline__ LaneWalk lane_walk_start(bool active)
-{
-    return LaneWalk{active ? 0u : kPNone, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-}
-
-__device__ __forceinline__ bool lane_walking(const LaneWalk& w) { return w.cur != kPNone; }
-
-__device__ __forceinline__ void lane_walk_pop(LaneWalk& w)
-{
-    if (w.top == 0) {
-        w.cur = kPNone;
-        return;
-    }
-    w.cur = w.s0;
-    w.s0 = w.s1;
-    w.s1 = w.s2;
-    w.s2 = w.s3;
-    w.s3 = w.s4;
-    w.s4 = w.s5;
-    w.s5 = w.s6;
-    w.s6 = w.s7;
-    w.top--;
-}
-
-// ORD = false: the walk is one DFS segment over the whole tree (the
-// reference order, hit.c's tie rule `t <= best`), started by lane_walk_dfs.
-__device__ __forceinline__ LaneWalk lane_walk_dfs(uint32_t num_nodes)
-{
-    return LaneWalk{0u, num_nodes, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-}
-
-template <bool FAST, bool COUNT, bool ORD = true>
-__device__ __forceinline__ void ordered_lane_step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
-                                                  LaneWalk& w, float& best_t, int& best_s, Counters& cnt)
-{
-    if (COUNT) cnt.steps++;
-    if (!ORD || w.end) {
-        lane_step<FAST, COUNT, ORD>(sc, sr, sp, pr, w.cur, best_t, best_s, cnt);
-        if (w.cur >= w.end) {
-            w.end = 0;
-            lane_walk_pop(w);
-        }
-        return;
-    }
-    const PNodeV nd = load_pnode_lane(sc.pnodes, w.cur);
-    float e0 = 0.0f, e1 = 0.0f;
-    const bool h0 = visit_child<FAST, COUNT>(sc, sr, sp, pr, nd.r0, nd.a0, nd.a1, nd.a2, nd.a3, nd.a4, nd.a5, e0,
-                                             best_t, best_s, cnt);
-    const bool h1 = visit_child<FAST, COUNT>(sc, sr, sp, pr, nd.r1, nd.b0, nd.b1, nd.b2, nd.b3, nd.b4, nd.b5, e1,
-                                             best_t, best_s, cnt);
-    if (h0 && h1) {
-        if (w.top < kLaneStack) {
-            const bool swap = e1 < e0;
-            w.s7 = w.s6;
-            w.s6 = w.s5;
-            w.s5 = w.s4;
-            w.s4 = w.s3;
-            w.s3 = w.s2;
-            w.s2 = w.s1;
-            w.s1 = w.s0;
-            w.s0 = swap ? nd.r0 : nd.r1;
-            w.top++;
-            w.cur = swap ? nd.r1 : nd.r0;
-        } else {
-            w.cur = nd.flat + 1;
-            w.end = nd.end;
-        }
-    } else if (h0) {
-        w.cur = nd.r0;
-    } else if (h1) {
-        w.cur = nd.r1;
-    } else {
-        lane_walk_pop(w);
-    }
-}
 
 // Per-lane four-wide walk (bounce rays): `cur` is the HNode to visit (kPNone:
 // done) or, while `end` != 0, the next node of a flat DFS segment ending at
@@ -1068,15 +907,7 @@ __device__ __forceinline__ void wide_leaf(const DevScene& sc, const SlabRay& sr,
     }
 }
 
-// A QNode slot bound: org + q * step in fp32 (q * step is exact), the
-// arithmetic build_qnodes checked against the node's fp32 box.
-__device__ __forceinline__ float q_dec(float org, uint32_t q, int k, float step)
-{
-    return org + (float)((q >> (8 * k)) & 0xffu) * step;
-}
-
-// Q: read the 48-B QNodes instead of the 64-B HNodes (same walk, same stack).
-template <bool FAST, bool COUNT, bool Q = false>
+template <bool FAST, bool COUNT>
 __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
                                                WideWalk& w, uint32_t* stk, float& best_t, int& best_s, Counters& cnt)
 {
@@ -1094,33 +925,7 @@ __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay
     float e0 = 0.0f, e1 = 0.0f, e2 = 0.0f, e3 = 0.0f;
     bool h0, h1, h2, h3;
     uint4 q3;  // the slots' references
-    if constexpr (Q) {
-        const uint4* p = (const uint4*)(sc.qnodes + w.cur);
-        const uint4 a = p[0], b = p[1], c = p[2];
-        const float ox = __uint_as_float(a.x), oy = __uint_as_float(a.y), oz = __uint_as_float(a.z);
-        const float sx = __uint_as_float((a.w & 0xffu) << 23);
-        const float sy = __uint_as_float(((a.w >> 8) & 0xffu) << 23);
-        const float sz = __uint_as_float(((a.w >> 16) & 0xffu) << 23);
-        const uint32_t im = (a.w >> 24) & 0xfu, lk = a.w >> 28;
-        auto test = [&](int k, float& e) {
-            const bool live = ((im | lk) >> k) & 1u;
-            if (COUNT && live) cnt.nodes++;
-            const bool pass = slab_cons(sr, pr, q_dec(ox, b.z, k, sx), q_dec(oy, b.w, k, sy), q_dec(oz, c.x, k, sz),
-                                        q_dec(ox, c.y, k, sx), q_dec(oy, c.z, k, sy), q_dec(oz, c.w, k, sz), e);
-            return pass & live;
-        };
-        h0 = test(0, e0);
-        h1 = test(1, e1);
-        h2 = test(2, e2);
-        h3 = test(3, e3);
-        auto ref = [&](int k) {
-            const uint32_t below = (1u << k) - 1u;
-            return (im >> k) & 1u   ? b.x + (uint32_t)__builtin_popcount(im & below)
-                   : (lk >> k) & 1u ? kPLeaf | (b.y + (uint32_t)__builtin_popcount(lk & below))
-                                    : kPNone;
-        };
-        q3 = make_uint4(ref(0), ref(1), ref(2), ref(3));
-    } else {
+    {
         const uint4* p = (const uint4*)(sc.hnodes + w.cur);
         const uint4 s0 = p[0], s1 = p[1], s2 = p[2], s3 = p[3];
         auto test = [&](const uint4& q, float& e) {
@@ -1190,8 +995,6 @@ __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay
 // values; candidates and the order of the passing children are reduced
 // across the quad with DPP. The result is the same closest hit: least t,
 // a tie to the larger sphere index -- an order-free rule.
-constexpr int kQuadStack = 32;   // entries per ray, in LDS
-constexpr int kQuadStride = 64;  // rays (quads) per 256-thread workgroup
 
 template <int CTRL>
 __device__ __forceinline__ uint32_t quad_perm(uint32_t v)
@@ -1224,7 +1027,7 @@ __device__ __forceinline__ void cand_merge(float& t, int& si)
 }
 
 // `stk`: this ray's LDS stack column (entry k at stk[k * STRIDE], CAP entries).
-template <bool FAST, int STRIDE = kQuadStride, int CAP = kQuadStack>
+template <bool FAST, int STRIDE, int CAP>
 __device__ __forceinline__ void quad_step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
                                           QuadWalk& w, uint32_t* stk, float& best_t, int& best_s)
 {
@@ -1306,7 +1109,7 @@ __device__ __forceinline__ void quad_step(const DevScene& sc, const SlabRay& sr,
 // direction component, `SlabRay::generic`) one at a time with the whole
 // wave (closest_bvh_chunked), the rest with the lane-parallel walk (or the
 // ordered packet walk, for UNIFORM on a tree that admits it).
-template <bool UNIFORM, bool FAST, bool COUNT, bool LPF = true>
+template <bool UNIFORM, bool FAST, bool COUNT>
 __device__ __forceinline__ void closest_hit(const DevScene& sc, const Ray& ray, bool active, float& best_t,
                                             int& best_s, Counters& cnt, uint32_t* wstk = nullptr)
 {
@@ -1327,23 +1130,10 @@ __device__ __forceinline__ void closest_hit(const DevScene& sc, const Ray& ray, 
         WideWalk w = wide_walk_start(active && !gen);
         while (__ballot(wide_walking(w))) {
             if (!wide_walking(w)) continue;
-            // counts follow the bounce kernel's node format (MIRT_OPT_QUANT)
-            if (COUNT && sc.qnodes)
-                wide_lane_step<FAST, COUNT, true>(sc, sr, sp, pr, w, wstk, best_t, best_s, cnt);
-            else
-                wide_lane_step<FAST, COUNT>(sc, sr, sp, pr, w, wstk, best_t, best_s, cnt);
+            wide_lane_step<FAST, COUNT>(sc, sr, sp, pr, w, wstk, best_t, best_s, cnt);
         }
-    } else if (!UNIFORM && FAST && sc.ordered) {
-        const SlabRay sr = slab_ray(ray);
-        const SphRay sp = sph_ray(ray);
-        Prune pr = prune_off();
-        best_t = INFINITY;
-        best_s = -1;
-        LaneWalk w = lane_walk_start(active && !gen);
-        while (__ballot(lane_walking(w)))
-            if (lane_walking(w)) ordered_lane_step<FAST, COUNT>(sc, sr, sp, pr, w, best_t, best_s, cnt);
     } else {
-        closest_bvh<UNIFORM, FAST, COUNT, LPF>(sc, ray, active && !gen, best_t, best_s, cnt);
+        closest_bvh<UNIFORM, FAST, COUNT>(sc, ray, active && !gen, best_t, best_s, cnt);
     }
     uint64_t gm = __ballot(gen);
     const int lane = threadIdx.x & 63;
@@ -1452,11 +1242,12 @@ __device__ __forceinline__ uint32_t blend_rgba(uint32_t base, uint32_t refl)
     return out;
 }
 
-// Traversal schedules (mirt_set_option MIRT_OPT_TRAVERSAL).
-// LANE / HYBRID prefetch both successors; the *_NP forms load on demand.
-// WAVEFRONT: camera rays as packets, then persistent per-lane bounce chains
-// fed by a queue (render.hip primary_kernel / bounce_kernel), depth >= 2.
-enum Trav { kTravUniform = 0, kTravLane = 1, kTravHybrid = 2, kTravLaneNP = 3, kTravHybridNP = 4, kTravWavefront = 5 };
+// Frame schedules (mirt_set_option MIRT_OPT_TRAVERSAL). TILE: one kernel,
+// each wave traces the whole paths of an 8x8 tile (trace_path: camera rays
+// as a packet, bounces per lane). WAVEFRONT (default, depth >= 2): camera
+// rays as packets, then persistent per-lane bounce chains fed by a queue
+// (render.hip primary_kernel / bounce_kernel).
+enum Trav { kTravTile = 0, kTravWavefront = 1 };
 
 // trace_ray (renderer.c:21-77) with the recursion turned into a loop over
 // bounce levels that the whole wave executes together (the traversal needs
@@ -1464,7 +1255,7 @@ enum Trav { kTravUniform = 0, kTravLane = 1, kTravHybrid = 2, kTravLaneNP = 3, k
 // The base colours of the hit levels (folded innermost-first at the end,
 // renderer.c:55-58) live in LDS, `cstack[level * cstride]`, one column per
 // thread, to keep them out of the register budget.
-template <int TRAV, bool FAST, bool COUNT>
+template <bool FAST, bool COUNT>
 __device__ __forceinline__ uint32_t trace_path(const DevScene& sc, Ray ray, bool alive, int depth, bool use_bvh,
                                                uint64_t key, Counters& cnt, uint32_t* cstack, int cstride,
                                                uint32_t* wstk = nullptr)
@@ -1478,12 +1269,11 @@ __device__ __forceinline__ uint32_t trace_path(const DevScene& sc, Ray ray, bool
         int s;
         if (use_bvh) {
             // primary rays of an 8x8 tile are coherent: walk them as one
-            // packet; bounce rays scatter: each lane walks alone (hybrid)
-            constexpr bool lpf = TRAV == kTravLane || TRAV == kTravHybrid;
-            if (TRAV == kTravUniform || ((TRAV == kTravHybrid || TRAV == kTravHybridNP) && level == 0))
+            // packet; bounce rays scatter: each lane walks alone
+            if (level == 0)
                 closest_hit<true, FAST, COUNT>(sc, ray, alive, t, s, cnt);
             else
-                closest_hit<false, FAST, COUNT, lpf>(sc, ray, alive, t, s, cnt, wstk);
+                closest_hit<false, FAST, COUNT>(sc, ray, alive, t, s, cnt, wstk);
         } else {
             closest_brute<FAST, COUNT>(sc, ray, alive, t, s, cnt);
         }

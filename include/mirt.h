@@ -288,47 +288,36 @@ float mirt_last_kernel_ms(mirt_ctx *ctx);
 int mirt_last_phase_ms(mirt_ctx *ctx, float *phase);
 
 /* Kernel schedule knobs (results are identical under every setting; only
-   speed changes). MIRT_OPT_TRAVERSAL: how a wave walks the tree --
-   MIRT_TRAV_UNIFORM (the wave walks the union of its lanes' walks with one
-   cursor, scalar node loads), MIRT_TRAV_LANE (each lane walks alone, vector
-   node loads), MIRT_TRAV_HYBRID (uniform for camera rays, per-lane for
-   bounces), MIRT_TRAV_HYBRID_NP (the same without successor prefetch in the
-   per-lane walk). MIRT_OPT_FAST_SLAB: 1 (default) = reciprocal-multiply
-   slab test with an exact-division fallback for undecidable boxes; 0 = the
-   division-only slab test of hit.c:49-82. MIRT_OPT_BLOCK_WAVES: 8x8 pixel
-   tiles (waves) per workgroup of the frame kernel: 1, 2, 4 (default) or 8.
-   MIRT_OPT_DEFER: 1 (default) = camera rays with a zero/tiny direction
+   speed changes). MIRT_OPT_TRAVERSAL: MIRT_TRAV_WAVEFRONT (default: camera-ray
+   packets, then persistent per-lane bounce chains fed by a queue, for BVH
+   frames of depth >= 2) or MIRT_TRAV_TILE (one kernel: each wave traces the
+   whole paths of an 8x8 tile; always used for depth 1 and brute force).
+   MIRT_OPT_FAST_SLAB: 1 (default) = reciprocal-multiply slab test with an
+   exact-division fallback for undecidable boxes; 0 = the division-only slab
+   test of hit.c:49-82 (and the reference DFS order everywhere).
+   MIRT_OPT_BLOCK_WAVES: 8x8 pixel tiles (waves) per workgroup of the tile
+   kernel: 1, 2, 4 (default) or 8. MIRT_OPT_DEFER: 1 (default) = on a tree
+   that does not admit ordered walks, camera rays with a zero/tiny direction
    component are traced first, one per wave (node-parallel walk).
    MIRT_OPT_PRUNE: 1 (default) = with the fast slab test, skip subtrees whose
    box the ray provably enters beyond the best hit so far (the closest hit and
    its tie rule are unchanged; active only for a tree whose boxes enclose
    their subtrees, checked at upload); 0 = the reference's exhaustive DFS.
    MIRT_OPT_ORDERED: 1 (default) = with pruning, walks enter the nearer child
-   first (same closest hit: ties still go to the later DFS leaf; active only
-   for a tree whose leaves hold increasing sphere indices in DFS order, as
-   the reference's builds do, and depth < 63); 0 = DFS order.
-   MIRT_OPT_WIDE: 1 (default) = with ordering, per-lane (bounce) walks use a
-   four-wide re-layout of the same tree (half the dependent steps; exact
-   because the reference slab test is monotone under box containment);
-   0 = the binary ordered walk. */
+   first -- camera rays as packets over both-children nodes, bounce rays over
+   a four-wide re-layout of the same tree (exact because the reference slab
+   test is monotone under box containment); same closest hit, ties still go
+   to the later DFS leaf; active only for a tree whose leaves hold increasing
+   sphere indices in DFS order, as the reference's builds do, and depth < 63;
+   0 = DFS order. */
 enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3, MIRT_OPT_DEFER = 4,
        MIRT_OPT_BOUNCE_THRESHOLD = 5, /* wavefront: shade finished bounce rays once fewer than
                                          this many lanes of a wave still walk (0..64, default 32) */
-       MIRT_OPT_PRUNE = 6, MIRT_OPT_ORDERED = 7, MIRT_OPT_WIDE = 8,
+       MIRT_OPT_PRUNE = 6, MIRT_OPT_ORDERED = 7,
        MIRT_OPT_BOUNCE_BLOCKS = 9,  /* wavefront: persistent bounce workgroups, 0 = occupancy x CUs */
-       MIRT_OPT_QUAD = 10,          /* four-wide bounce walk: 1 = one ray per quad of lanes throughout,
-                                       the four slot tests side by side; 0 (default) = one ray per lane */
-       MIRT_OPT_QUAD_DRAIN = 11,    /* four-wide, one ray per lane: 1 (default) = once the queue is dry
-                                       and <= 16 lanes of a wave are busy, finish them as quads */
-       MIRT_OPT_QUANT = 12,         /* four-wide, one ray per lane: 1 = the bounce walk reads 48-B nodes
-                                       whose slot boxes are 8-bit offsets from a per-node origin
-                                       (rounded outward); 0 = the 64-B fp16 nodes */
-       MIRT_OPT_HNODE_DFS = 13      /* four-wide walks: 1 = the 64-B nodes numbered depth-first (a node's
-                                       first inner child next to it in memory); 0 = breadth-first */ };
-enum { MIRT_TRAV_UNIFORM = 0, MIRT_TRAV_LANE = 1, MIRT_TRAV_HYBRID = 2, MIRT_TRAV_LANE_NP = 3,
-       MIRT_TRAV_HYBRID_NP = 4,  /* *_NP: per-lane walk without successor prefetch */
-       MIRT_TRAV_WAVEFRONT = 5   /* default: camera-ray packets, then persistent per-lane
-                                    bounce chains fed by a queue (depth >= 2) */ };
+       MIRT_OPT_QUAD_DRAIN = 11     /* four-wide bounce walk: 1 (default) = once the queue is dry
+                                       and <= 16 lanes of a wave are busy, finish them as quads */ };
+enum { MIRT_TRAV_TILE = 0, MIRT_TRAV_WAVEFRONT = 1 };
 int mirt_set_option(mirt_ctx *ctx, int option, int value);
 int mirt_get_option(mirt_ctx *ctx, int option);
 

@@ -22,7 +22,7 @@ def main():
     r = mirt.Renderer(0)
     r.upload(s, b)
     cam = mirt.default_camera()
-    for depth, trav in [(1, abi.TRAV_UNIFORM), (5, abi.TRAV_HYBRID)]:
+    for depth, trav in [(1, abi.TRAV_TILE), (5, abi.TRAV_TILE)]:
         r.set_option(abi.OPT_TRAVERSAL, trav)
         for bw in (1, 2, 4, 8):
             r.set_option(abi.OPT_BLOCK_WAVES, bw)

@@ -2,7 +2,7 @@
 reference-DFS work and SIMD efficiency of every schedule.
 
     python scripts/profile_kernel.py --counts                 # work + efficiency table
-    python scripts/profile_kernel.py --trav 2 --fast 1 --depth 5 --frames 5 [--opt 7=0]  # frames to profile
+    python scripts/profile_kernel.py --trav 1 --fast 1 --depth 5 --frames 5 [--opt 7=0]  # frames to profile
 """
 import argparse
 import importlib
@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--scene", default="render10000")
     ap.add_argument("--W", type=int, default=1920)
     ap.add_argument("--H", type=int, default=1080)
-    ap.add_argument("--trav", type=int, default=abi.TRAV_HYBRID)
+    ap.add_argument("--trav", type=int, default=abi.TRAV_WAVEFRONT)
     ap.add_argument("--fast", type=int, default=1)
     ap.add_argument("--depth", type=int, default=5)
     ap.add_argument("--frames", type=int, default=3)
@@ -36,7 +36,7 @@ def main():
     cam = mirt.default_camera()
     if a.counts:
         for depth in (1, 5):
-            for trav in (abi.TRAV_UNIFORM, abi.TRAV_LANE, abi.TRAV_HYBRID):
+            for trav in (abi.TRAV_TILE,):
                 r.set_option(abi.OPT_TRAVERSAL, trav)
                 c = r.count_frame(cam, a.W, a.H, depth=depth)
                 c.update(scene=a.scene, depth=depth, trav=trav,

@@ -54,7 +54,7 @@ def main():
     r.upload(s, b)
     cam = mirt.default_camera()
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    configs = [(1, abi.TRAV_UNIFORM, 0), (1, abi.TRAV_UNIFORM, 1)]
+    configs = [(1, abi.TRAV_TILE, 0), (1, abi.TRAV_TILE, 1)]
     if len(sys.argv) > 1:   # depth,trav,ordered ...
         configs = [tuple(int(v) for v in a.split(",")) for a in sys.argv[1:]]
     for depth, trav, ordered in configs:
