@@ -106,6 +106,7 @@ SIGNATURES = [
     ("mirt_bvh_flatten", I, [P, P, P, I]),
     ("mirt_bvh_build_flat", I, [P, I, I, I, C.POINTER(P), C.POINTER(I)]),
     ("mirt_bvh_free_flat", None, [P]),
+    ("mirt_bvh_validate_flat", I, [P, I, I]),
     ("mirt_bvh_build_flat_cached", I, [C.c_char_p, P, I, I, I, C.POINTER(P), C.POINTER(I), C.POINTER(I)]),
     ("mirt_create", I, [I, C.POINTER(P)]),
     ("mirt_destroy", None, [P]),

@@ -32,6 +32,8 @@
 #include <cstring>
 #include <future>
 #include <memory>
+#include <new>
+#include <system_error>
 #include <vector>
 
 #include "internal.h"
@@ -224,9 +226,14 @@ struct FlatBuilder {
             l->s = r->s = s;
             l->par = r->par = par - 1;
             FlatBuilder *lp = l.get(), *rp = r.get();
-            auto fl = std::async(std::launch::async, [=] { lp->run(lo, mid, depth + 1); });
+            std::future<void> fl;
+            try {
+                fl = std::async(std::launch::async, [=] { lp->run(lo, mid, depth + 1); });
+            } catch (const std::system_error&) {  // no thread to be had: build it here, same bits
+                lp->run(lo, mid, depth + 1);
+            }
             rp->run(mid, hi, depth + 1);
-            fl.get();
+            if (fl.valid()) fl.get();
             for (auto* k : {&l, &r}) {
                 mirt_node mk{};
                 mk.sphere = -2 - (int32_t)kids.size();
@@ -244,6 +251,15 @@ struct FlatBuilder {
     }
 };
 
+void free_tree(mirt_bvh_node* node)  // benchmark.c:81-88
+{
+    if (!node) return;
+    free_tree(node->left);
+    free_tree(node->right);
+    std::free(node);
+}
+
+// nullptr if a malloc failed (every node allocated so far is freed)
 mirt_bvh_node* to_pointer_tree(const std::vector<mirt_node>& f, const std::vector<int32_t>& counts,
                                mirt_sphere* base, int& i)
 {
@@ -252,15 +268,19 @@ mirt_bvh_node* to_pointer_tree(const std::vector<mirt_node>& f, const std::vecto
     if (!n) return nullptr;
     n->bounds.min = {f[me].bmin[0], f[me].bmin[1], f[me].bmin[2]};
     n->bounds.max = {f[me].bmax[0], f[me].bmax[1], f[me].bmax[2]};
+    n->left = n->right = nullptr;
+    n->sphere = nullptr;
+    n->sphere_count = 0;
     if (f[me].sphere >= 0) {
-        n->left = n->right = nullptr;
         n->sphere = base + f[me].sphere;
         n->sphere_count = counts[me];
     } else {
         n->left = to_pointer_tree(f, counts, base, i);
-        n->right = to_pointer_tree(f, counts, base, i);
-        n->sphere = nullptr;
-        n->sphere_count = 0;
+        n->right = n->left ? to_pointer_tree(f, counts, base, i) : nullptr;
+        if (!n->right) {
+            free_tree(n);
+            return nullptr;
+        }
     }
     return n;
 }
@@ -288,13 +308,61 @@ int flatten_rec(const mirt_bvh_node* n, const mirt_sphere* base, mirt_node* out,
     return at;
 }
 
+int set_nomem(const char* fn)
+{
+    mirt::set_error("%s: out of host memory", fn);
+    return MIRT_E_NOMEM;
+}
+
 }  // namespace
+
+namespace mirt {
+
+int validate_flat(const mirt_node* nd, int nn, int num_spheres, int sphere_lo, const char* fn)
+{
+    if (nn < 0 || (nn > 0 && !nd)) {
+        set_error("%s: invalid node array", fn);
+        return MIRT_E_INVALID;
+    }
+    if (nn == 0) return MIRT_OK;
+    if ((nd[0].skip & MIRT_SKIP_MASK) != (uint32_t)nn) {
+        set_error("%s: root skip %u != node count %d", fn, nd[0].skip & MIRT_SKIP_MASK, nn);
+        return MIRT_E_INVALID;
+    }
+    for (int i = 0; i < nn; i++) {
+        const uint32_t skip = nd[i].skip & MIRT_SKIP_MASK;
+        const bool leaf = nd[i].sphere >= 0;
+        const bool empty = (nd[i].skip & MIRT_NODE_EMPTY) != 0;
+        bool ok = skip > (uint32_t)i && skip <= (uint32_t)nn && nd[i].sphere >= -1 && nd[i].sphere <= num_spheres &&
+                  (!leaf || nd[i].sphere >= sphere_lo) && (!empty || leaf);
+        if (ok && leaf) {
+            ok = skip == (uint32_t)i + 1;
+        } else if (ok) {
+            // inner: left child i+1, right child r = the left subtree's end;
+            // both subtrees nest exactly inside (i, skip)
+            const uint32_t r = (uint32_t)i + 1 < skip ? nd[i + 1].skip & MIRT_SKIP_MASK : 0u;
+            ok = (uint32_t)i + 1 < skip && r > (uint32_t)i + 1 && r < skip && (nd[r].skip & MIRT_SKIP_MASK) == skip;
+        }
+        if (!ok) {
+            set_error("%s: malformed node %d (sphere %d, skip %u)", fn, i, nd[i].sphere, skip);
+            return MIRT_E_INVALID;
+        }
+    }
+    return MIRT_OK;
+}
+
+}  // namespace mirt
 
 extern "C" {
 
+int mirt_bvh_validate_flat(const mirt_node* nodes, int num_nodes, int num_spheres)
+{
+    return mirt::validate_flat(nodes, num_nodes, num_spheres, 0, "mirt_bvh_validate_flat");
+}
+
 int mirt_bvh_build_flat(mirt_sphere* spheres, int start, int end, int depth, mirt_node** out_nodes,
                         int* out_count)
-{
+try {
     if (!spheres || !out_nodes || !out_count || start < 0 || end < start) {
         mirt::set_error("mirt_bvh_build_flat: invalid arguments");
         return MIRT_E_INVALID;
@@ -312,12 +380,14 @@ int mirt_bvh_build_flat(mirt_sphere* spheres, int start, int end, int depth, mir
     *out_nodes = out;
     *out_count = (int)b.total;
     return MIRT_OK;
+} catch (const std::bad_alloc&) {
+    return set_nomem("mirt_bvh_build_flat");
 }
 
 void mirt_bvh_free_flat(mirt_node* nodes) { std::free(nodes); }
 
 mirt_bvh_node* mirt_build_bvh_node(mirt_sphere* spheres, int start, int end, int depth)
-{
+try {
     if (!spheres || start < 0 || end < start) {
         mirt::set_error("mirt_build_bvh_node: invalid arguments");
         return nullptr;
@@ -329,16 +399,15 @@ mirt_bvh_node* mirt_build_bvh_node(mirt_sphere* spheres, int start, int end, int
     std::vector<int32_t> counts;
     const std::vector<mirt_node> flat = b.flat(&counts);
     int i = 0;
-    return to_pointer_tree(flat, counts, spheres, i);
+    mirt_bvh_node* root = to_pointer_tree(flat, counts, spheres, i);
+    if (!root) set_nomem("mirt_build_bvh_node");
+    return root;
+} catch (const std::bad_alloc&) {
+    set_nomem("mirt_build_bvh_node");
+    return nullptr;
 }
 
-void mirt_free_bvh(mirt_bvh_node* node)  // benchmark.c:81-88
-{
-    if (!node) return;
-    mirt_free_bvh(node->left);
-    mirt_free_bvh(node->right);
-    std::free(node);
-}
+void mirt_free_bvh(mirt_bvh_node* node) { free_tree(node); }
 
 int mirt_bvh_count(const mirt_bvh_node* root) { return count_tree(root); }
 

@@ -15,13 +15,15 @@
 //   uint64_t payload      the same hash over the stored spheres and nodes
 //   mirt_sphere[end-start]  spheres[start,end) as the build left them
 //   mirt_node[num_nodes]
-// A file whose header, key or payload hash does not match is ignored and
-// rewritten; writes go to "<path>.tmp.<pid>" and are renamed into place, so a
+// A file whose header, key or payload hash does not match, whose tree is not
+// well formed (mirt_bvh_validate_flat) or whose spheres are not a permutation
+// of the input is ignored and rewritten; writes go to "<path>.tmp.<pid>" and are renamed into place, so a
 // reader never sees a half-written file.
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -69,11 +71,28 @@ uint64_t input_key(const mirt_sphere* s, int start, int end, int depth)
     return f.h;
 }
 
+// Order-independent hash of a sphere array (sum of a 64-bit mix of each
+// record): equal for a permutation, so a cached array must hold exactly the
+// input's spheres.
+uint64_t multiset_hash(const mirt_sphere* s, size_t n)
+{
+    uint64_t sum = 0;
+    for (size_t i = 0; i < n; i++) {
+        Fnv f;
+        f.add(s + i, sizeof(mirt_sphere));
+        uint64_t z = f.h + 0x9e3779b97f4a7c15ull;  // splitmix64 finaliser
+        z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+        z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+        sum += z ^ (z >> 31);
+    }
+    return sum;
+}
+
 // Loads the file into `sph` (end-start spheres) and a malloc'd node array if
 // it is a valid cache entry for `key`; returns false otherwise, touching
 // nothing the caller owns.
-bool try_load(const char* path, uint64_t key, int start, int end, int depth, std::vector<mirt_sphere>& sph,
-              mirt_node** nodes, int* count)
+bool try_load(const char* path, const mirt_sphere* input, uint64_t key, int start, int end, int depth,
+              std::vector<mirt_sphere>& sph, mirt_node** nodes, int* count)
 {
     FILE* f = std::fopen(path, "rb");
     if (!f) return false;
@@ -96,6 +115,10 @@ bool try_load(const char* path, uint64_t key, int start, int end, int depth, std
         p.add(nd, (size_t)h.num_nodes * sizeof(mirt_node));
         ok = p.h == h.payload;
     }
+    // the payload hash has no secret: also require a tree the uploads accept
+    // (leaves index spheres[start, end]) over a permutation of the input
+    ok = ok && mirt::validate_flat(nd, h.num_nodes, end, start, "cache") == MIRT_OK &&
+         multiset_hash(sph.data(), sph.size()) == multiset_hash(input + start, (size_t)(end - start));
     if (!ok) {
         std::free(nd);
         return false;
@@ -144,14 +167,14 @@ extern "C" {
 
 int mirt_bvh_build_flat_cached(const char* path, mirt_sphere* spheres, int start, int end, int depth,
                                mirt_node** out_nodes, int* out_count, int* out_cached)
-{
+try {
     if (!path || !spheres || !out_nodes || !out_count || start < 0 || end < start) {
         mirt::set_error("mirt_bvh_build_flat_cached: invalid arguments");
         return MIRT_E_INVALID;
     }
     const uint64_t key = input_key(spheres, start, end, depth);
     std::vector<mirt_sphere> sph;
-    if (try_load(path, key, start, end, depth, sph, out_nodes, out_count)) {
+    if (try_load(path, spheres, key, start, end, depth, sph, out_nodes, out_count)) {
         std::memcpy(spheres + start, sph.data(), sph.size() * sizeof(mirt_sphere));
         if (out_cached) *out_cached = 1;
         return MIRT_OK;
@@ -161,6 +184,9 @@ int mirt_bvh_build_flat_cached(const char* path, mirt_sphere* spheres, int start
     const bool saved = save(path, key, start, end, depth, spheres + start, *out_nodes, *out_count);
     if (out_cached) *out_cached = saved ? 0 : -1;
     return MIRT_OK;
+} catch (const std::bad_alloc&) {
+    mirt::set_error("mirt_bvh_build_flat_cached: out of host memory");
+    return MIRT_E_NOMEM;
 }
 
 }  // extern "C"

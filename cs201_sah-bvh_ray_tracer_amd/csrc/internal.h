@@ -15,4 +15,11 @@ void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
 int shard_row_count(const mirt_frame_desc* fd);
 bool frame_desc_valid(const mirt_frame_desc* fd);
 
+// A well-formed flat pre-order tree (mirt_node): root skip == nn; every skip
+// in (i, nn]; leaves skip to i + 1 and index spheres in [sphere_lo,
+// num_spheres] (num_spheres: the never-hit sentinel); the empty flag only on
+// leaves; every inner node's two subtrees [i+1, r) and [r, skip) nest inside
+// it. MIRT_OK or MIRT_E_INVALID with the message prefixed by `fn`.
+int validate_flat(const mirt_node* nd, int nn, int num_spheres, int sphere_lo, const char* fn);
+
 }  // namespace mirt

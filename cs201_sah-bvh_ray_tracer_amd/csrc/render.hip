@@ -11,6 +11,7 @@
 #include <cstdint>
 #include <algorithm>
 #include <cstring>
+#include <new>
 #include <vector>
 
 #include "internal.h"
@@ -809,6 +810,11 @@ struct mirt_ctx {
     // wavefront phase boundaries of the last frame (any API)
     hipEvent_t ph0 = nullptr, ph1 = nullptr, ph2 = nullptr;
     bool phases_valid = false;
+    // the frame scratch (queue, deferral list, phase events) is per ctx: a
+    // launch on another stream than the previous one waits for it
+    hipEvent_t done = nullptr;
+    hipStream_t last_stream = nullptr;
+    bool launched = false;
     // scene (replicated per device, uploaded once)
     DNode* d_nodes = nullptr;
     mirt_node* d_nodes32 = nullptr;
@@ -1096,8 +1102,23 @@ void dispatch_render(bool fast, const DevScene& sc, const FrameConst& f, uint32_
         render_kernel<false, COUNT><<<blocks + dfr.blocks, 64 * bw, 0, s>>>(sc, f, d_out, d_acc, d_counts, d_ws, dfr);
 }
 
+int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_acc, hipStream_t s, bool timed,
+                       mirt_counts* d_counts, uint32_t* d_wave_stats, uint64_t* d_bdiag);
+
 int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_acc, hipStream_t s, bool timed,
                   mirt_counts* d_counts, uint32_t* d_wave_stats = nullptr, uint64_t* d_bdiag = nullptr)
+{
+    if (c->launched && c->last_stream != s) HIP_TRY(hipStreamWaitEvent(s, c->done, 0));
+    const int rc = launch_render_body(c, f, d_out, d_acc, s, timed, d_counts, d_wave_stats, d_bdiag);
+    if (rc) return rc;
+    HIP_TRY(hipEventRecord(c->done, s));
+    c->last_stream = s;
+    c->launched = true;
+    return MIRT_OK;
+}
+
+int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_acc, hipStream_t s, bool timed,
+                       mirt_counts* d_counts, uint32_t* d_wave_stats, uint64_t* d_bdiag)
 {
     const int tiles = ((f.width + 7) / 8) * ((f.num_rows + 7) / 8);
     const int bw = c->block_waves;
@@ -1224,7 +1245,11 @@ int mirt_create(int device, mirt_ctx** out)
         return MIRT_E_INVALID;
     }
     HIP_TRY(hipSetDevice(device));
-    mirt_ctx* c = new mirt_ctx();
+    mirt_ctx* c = new (std::nothrow) mirt_ctx();
+    if (!c) {
+        set_error("mirt_create: out of host memory");
+        return MIRT_E_NOMEM;
+    }
     c->device = device;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&c->ev0);
@@ -1232,6 +1257,7 @@ int mirt_create(int device, mirt_ctx** out)
     if (e == hipSuccess) e = hipEventCreate(&c->ph0);
     if (e == hipSuccess) e = hipEventCreate(&c->ph1);
     if (e == hipSuccess) e = hipEventCreate(&c->ph2);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipMalloc((void**)&c->d_counts, sizeof(mirt_counts));
     if (e == hipSuccess) {
         int cus = 0, per_cu = 0;
@@ -1260,33 +1286,22 @@ void mirt_destroy(mirt_ctx* c)
         if (p) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
-    for (hipEvent_t ev : {c->ph0, c->ph1, c->ph2})
+    for (hipEvent_t ev : {c->ph0, c->ph1, c->ph2, c->done})
         if (ev) (void)hipEventDestroy(ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
 
 int mirt_scene_upload_flat(mirt_ctx* c, const mirt_sphere* spheres, int ns, const mirt_node* nodes, int nn)
-{
+try {
     if (!ctx_ok(c, false, "mirt_scene_upload_flat")) return MIRT_E_INVALID;
     if (ns < 0 || nn < 0 || (ns > 0 && !spheres) || (nn > 0 && !nodes)) {
         set_error("mirt_scene_upload_flat: invalid arguments");
         return MIRT_E_INVALID;
     }
-    // validate the tree so a malformed one cannot send the kernel out of bounds
-    for (int i = 0; i < nn; i++) {
-        const uint32_t skip = nodes[i].skip & MIRT_SKIP_MASK;
-        const bool leaf = nodes[i].sphere >= 0;
-        if (skip <= (uint32_t)i || skip > (uint32_t)nn || nodes[i].sphere > ns || nodes[i].sphere < -1 ||
-            (leaf && skip != (uint32_t)i + 1) || (!leaf && i + 1 >= nn)) {
-            set_error("mirt_scene_upload_flat: malformed node %d", i);
-            return MIRT_E_INVALID;
-        }
-    }
-    if (nn > 0 && (nodes[0].skip & MIRT_SKIP_MASK) != (uint32_t)nn) {
-        set_error("mirt_scene_upload_flat: root skip %u != node count %d", nodes[0].skip & MIRT_SKIP_MASK, nn);
-        return MIRT_E_INVALID;
-    }
+    // a malformed tree must not send the host layout builders or the kernels
+    // out of bounds
+    if (int rc = validate_flat(nodes, nn, ns, 0, "mirt_scene_upload_flat")) return rc;
     float r_max = 0.0f, c_max = 0.0f;
     const bool encloses = tree_encloses(spheres, ns, nodes, nn, &r_max, &c_max);
     std::vector<float4> geo((size_t)ns + 1);
@@ -1350,10 +1365,13 @@ int mirt_scene_upload_flat(mirt_ctx* c, const mirt_sphere* spheres, int ns, cons
     c->r_max = r_max;
     c->c_max = c_max;
     return MIRT_OK;
+} catch (const std::bad_alloc&) {
+    set_error("mirt_scene_upload_flat: out of host memory");
+    return MIRT_E_NOMEM;
 }
 
 int mirt_scene_upload(mirt_ctx* c, const mirt_sphere* spheres, int ns, const mirt_bvh_node* root)
-{
+try {
     if (!root) return mirt_scene_upload_flat(c, spheres, ns, nullptr, 0);
     const int nn = mirt_bvh_count(root);
     std::vector<mirt_node> flat((size_t)nn);
@@ -1362,6 +1380,9 @@ int mirt_scene_upload(mirt_ctx* c, const mirt_sphere* spheres, int ns, const mir
         return MIRT_E_INVALID;
     }
     return mirt_scene_upload_flat(c, spheres, ns, flat.data(), nn);
+} catch (const std::bad_alloc&) {
+    set_error("mirt_scene_upload: out of host memory");
+    return MIRT_E_NOMEM;
 }
 
 int mirt_render_frame_device(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, uint32_t* d_out,

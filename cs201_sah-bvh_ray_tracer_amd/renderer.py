@@ -105,6 +105,14 @@ def build_bvh(spheres, start=0, end=None, depth=0):
     return Bvh(nodes)
 
 
+def validate_bvh(nodes, num_spheres):
+    """mirt_bvh_validate_flat: raises MirtError unless `nodes` (abi.NODE) is a
+    well-formed flat pre-order tree over num_spheres spheres."""
+    nodes = np.ascontiguousarray(nodes, dtype=abi.NODE)
+    check(load().mirt_bvh_validate_flat(ptr(nodes) if len(nodes) else None, len(nodes), num_spheres),
+          "mirt_bvh_validate_flat")
+
+
 def build_bvh_cached(path, spheres, start=0, end=None, depth=0):
     """build_bvh through a flattened-tree cache file (mirt_bvh_build_flat_cached):
     returns (Bvh, cached) with cached 1 = loaded from `path`, 0 = built and

@@ -181,6 +181,14 @@ int mirt_bvh_flatten(const mirt_bvh_node *root, const mirt_sphere *base, mirt_no
 int mirt_bvh_build_flat(mirt_sphere *spheres, int start, int end, int depth,
                         mirt_node **out_nodes, int *out_count);
 void mirt_bvh_free_flat(mirt_node *nodes);
+/* Check that nodes[0, num_nodes) is a well-formed flat pre-order tree over
+   num_spheres spheres: root skip == num_nodes, every skip in (i, num_nodes],
+   leaves skip to i + 1 and index spheres in [0, num_spheres] (num_spheres =
+   the never-hit sentinel), MIRT_NODE_EMPTY only on leaves, and every inner
+   node's two subtrees [i+1, r) and [r, skip) nest exactly inside it.
+   MIRT_OK or MIRT_E_INVALID (mirt_last_error names the first bad node). The
+   uploads run this check; it never touches the GPU. */
+int mirt_bvh_validate_flat(const mirt_node *nodes, int num_nodes, int num_spheres);
 /* mirt_bvh_build_flat through a flattened-tree cache file (SURVEY.md §8(f)
    rank 3; replaces the build_bvh_node call at main.c:225 / benchmark.c:317 on
    a rerun). If `path` holds the tree of exactly these input spheres
@@ -222,7 +230,11 @@ int mirt_render_frame(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_de
    j's slab at j * num_rows * width). d_accum is a device float buffer of
    num_rows * width * 3 (may be NULL when fd->accumulate == 0); given with
    samples > 1, the frames are folded into it and slab 0 receives the display
-   after the last. Inputs are already resident in HBM. */
+   after the last. Inputs are already resident in HBM. The ctx's frame scratch
+   (bounce queue, deferral list) is one per ctx: a launch on a different
+   stream than the ctx's previous launch first waits for that launch (an
+   event), so frames of one ctx never overlap; use one ctx per stream for
+   frames in flight. */
 int mirt_render_frame_device(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_desc *fd,
                              uint32_t *d_out, float *d_accum, void *stream);
 

@@ -217,3 +217,91 @@ def test_tree_cache_file(mirt, small, tmp_path):
     b, cached = mirt.build_bvh_cached(tmp_path / "no_such_dir" / "x.bvh", s)
     assert cached == -1 and b.nodes.tobytes() == small["render_1000_1_tree"].tobytes()
     assert not list(tmp_path.glob("*.tmp.*"))
+
+
+def _node(sphere, skip, lo=(0, 0, 0), hi=(1, 1, 1)):
+    return (lo, hi, sphere, skip)
+
+
+def test_validate_flat_tree(mirt, small):
+    """mirt_bvh_validate_flat (run by both uploads and the cache loader)
+    accepts the reference's trees and rejects every malformed shape that
+    could send the layout builders or kernels out of bounds."""
+    abi = mirt.abi
+    for key in ("render_1000_1_tree", "bench_1000_1_tree"):
+        mirt.validate_bvh(small[key], 1000)
+    mirt.validate_bvh(np.zeros(0, abi.NODE), 0)
+    E = abi.NODE_EMPTY
+    bad = {
+        # ADVICE r1: inner node whose right child is the end of the array
+        "right_child_at_end": [_node(-1, 2), _node(0, 2)],
+        "truncated": [_node(-1, 3), _node(0, 2), _node(1, 3)][:2],
+        "root_skip": [_node(-1, 3), _node(0, 2), _node(1, 3), _node(2, 4)],
+        "leaf_skip": [_node(-1, 3), _node(0, 3), _node(1, 3)],
+        "not_nested": [_node(-1, 5), _node(-1, 4), _node(0, 3), _node(1, 4), _node(2, 6), _node(3, 6)][:5],
+        "right_overruns": [_node(-1, 4), _node(-1, 3), _node(0, 3), _node(1, 5), _node(2, 5)],
+        "sphere_range": [_node(-1, 3), _node(0, 2), _node(7, 3)],
+        "bad_sphere": [_node(-1, 3), _node(0, 2), _node(-5, 3)],
+        "empty_inner": [_node(-1, 3 | E), _node(0, 2), _node(1, 3)],
+        "skip_backwards": [_node(-1, 3), _node(0, 0), _node(1, 3)],
+    }
+    for name, rows in bad.items():
+        arr = np.array(rows, dtype=abi.NODE)
+        with pytest.raises(mirt.MirtError):
+            mirt.validate_bvh(arr, 3)
+            raise AssertionError(name)
+    ok = np.array([_node(-1, 3), _node(0, 2), _node(3, 3 | E)], dtype=abi.NODE)   # sentinel + empty leaf
+    mirt.validate_bvh(ok, 3)
+
+
+def _fnv_words(h, b):
+    n8 = len(b) // 8 * 8
+    for w in np.frombuffer(b[:n8], dtype="<u8").tolist():
+        h = ((h ^ w) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    for c in b[n8:]:
+        h = ((h ^ c) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def test_tree_cache_rejects_forged_files(mirt, small, tmp_path):
+    """The cache hashes carry no secret: a file rewritten with a
+    recomputed payload hash but a malformed tree, or spheres that are not a
+    permutation of the input, is treated as a miss and rebuilt."""
+    import struct
+    path = tmp_path / "scene.bvh"
+    s = small["render_1000_1_pre"].copy()
+    mirt.build_bvh_cached(path, s)
+    raw = bytearray(path.read_bytes())
+    hdr, body = raw[:48], raw[48:]
+    ns = 1000
+    sph = np.frombuffer(bytes(body[:20 * ns]), dtype=mirt.abi.SPHERE).copy()
+    nodes = np.frombuffer(bytes(body[20 * ns:]), dtype=mirt.abi.NODE).copy()
+
+    def forge(sph2, nodes2):
+        payload = _fnv_words(1469598103934665603, sph2.tobytes() + nodes2.tobytes())
+        h = bytes(hdr[:40]) + struct.pack("<Q", payload)
+        path.write_bytes(h + sph2.tobytes() + nodes2.tobytes())
+
+    # 1. an inner node's right child pointed past its parent's subtree
+    n2 = nodes.copy()
+    inner = np.nonzero(n2["sphere"] < 0)[0]
+    n2["skip"][inner[3] + 1] = len(n2)          # left child's subtree "ends" at the array end
+    forge(sph, n2)
+    s = small["render_1000_1_pre"].copy()
+    b, cached = mirt.build_bvh_cached(path, s)
+    assert cached == 0 and b.nodes.tobytes() == small["render_1000_1_tree"].tobytes()
+    # 2. a leaf index out of range
+    n2 = nodes.copy()
+    n2["sphere"][np.nonzero(n2["sphere"] >= 0)[0][5]] = 5000
+    forge(sph, n2)
+    s = small["render_1000_1_pre"].copy()
+    assert mirt.build_bvh_cached(path, s)[1] == 0
+    # 3. spheres that are not a permutation of the input
+    s2 = sph.copy()
+    s2["radius"][17] += 1.0
+    forge(s2, nodes)
+    s = small["render_1000_1_pre"].copy()
+    assert mirt.build_bvh_cached(path, s)[1] == 0
+    assert s.tobytes() == small["render_1000_1_post"].tobytes()
+    # the genuine file still hits
+    assert mirt.build_bvh_cached(path, small["render_1000_1_pre"].copy())[1] == 1
