@@ -6,6 +6,10 @@ MAX_DEPTH, main.c:19/366) -> RGBA8 framebuffer.
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...     (N > 1)
 
+`python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment
+starts the N rank processes itself (one per GPU, MASTER_ADDR 127.0.0.1); the
+parent never touches the GPU and exits with the worst rank's status.
+
 One step at N GPUs = N successive frames of the reference's accumulating
 display loop (main.c:379-408: the camera holds still, frame j adds RNG sample
 j), each 1920x1080 at 1 primary ray per pixel: every rank renders its
@@ -13,24 +17,38 @@ interleaved 8-row blocks of all N frames in ONE launch into its HBM slabs
 (scene resident, uploaded once), folds them into its accumulation buffer on
 the device, and for N > 1 the displayed slabs are gathered to rank 0 over
 RCCL and de-interleaved there. Per-GPU work is one frame's worth of rays
-whatever N is ("scaling": "weak"); `--scaling strong` instead splits ONE
-frame over the N ranks (its per-GPU launch shrinks with N until the bounce
-pass's longest chains set the time). value = W*H primary rays per frame *
-frames per step * K / (max over ranks of the timed region). Rank 0 prints
-one JSON line.
+whatever N is ("scaling": "weak"). At N > 1 the line also carries
+`value_strong`: ONE frame split N ways per step, timed the same way (its
+per-GPU launch shrinks with N until the bounce pass's longest chains set the
+time); `--scaling strong` makes that the headline. value = W*H primary rays
+per frame * frames per step * K / (max over ranks of the timed region).
 
 Successive steps are triple-buffered (`--pipeline 3`, default): three device
 contexts with the scene resident in each take turns on their own streams, so
 step k + 1's launches fill the CU slots that step k's bounce pass frees while
-its last chains drain (measured: 1.73 ms per frame serial, 1.38 / 1.33 /
-1.30 ms with 2 / 3 / 4 contexts). Each frame is still rendered whole and
-its bytes do not change; only the gap between frames closes. The timed
-region still brackets all K steps (barrier + synchronize on both sides).
+its last chains drain. Each frame is still rendered whole and its bytes do
+not change; only the gap between frames closes. The timed region brackets all
+K steps (barrier + synchronize on both sides).
+
+Also in the line (N = 1): `host_inclusive_mrays_s`, SURVEY §8(d)'s t_frame
+(call -> RGBA8 frame in host memory): the same three contexts, each frame's
+D2H copy into page-locked memory enqueued behind its kernels
+(mirt_render_frame_async) so it overlaps the next frame; the blocking
+single-call rate into pageable memory beside it. `roofline`: the dominant
+kernel (the bounce pass) priced per §8(d) plus the bound the PMC counters
+measured (profiles/r02_pmc_bound.json). `cpu_baseline`: the unmodified
+reference sources (oracle/_ref) on this host's cores.
+
+`--dry` (CPU only, gloo): the same launcher, shard geometry, gather and
+max-over-ranks timing with a synthetic slab in place of the GPU frame --
+a plumbing check for CPU tests; its line says "dry": true and is no measurement.
 """
 import argparse
 import importlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -43,6 +61,7 @@ sys.path.insert(0, ROOT)
 mirt = importlib.import_module("cs201_sah-bvh_ray_tracer_amd")
 shard = importlib.import_module("cs201_sah-bvh_ray_tracer_amd.shard")
 
+METRIC = "Mrays/s at 1080p, 10k spheres; 1/2/4/8 GPU + CPU baseline"
 W, H, NSPH, DEPTH, SEED, ROW_BLOCK = 1920, 1080, 10000, 5, 1, 8
 KIND, SPP, JITTER = "render", 1, False
 # --workload: BASELINE.json configs (the default is configs[1], the metric's
@@ -61,13 +80,15 @@ WORKLOADS = {
                             "4 spp jittered, depth 5 (BASELINE configs[4])"),
 }
 PEAK_HBM_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+PEAK_L2_GBS = 34500.0   # aggregate L2 (MI355X_MICROARCH.md §L2)
 NODE_B, SPHERE_B, COLOR_B, PIXEL_B = 32, 16, 4, 4
 KERNEL = "bounce_kernel<true, 2, false>"   # dominant kernel of the default (wavefront, four-wide) schedule
+PMC_BOUND = os.path.join(ROOT, "profiles", "r02_pmc_bound.json")
 
 
 def algorithmic_bytes(c, pixels):
-    """per frame, sum over traced rays of 32 B per reference-DFS
-    node test + 16 B per sphere test, 4 B per hit colour, 4 B per pixel written."""
+    """per frame, sum over traced rays of 32 B per node test +
+    16 B per sphere test, 4 B per hit colour, 4 B per pixel written."""
     return NODE_B * c["nodes"] + SPHERE_B * c["spheres"] + COLOR_B * c["hits"] + PIXEL_B * pixels
 
 
@@ -79,88 +100,225 @@ def bounce_bytes(c):
             + COLOR_B * (c["hits"] - c["hits_primary"]) + PIXEL_B * c["hits_primary"])
 
 
-def cpu_baseline(target_s=12.0):
+# ------------------------------------------------------------------ CPU leg
+
+def host_cpu():
+    """nproc, the affinity mask's size and the CPU model of this host."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "model": model,
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+
+
+def cpu_threads():
+    """Threads for the all-core leg: the box's CPU share where the environment
+    states it (OMP_NUM_THREADS: the GPU box sets it to its 16-CPU share,
+    while nproc there reports the whole machine), else the affinity mask."""
+    aff = len(os.sched_getaffinity(0))
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        return min(int(env), aff), "OMP_NUM_THREADS"
+    return aff, "sched_getaffinity"
+
+
+def cpu_baseline(target_s=10.0):
     """The reference render path on this host's cores: oracle/_ref (the
     unmodified reference sources compiled in-tree) if present, else the
-    oracle restatement. Bounded sample: evenly spaced rows of the same
-    frame, stride chosen so the run takes ~target_s."""
+    oracle restatement. Bounded samples of the same frame: evenly spaced
+    rows, stride chosen so each leg takes about its budget.
+      value              all threads, -O2 (SURVEY §8(d) CPU baseline (b))
+      single_core_value  one thread, -O2 ((a))
+      O0_single_core     one thread, the reference's own flags (Makefile:3,43: no -O, -g)
+      config0            BASELINE configs[0]: 640x480, 100 spheres, depth 5, BVH on, full frames"""
     from oracle.lib import Oracle, Reference
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
-    try:
-        ref = Reference(W, H)
-        kind = "reference"
-    except (FileNotFoundError, OSError):
-        ref, kind = None, "port"
+    threads, source = cpu_threads()
     o = Oracle()
-    # same scene (bit-identical generator), same tree ([0, N), depth 0)
-    s = o.render_scene(SEED, NSPH) if KIND == "render" else o.bench_scene(SEED, NSPH)
-    cam = mirt.default_camera()
-    if ref is not None:
-        s_ref = s.copy()
-        tree = ref.build(s_ref)
 
-        def run(step, nthreads):
-            t0 = time.perf_counter()
-            img = ref.render(cam, s_ref, tree, depth=DEPTH, mode=1, seed=SEED, row0=0, step=step,
-                             threads=nthreads, jitter=JITTER)
-            return time.perf_counter() - t0, img.shape[0]
-    else:
-        tree = o.build(s)
+    def make(Wc, Hc, nsph, kind, opt="O2"):
+        try:
+            ref = Reference(Wc, Hc, opt)
+            k = "reference"
+        except (FileNotFoundError, OSError):
+            if opt != "O2":
+                return None
+            ref, k = None, "port"
+        s = o.render_scene(SEED, nsph) if kind == "render" else o.bench_scene(SEED, nsph)
+        cam = mirt.default_camera()
+        if ref is not None:
+            tree = ref.build(s)
 
-        def run(step, nthreads):
-            rows = np.arange(0, H, step, dtype=np.int32)
-            t0 = time.perf_counter()
-            o.render(cam, W, H, s, tree, depth=DEPTH, mode=1, seed=SEED, rows=rows, threads=nthreads, jitter=JITTER)
-            return time.perf_counter() - t0, len(rows)
+            def run(step, nthreads):
+                t0 = time.perf_counter()
+                img = ref.render(cam, s, tree, depth=DEPTH, mode=1, seed=SEED, row0=0, step=step,
+                                 threads=nthreads, jitter=JITTER)
+                return time.perf_counter() - t0, img.shape[0]
+            free = lambda: ref.free(tree)  # noqa: E731
+        else:
+            tree = o.build(s)
 
-    def sample(step, nthreads, budget):
-        # repeat the strided frame until the budget is spent (a fast host
-        # renders the whole frame in a few seconds)
+            def run(step, nthreads):
+                rows = np.arange(0, Hc, step, dtype=np.int32)
+                t0 = time.perf_counter()
+                o.render(cam, Wc, Hc, s, tree, depth=DEPTH, mode=1, seed=SEED, rows=rows, threads=nthreads,
+                         jitter=JITTER)
+                return time.perf_counter() - t0, len(rows)
+            free = lambda: o.free(tree)  # noqa: E731
+        return run, free, k
+
+    def sample(run, Wc, Hc, nthreads, budget):
+        probe_t, probe_rows = run(max(1, Hc // (2 * nthreads)), nthreads)   # ~2 rows per thread
+        per_row = probe_t / max(probe_rows, 1)
+        step = max(1, int(np.ceil(Hc * per_row / budget)))
         t = rows = reps = 0
-        while t < budget or reps == 0:
+        while t < 0.8 * budget or reps == 0:    # whole strided frames, repeated on a fast host
             dt, n = run(step, nthreads)
             t, rows, reps = t + dt, rows + n, reps + 1
-        return t, rows, reps
+        return {"value": round(rows * Wc / t / 1e6, 5), "step": step, "reps": reps, "rows": rows, "s": round(t, 2)}
 
-    probe_t, probe_rows = run(max(1, H // (2 * threads)), threads)   # ~2 rows per thread
-    per_row = probe_t / max(probe_rows, 1)
-    step = max(1, int(np.ceil(H * per_row / target_s)))
-    t, rows, reps = sample(step, threads, 0.8 * target_s)
-    value = rows * W / t / 1e6
-    step1 = max(step * threads, 1)                 # single core, same row density / threads
-    t1, rows1, reps1 = sample(step1, 1, 0.8 * target_s)
-    value1 = rows1 * W / t1 / 1e6
-    if ref is not None:
-        ref.free(tree)
-    else:
-        o.free(tree)
-    return {"value": round(value, 5), "unit": "Mrays/s", "cores": threads, "kind": kind,
-            "sample": f"every {step}th row of the {W}x{H} frame (sample 0{', jittered' if JITTER else ''}) x {reps} "
-                      f"({rows} rows, {rows * W} primary rays, depth {DEPTH}, {threads} OpenMP threads, "
-                      f"row-dynamic schedule) in {t:.1f} s",
-            "single_core_value": round(value1, 5),
-            "single_core_sample": f"every {step1}th row x {reps1} ({rows1} rows) in {t1:.1f} s"}
+    run, free, kind = make(W, H, NSPH, KIND)
+    multi = sample(run, W, H, threads, target_s)
+    single = sample(run, W, H, 1, target_s / 2)
+    free()
+    out = {"value": multi["value"], "unit": "Mrays/s", "cores": threads, "kind": kind,
+           "sample": f"every {multi['step']}th row of the {W}x{H} frame (sample 0{', jittered' if JITTER else ''}) "
+                     f"x {multi['reps']} ({multi['rows']} rows, {multi['rows'] * W} primary rays, depth {DEPTH}, "
+                     f"{threads} OpenMP threads [{source}], row-dynamic schedule, gcc -O2 -ffp-contract=off) "
+                     f"in {multi['s']} s",
+           "host": host_cpu(),
+           "single_core_value": single["value"],
+           "single_core_sample": f"every {single['step']}th row x {single['reps']} ({single['rows']} rows) "
+                                 f"in {single['s']} s, -O2"}
+    m0 = make(W, H, NSPH, KIND, "O0")
+    if m0 is not None:
+        run0, free0, _ = m0
+        s0 = sample(run0, W, H, 1, target_s / 2)
+        free0()
+        out["O0_single_core_value"] = s0["value"]
+        out["O0_single_core_sample"] = (f"every {s0['step']}th row x {s0['reps']} ({s0['rows']} rows) in {s0['s']} s, "
+                                        "the reference's own flags (-g, no -O: Makefile:3,43)")
+    # BASELINE configs[0]: 640x480, 100 random spheres, BVH on
+    cfg0 = {"workload": "640x480, 100 random spheres, BVH on, depth 5 (BASELINE configs[0])"}
+    for label, opt, nt in (("value", "O2", threads), ("single_core_value", "O2", 1), ("O0_single_core_value", "O0", 1)):
+        m = make(640, 480, 100, "render", opt)
+        if m is None:
+            continue
+        r_, f_, _ = m
+        cfg0[label] = sample(r_, 640, 480, nt, 2.0)["value"]
+        f_()
+    out["config0"] = cfg0
+    return out
 
 
-def load_traffic(kernel):
-    """Per-launch HBM bytes of the render kernel from the committed PMC
-    profile (profiles/pmc_render.json, written by scripts/collect_profiles.py
-    from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this bench), if
-    it was taken on this workload and kernel."""
-    p = os.path.join(ROOT, "profiles", "pmc_render.json")
-    if not os.path.exists(p):
+# ------------------------------------------------------------- launching
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """Start n copies of this script as ranks 0..n-1 (the torchrun contract's
+    environment) and wait; a failing rank ends the others. Runs before any
+    GPU call in this process."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def timed(world, steps, body):
+    """barrier + synchronize, `steps` bodies, synchronize + barrier; seconds."""
+    cuda = torch.cuda.is_initialized()
+    if world > 1:
+        dist.barrier()
+    if cuda:
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        body()
+    if cuda:
+        torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def dry_main(args, world, rank):
+    """CPU plumbing check: synthetic slabs through the shard geometry, the
+    gather and the timing of the GPU path (gloo)."""
+    if world > 1:
+        dist.init_process_group("gloo")
+    fd = mirt.frame_desc(W, H, depth=DEPTH, row_block=ROW_BLOCK, shard=rank, num_shards=world)
+    rows = mirt.shard_rows(fd)
+    slab = torch.zeros((shard.slab_rows(H, ROW_BLOCK, world), W), dtype=torch.int32)
+    slab[:len(rows)] = torch.from_numpy(rows.astype(np.int64)[:, None] * W + np.arange(W)).to(torch.int32)
+    frame = [None]
+
+    def step():
+        frame[0] = shard.gather_frame(slab, H, ROW_BLOCK) if world > 1 else shard.assemble(slab[None], H, ROW_BLOCK)
+
+    for _ in range(args.warmup):
+        step()
+    el = timed(world, args.steps, step)
+    t = torch.tensor([el], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        want = torch.arange(H * W, dtype=torch.int64).reshape(H, W).to(torch.int32)
+        ok = bool(torch.equal(frame[0], want))
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "Mrays/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": None, "higher_is_better": True,
+                          "scaling": args.scaling, "vs_baseline": None, "dtype": "f32", "dry": True,
+                          "data": "synthetic slabs (no rendering): launcher / gather plumbing check",
+                          "frame_assembled_ok": ok, "gather_ms_per_step": round(float(t[0]) / args.steps * 1e3, 4),
+                          "config": {"workload": WORKLOADS[args.workload]["desc"], "name": args.workload,
+                                     "parallelism": f"row-block shard x{world}" + (" + gloo gather" if world > 1 else "")}}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+# ------------------------------------------------------------------ main
+
+def load_pmc_bound():
+    """The PMC-derived bound of the frame kernels (profiles/r02_pmc_bound.json,
+    scripts/pmc_probe.sh + scripts/pmc_summary.py) for this workload."""
+    if not os.path.exists(PMC_BOUND):
         return None
-    with open(p) as f:
+    with open(PMC_BOUND) as f:
         d = json.load(f)
-    if d.get("workload") != [W, H, NSPH, DEPTH] or d.get("kernel") != kernel:
-        return None
-    return d.get("hbm_bytes_per_launch")
+    return d if d.get("workload") == [W, H, NSPH, DEPTH] else None
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-host", action="store_true", help="skip the host-inclusive (D2H) leg")
@@ -169,21 +327,27 @@ def main():
                     help="device contexts alternating successive steps on their own streams (1 = serial)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
                     help="weak: N frames in flight per step at N GPUs (default); strong: one frame split N ways")
+    ap.add_argument("--dry", action="store_true", help="CPU plumbing check over gloo (no GPU, no measurement)")
     args = ap.parse_args()
     global W, H, NSPH, KIND, SPP, JITTER
     wl = WORKLOADS[args.workload]
     W, H, NSPH, KIND, SPP, JITTER = wl["W"], wl["H"], wl["NSPH"], wl["KIND"], wl["SPP"], wl["JITTER"]
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}; measuring {world} rank(s)", file=sys.stderr)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if args.dry:
+        return dry_main(args, world, rank)
     if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
-    assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
 
     spheres = (mirt.create_random_spheres(NSPH, SEED) if KIND == "render"
                else mirt.create_benchmark_spheres(NSPH, SEED))
@@ -210,48 +374,39 @@ def main():
     ref_counts = r.count_frame(cam, W, H, depth=DEPTH, seed=SEED, row_block=ROW_BLOCK, shard=rank,
                                num_shards=world, samples=frames, jitter=JITTER)
     r.set_option(mirt.abi.OPT_PRUNE, 1)
-    alg_bytes = algorithmic_bytes(counts, my_rows * W * frames)
 
     # a non-default stream for the serial measurement loop below (the timed
-    # loop runs on the ShardedFrame's own streams when double-buffered)
+    # loop runs on the ShardedFrame's own streams when pipelined)
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
+
+    def step_fn(s, f):
+        def body():
+            s.render_local(cam, f)
+            if world > 1:
+                s.gather()          # N = 1: the slab is the frame
+        return body
+
+    body = step_fn(sf, fd)
     for _ in range(args.warmup):
-        sf.render_local(cam, fd)
-        if world > 1:
-            sf.gather()
-    torch.cuda.synchronize()
+        body()
+    elapsed = timed(world, args.steps, body)
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        sf.render_local(cam, fd)
-        if world > 1:
-            sf.gather()          # N = 1: the slab is the frame
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-
-    # depth 1 alongside (camera rays and their shading only),
-    # same pipeline, same step
-    fd1 = sf.desc(depth=1, seed=SEED, jitter=JITTER)
+    # depth 1 alongside (camera rays and their shading only)
+    body1 = step_fn(sf, sf.desc(depth=1, seed=SEED, jitter=JITTER))
     for _ in range(2):
-        sf.render_local(cam, fd1)
-    torch.cuda.synchronize()
+        body1()
+    elapsed_d1 = timed(world, args.steps, body1)
+
+    # the other scaling mode at N > 1 (same contexts, its own slabs)
+    elapsed_other, frames_other = None, None
     if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    for k in range(args.steps):
-        sf.render_local(cam, fd1)
-        if world > 1:
-            sf.gather()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed_d1 = time.perf_counter() - t1
+        frames_other = SPP * (1 if args.scaling == "weak" else world)
+        sf2 = shard.ShardedFrame(r, W, H, ROW_BLOCK, samples=frames_other, renderers=rs)
+        body2 = step_fn(sf2, sf2.desc(depth=DEPTH, seed=SEED, jitter=JITTER))
+        for _ in range(args.warmup):
+            body2()
+        elapsed_other = timed(world, args.steps, body2)
 
     # per-kernel split of the same launch, one context, serial (untimed loop:
     # each launch waits for its events): torch events around the launch and
@@ -259,7 +414,7 @@ def main():
     slabs = torch.zeros((frames, sf.rows, W), dtype=torch.int32, device="cuda")
     acc = torch.zeros((sf.rows, W, 3), dtype=torch.float32, device="cuda") if frames > 1 else None
     phases, launch = [], []
-    for _ in range(args.steps):
+    for _ in range(min(args.steps, 20)):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         r.render_frame_device(cam, fd, slabs.data_ptr(), acc.data_ptr() if acc is not None else None,
@@ -271,29 +426,28 @@ def main():
     primary_ms, bounce_ms = (float(v) for v in np.mean(np.array(phases), axis=0))
     kernel_ms = float(np.mean(launch))
 
-    t = torch.tensor([elapsed, kernel_ms, elapsed_d1], dtype=torch.float64, device="cuda")
+    t = torch.tensor([elapsed, kernel_ms, elapsed_d1, elapsed_other or 0.0], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kernel_ms_max, elapsed_d1 = float(t[0]), float(t[1]), float(t[2])
+    elapsed, kernel_ms_max, elapsed_d1, elapsed_other = (float(v) for v in t)
+
+    host = None
+    if rank == 0 and world == 1 and not args.no_host:
+        host = host_inclusive(rs, cam, args.steps)
 
     if rank == 0:
         value = W * H * frames * args.steps / elapsed / 1e6   # primary rays: W*H per sample
-        frame_gbs = alg_bytes / (kernel_ms / 1e3) / 1e9
-        b_bytes = bounce_bytes(counts)
-        achieved = b_bytes / (bounce_ms / 1e3) / 1e9
-        traffic = load_traffic(KERNEL) if world == 1 else None
-        # the same frame through the blocking host API (kernel + D2H over PCIe)
-        host = None
-        if world == 1 and not args.no_host:
-            img = r.render_frame(cam, W, H, depth=DEPTH, seed=SEED, samples=SPP, jitter=JITTER)
-            dts = []
-            for _ in range(11):   # median call: pageable-buffer page faults make single calls noisy
-                t1 = time.perf_counter()
-                img = r.render_frame(cam, W, H, depth=DEPTH, seed=SEED, samples=SPP, jitter=JITTER)
-                dts.append(time.perf_counter() - t1)
-            host = W * H * SPP / sorted(dts)[len(dts) // 2] / 1e6
+        pixels = my_rows * W * frames
+        ref_frame_bytes = algorithmic_bytes(ref_counts, pixels)
+        exec_frame_bytes = algorithmic_bytes(counts, pixels)
+        ref_b = bounce_bytes(ref_counts)
+        exec_b = bounce_bytes(counts)
+        achieved = ref_b / (bounce_ms / 1e3) / 1e9
+        pmc = load_pmc_bound() if world == 1 else None
+        pb = pmc["kernels"].get("t1_f1_d5/bounce", {}).get("derived", {}) if pmc else {}
+        traffic = pb.get("hbm_bytes")
         line = {
-            "metric": "Mrays/s at 1080p, 10k spheres; 1/2/4/8 GPU + CPU baseline",
+            "metric": METRIC,
             "value": round(value, 3),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -312,36 +466,107 @@ def main():
                        "row_block": ROW_BLOCK,
                        "parallelism": f"row-block shard x{world}" + (" + RCCL gather" if world > 1 else "")
                                       + (f", {frames} accumulated frames in flight" if frames > 1 else "")},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
-                         "kernel": KERNEL, "kernel_ms": round(bounce_ms, 4),
-                         "algorithmic_bytes_per_launch": int(b_bytes),
-                         "primary_kernel_ms": round(primary_ms, 4),
-                         "primary_algorithmic_bytes": int(alg_bytes - b_bytes),
-                         "frame_ms": round(kernel_ms, 4), "frame_algorithmic_bytes": int(alg_bytes),
-                         "frame_achieved": round(frame_gbs, 1),
-                         "frame_achieved_pipelined": round(alg_bytes / (elapsed / args.steps) / 1e9, 1),
-                         "note": "bytes of the node/sphere reads the (pruned) walk performs, per SURVEY 8(d) "
-                                 "unit costs; the tree is L2/MALL-resident, so frac measures the achieved "
-                                 "cache-fed rate against the HBM peak. kernel_ms / frame_ms: one launch alone "
-                                 "(serial loop); the timed loop overlaps successive launches (pipeline)"},
+            "roofline": {
+                "bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
+                "kernel": KERNEL, "kernel_ms": round(bounce_ms, 4),
+                "algorithmic_bytes_per_launch": int(ref_b),
+                "definition": "SURVEY 8(d): bytes of the REFERENCE's exhaustive DFS (hit.c:91-109, no pruning) "
+                              "for the bounce levels at 32 B/node test + 16 B/sphere test + 4 B/hit colour + "
+                              "4 B/pixel, / the bounce kernel's HIP-event time. The tree is L2/MALL-resident, so "
+                              "this effective rate exceeds the HBM peak by construction (frac > 1): it is not HBM "
+                              "use. Measured HBM use and the unit that does bound the kernel: hbm_measured, "
+                              "bound_measured.",
+                "hbm_measured": None if traffic is None else {
+                    "bytes_per_launch": traffic, "gbs": round(traffic / (bounce_ms / 1e3) / 1e9, 2),
+                    "frac": round(traffic / (bounce_ms / 1e3) / 1e9 / PEAK_HBM_GBS, 5)},
+                "bound_measured": None if not pb else {
+                    "unit": {"td_busy": "TD (vector-memory data return)", "ta_busy": "TA (vector-memory address)",
+                             "valu_busy": "VALU issue", "l2_frac_upper": "L2 bandwidth",
+                             "hbm_frac": "HBM bandwidth"}.get(pb.get("busiest_unit"), pb.get("busiest_unit")),
+                    "td_busy": pb.get("td_busy"), "ta_busy": pb.get("ta_busy"), "valu_busy": pb.get("valu_busy"),
+                    "l2_hit": pb.get("l2_hit"), "l2_read_gbs_upper": pb.get("l2_read_gbs_upper"),
+                    "l2_peak_gbs": PEAK_L2_GBS, "l2_frac_upper": pb.get("l2_frac_upper"),
+                    "l2_read_latency_cycles": pb.get("l2_read_latency_cycles"),
+                    "wait_any_per_wave_cycle": pb.get("wait_any_per_wave_cycle"),
+                    "executed_bytes_per_launch": int(exec_b),
+                    "executed_gbs": round(exec_b / (bounce_ms / 1e3) / 1e9, 1),
+                    "executed_vs_reference_bytes": round(exec_b / max(ref_b, 1), 4),
+                    "source": os.path.relpath(PMC_BOUND, ROOT) + " (medians over launches of "
+                              "scripts/profile_kernel.py, one rocprofv3 --pmc pass per counter set)"},
+                "primary_kernel_ms": round(primary_ms, 4),
+                "primary_algorithmic_bytes": int(ref_frame_bytes - ref_b),
+                "frame_ms": round(kernel_ms, 4), "frame_algorithmic_bytes": int(ref_frame_bytes),
+                "frame_executed_bytes": int(exec_frame_bytes),
+                "note": "kernel_ms / frame_ms: one launch alone (serial loop); the timed loop overlaps "
+                        "successive launches (pipeline)"},
             "work": {k: int(v) for k, v in counts.items()},
             "work_reference_dfs": {k: int(v) for k, v in ref_counts.items() if k != "lane_steps"},
             "traced_rays_per_s_M": round(counts["rays"] * world / (kernel_ms_max / 1e3) / 1e6, 3),
             "depth1_mrays_s": round(W * H * frames * args.steps / elapsed_d1 / 1e6, 3),
-            "host_inclusive_mrays_s": None if host is None else round(host, 3),
             "bvh_build_s": round(build_s, 4),
         }
+        if elapsed_other:
+            other = W * H * frames_other * args.steps / elapsed_other / 1e6
+            line["value_weak"] = round(value if args.scaling == "weak" else other, 3)
+            line["value_strong"] = round(other if args.scaling == "weak" else value, 3)
+        if host is not None:
+            line.update(host)
         if world == 1 and not args.no_cpu:
             cb = cpu_baseline()
             line["cpu_baseline"] = cb
             line["speedup_vs_cpu"] = round(value / cb["value"], 1)
+            line["speedup_vs_cpu_single_core"] = round(value / cb["single_core_value"], 1)
+            if host is not None:
+                line["host_inclusive_speedup_vs_cpu"] = round(host["host_inclusive_mrays_s"] / cb["value"], 1)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
     for x in rs:
         x.close()
+    return 0
+
+
+def host_inclusive(rs, cam, steps):
+    """SURVEY §8(d) t_frame: frames delivered to host memory. Pipelined: ctx
+    k % n renders frame k and copies it into its page-locked buffer
+    (mirt_render_frame_async), waiting first for its frame k - n; blocking:
+    mirt_render_frame into a pageable array, one call at a time."""
+    fdh = mirt.frame_desc(W, H, depth=DEPTH, seed=SEED, samples=SPP, jitter=JITTER)
+    bufs = [mirt.HostBuffer((H, W, 4)) for _ in rs]
+    n = len(rs)
+
+    def run(k0, count):
+        for k in range(k0, k0 + count):
+            i = k % n
+            rs[i].wait()
+            rs[i].render_frame_async(cam, fdh, bufs[i])
+        for x in rs:
+            x.wait()
+
+    run(0, 2 * n)
+    steps_h = max(steps, 50)
+    t0 = time.perf_counter()
+    run(0, steps_h)
+    el = time.perf_counter() - t0
+    last = bufs[(steps_h - 1) % n].array.copy()
+    # the blocking call (pageable destination); median: page faults make single calls noisy
+    img = rs[0].render_frame(cam, W, H, depth=DEPTH, seed=SEED, samples=SPP, jitter=JITTER)
+    dts = []
+    for _ in range(11):
+        t1 = time.perf_counter()
+        img = rs[0].render_frame(cam, W, H, depth=DEPTH, seed=SEED, samples=SPP, jitter=JITTER)
+        dts.append(time.perf_counter() - t1)
+    for b in bufs:
+        b.close()
+    return {"host_inclusive_mrays_s": round(W * H * SPP * steps_h / el / 1e6, 3),
+            "host_inclusive_ms_per_frame": round(el / steps_h * 1e3, 4),
+            "host_inclusive_frames": steps_h,
+            "host_inclusive_method": f"{n} ctxs, kernels + async D2H into page-locked buffers "
+                                     "(mirt_render_frame_async), frame k waits for frame k - n",
+            "host_frame_equals_blocking_call": bool((last == img).all()),
+            "host_blocking_mrays_s": round(W * H * SPP / sorted(dts)[len(dts) // 2] / 1e6, 3)}
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

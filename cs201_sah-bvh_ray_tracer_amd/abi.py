@@ -115,6 +115,10 @@ SIGNATURES = [
     ("mirt_shard_rows", I, [P, P]),
     ("mirt_render_frame", I, [P, P, P, P]),
     ("mirt_render_frame_device", I, [P, P, P, P, P, P]),
+    ("mirt_render_frame_async", I, [P, P, P, P]),
+    ("mirt_ctx_wait", I, [P]),
+    ("mirt_host_alloc", I, [C.c_size_t, C.POINTER(P)]),
+    ("mirt_host_free", None, [P]),
     ("mirt_accum_download", I, [P, P, C.c_size_t]),
     ("mirt_trace_rays", I, [P, P, I, I, I, C.c_uint64, C.c_uint32, P]),
     ("mirt_intersect_rays", I, [P, P, I, I, P]),

@@ -806,6 +806,7 @@ struct mirt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed_recorded = false;  // ev0/ev1 bracket a launch (mirt_last_kernel_ms)
     float last_ms = 0.0f;
     // wavefront phase boundaries of the last frame (any API)
     hipEvent_t ph0 = nullptr, ph1 = nullptr, ph2 = nullptr;
@@ -1124,7 +1125,10 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
     const int bw = c->block_waves;
     const int blocks = (tiles + bw - 1) / bw;
     if (blocks == 0) return MIRT_OK;
-    if (timed) HIP_TRY(hipEventRecord(c->ev0, s));
+    if (timed) {
+        HIP_TRY(hipEventRecord(c->ev0, s));
+        c->timed_recorded = true;
+    }
     // several frames and an accumulation buffer: raw colours per frame, then
     // fold_samples_kernel accumulates them in order
     float* const d_fold = f.samples > 1 ? d_acc : nullptr;
@@ -1401,15 +1405,22 @@ int mirt_render_frame_device(mirt_ctx* c, const mirt_camera* cam, const mirt_fra
     return launch_render(c, f, d_out, d_acc, (hipStream_t)stream, false, nullptr);
 }
 
-int mirt_render_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, mirt_rgba8* out)
+}  // extern "C"
+
+namespace {
+
+// The frame of mirt_render_frame up to and including its D2H copy, enqueued
+// on the ctx's stream.
+int enqueue_host_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, mirt_rgba8* out,
+                       const char* fn)
 {
-    if (!ctx_ok(c, true, "mirt_render_frame")) return MIRT_E_NOSCENE;
+    if (!ctx_ok(c, true, fn)) return MIRT_E_NOSCENE;
     if (!cam || !frame_desc_valid(fd) || !out) {
-        set_error("mirt_render_frame: invalid arguments");
+        set_error("%s: invalid arguments", fn);
         return MIRT_E_INVALID;
     }
     if (fd->use_bvh && c->num_nodes == 0) {
-        set_error("mirt_render_frame: use_bvh set but no tree uploaded");
+        set_error("%s: use_bvh set but no tree uploaded", fn);
         return MIRT_E_NOSCENE;
     }
     const FrameConst f = make_frame_const(cam, fd);
@@ -1425,9 +1436,45 @@ int mirt_render_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc
     rc = launch_render(c, f, c->d_out, c->d_acc, c->stream, true, nullptr);
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(out, c->d_out, pixels * 4, hipMemcpyDeviceToHost, c->stream));
+    return MIRT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mirt_render_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, mirt_rgba8* out)
+{
+    if (int rc = enqueue_host_frame(c, cam, fd, out, "mirt_render_frame")) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));
     HIP_TRY(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
     return MIRT_OK;
+}
+
+int mirt_render_frame_async(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, mirt_rgba8* out)
+{
+    return enqueue_host_frame(c, cam, fd, out, "mirt_render_frame_async");
+}
+
+int mirt_ctx_wait(mirt_ctx* c)
+{
+    if (!ctx_ok(c, false, "mirt_ctx_wait")) return MIRT_E_INVALID;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->timed_recorded) HIP_TRY(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+    return MIRT_OK;
+}
+
+int mirt_host_alloc(size_t bytes, void** out)
+{
+    if (!out) return MIRT_E_INVALID;
+    *out = nullptr;
+    HIP_TRY(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+    return MIRT_OK;
+}
+
+void mirt_host_free(void* p)
+{
+    if (p) (void)hipHostFree(p);
 }
 
 int mirt_accum_download(mirt_ctx* c, float* out, size_t count)

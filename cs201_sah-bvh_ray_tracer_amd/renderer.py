@@ -177,6 +177,31 @@ def shard_rows(fd):
     return rows
 
 
+class HostBuffer:
+    """Page-locked host memory (mirt_host_alloc) viewed as a numpy array."""
+
+    def __init__(self, shape, dtype=np.uint8):
+        self.L = load()
+        nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
+        p = C.c_void_p()
+        check(self.L.mirt_host_alloc(nbytes, C.byref(p)), "mirt_host_alloc")
+        self.p = p
+        buf = (C.c_char * max(nbytes, 1)).from_address(p.value)
+        self.array = np.frombuffer(buf, dtype=dtype, count=int(np.prod(shape))).reshape(shape)
+
+    def close(self):
+        if self.p:
+            self.array = None
+            self.L.mirt_host_free(self.p)
+            self.p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Renderer:
     """One device context (mirt_ctx) with a resident scene."""
 
@@ -231,6 +256,20 @@ class Renderer:
         out = np.zeros((n, width, 4), np.uint8)
         check(self.L.mirt_render_frame(self.h, C.byref(cam), C.byref(fd), ptr(out)), "mirt_render_frame")
         return out
+
+    def render_frame_async(self, cam, fd, out):
+        """Enqueue the frame and its D2H copy into `out` (a HostBuffer, or any
+        C-contiguous uint8 array of the shard's rows x width x 4) on the ctx's
+        own stream; `out` is complete after wait()."""
+        arr = out.array if isinstance(out, HostBuffer) else out
+        n = check(self.L.mirt_shard_rows(C.byref(fd), None), "mirt_shard_rows")
+        if arr.nbytes < n * fd.width * 4 or not arr.flags["C_CONTIGUOUS"]:
+            raise MirtError(f"render_frame_async: output holds {arr.nbytes} bytes, the shard needs {n * fd.width * 4}")
+        check(self.L.mirt_render_frame_async(self.h, C.byref(cam), C.byref(fd), ptr(arr)), "mirt_render_frame_async")
+
+    def wait(self):
+        """Block until the ctx's stream is idle (mirt_ctx_wait)."""
+        check(self.L.mirt_ctx_wait(self.h), "mirt_ctx_wait")
 
     def render_frame_device(self, cam, fd, d_out, d_acc=None, stream=None):
         """Enqueue a frame into device memory (integer device pointers)."""

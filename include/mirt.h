@@ -238,6 +238,25 @@ int mirt_render_frame(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_de
 int mirt_render_frame_device(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_desc *fd,
                              uint32_t *d_out, float *d_accum, void *stream);
 
+/* Frames in flight to host memory (SURVEY §8(d) t_frame: call -> RGBA8 on
+   the host). mirt_render_frame_async enqueues what mirt_render_frame does --
+   the frame's kernels and the D2H copy of its display into `out` -- on the
+   ctx's own stream and returns at once; `out` holds the frame once
+   mirt_ctx_wait(ctx) returns (or after the next blocking call on the ctx).
+   `out` should be page-locked memory from mirt_host_alloc: then the copy is a
+   DMA that overlaps the next frame's kernels on another ctx; pageable memory
+   works too but the runtime stages it. Rotating two or three ctxs (each with
+   the scene uploaded) keeps the GPU busy while earlier frames drain and
+   copy: for frame k use ctx k % n, mirt_ctx_wait it first (its buffer from
+   frame k - n is then complete), then mirt_render_frame_async. */
+int mirt_render_frame_async(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_desc *fd, mirt_rgba8 *out);
+/* Block until every call enqueued on the ctx's stream has finished. */
+int mirt_ctx_wait(mirt_ctx *ctx);
+/* Page-locked host memory (hipHostMalloc) for frame outputs; mirt_host_free
+   releases it (NULL is ignored). */
+int mirt_host_alloc(size_t bytes, void **out);
+void mirt_host_free(void *p);
+
 /* Download the ctx's accumulation buffer (row-major float3 of the shard). */
 int mirt_accum_download(mirt_ctx *ctx, float *out, size_t count);
 

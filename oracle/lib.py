@@ -145,8 +145,9 @@ class Oracle:
 class Reference:
     """The unmodified reference sources (oracle/_ref/libref_<W>x<H>.so)."""
 
-    def __init__(self, W, H):
-        path = os.path.join(REF_DIR, f"libref_{W}x{H}.so")
+    def __init__(self, W, H, opt="O2"):
+        """opt "O2": -O2 build; "O0": the reference's own flags (no -O, -g)."""
+        path = os.path.join(REF_DIR, f"libref_{W}x{H}.so" if opt == "O2" else f"libref_{opt}_{W}x{H}.so")
         if not os.path.exists(path):
             raise FileNotFoundError(path)
         L = C.CDLL(path)

@@ -21,12 +21,13 @@ step() {
 for s in $STEPS; do
   case $s in
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()";;
-    tests) step pytest_gpu 1200 python -m pytest tests -m gpu -x -q;;
+    tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread;;
     bench) step bench 600 python bench.py;;
+    bench_wl) for wl in 1080p_100k 4k_10k 4k_1m_4spp; do step bench_$wl 600 python bench.py --workload $wl --no-cpu; done;;
     # one launch at a time (--pipeline 1): per-kernel durations as bench.py's serial measurement loop sees them
-    prof)  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu --pipeline 1;;
-    pmc)   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --no-cpu --no-host --steps 5 --warmup 1 --pipeline 1
-           step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --no-cpu --no-host --steps 5 --warmup 1 --pipeline 1;;
+    prof)  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu --no-host --pipeline 1;;
+    pmc)   step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --no-cpu --no-host --steps 5 --warmup 1 --pipeline 1
+           step pmc_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --no-cpu --no-host --steps 5 --warmup 1 --pipeline 1;;
   esac
 done
 echo "done"

@@ -1,7 +1,10 @@
 #!/bin/bash
 # Counter probe of the frame kernels, one small counter set per rocprofv3 pass
-# (large sets can exceed the hardware and hang the profiler):
+# (a set beyond the hardware's per-block limits hangs the profiler, so every
+# pass runs under its own kill timeout and stays within 8 SQ / 4 TCC / 4 TCP /
+# 2 TA / 2 TD / 2 GRBM counters):
 #   scripts/pmc_probe.sh <tag> "<trav> <fast> <depth>" ...
+# Summarise with scripts/pmc_summary.py gpurun_out/<tag> [--json out.json].
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -14,6 +17,9 @@ SETS=(
  "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum"
  "TCP_TCC_READ_REQ_LATENCY_sum GRBM_GUI_ACTIVE"
  "TCC_HIT_sum TCC_MISS_sum"
+ "FETCH_SIZE"
+ "WRITE_SIZE"
+ "SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE"
 )
 for cfg in "$@"; do
   set -- $cfg
@@ -21,8 +27,8 @@ for cfg in "$@"; do
   i=0
   for cs in "${SETS[@]}"; do
     i=$((i+1))
-    timeout -k 10 90 rocprofv3 --pmc $cs --output-format csv -d "$OUT/$tag.$i" -o run -- \
-        python3 scripts/profile_kernel.py --trav $1 --fast $2 --depth $3 --frames 2 > "$OUT/$tag.$i.log" 2>&1
+    timeout -s KILL 90 rocprofv3 --pmc $cs --output-format csv -d "$OUT/$tag.$i" -o run -- \
+        python3 scripts/profile_kernel.py --trav $1 --fast $2 --depth $3 --frames 3 > "$OUT/$tag.$i.log" 2>&1
     rc=$?
     if [ $rc -ne 0 ]; then echo "$tag set $i rc=$rc"; grep -m2 -i "error" "$OUT/$tag.$i.log"; [ $rc -gt 1 ] && exit $rc; fi
   done

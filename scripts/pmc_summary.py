@@ -1,43 +1,133 @@
-"""Summarise scripts/pmc_probe.sh output: per config, the render kernel's
-counters (median over its launches)."""
+"""Summarise scripts/pmc_probe.sh output into the bound of each frame kernel.
+
+    python scripts/pmc_summary.py gpurun_out/<tag> [--json profiles/<tag>_pmc_bound.json] [--copy profiles/<tag>_pmc]
+
+Per config and kernel (primary / bounce): the median over its launches of
+every counter (the first launch of a run is cold, the median ignores it), and
+the utilisations derived from them (MI355X_MICROARCH.md for the units):
+
+  kernel cycles     GRBM_GUI_ACTIVE / 8 (the counter sums the 8 XCDs)
+  TD / TA busy      TD_TD_BUSY_sum, TA_TA_BUSY_sum over 256 CUs x cycles
+  VALU busy         SQ_INSTS_VALU x 2 cycles (one wave64 instruction issues over
+                    2 cycles) over 1024 SIMDs x cycles
+  L2 hit            TCC_HIT / (TCC_HIT + TCC_MISS)
+  L2 read bytes     TCP_TCC_READ_REQ x 128 B (gfx950 L2 line; an upper bound:
+                    partial-line requests count as whole lines) vs the 34.5 TB/s L2
+  L1 accesses       TCP_TOTAL_CACHE_ACCESSES per CU per cycle
+  HBM bytes         FETCH_SIZE x 2 (gfx950 tallies a wide read at half) +
+                    WRITE_SIZE, both KiB
+  mean L2 latency   TCP_TCC_READ_REQ_LATENCY / TCP_TCC_READ_REQ (cycles)
+"""
+import argparse
 import collections
 import csv
 import glob
+import json
 import os
+import shutil
 import statistics
-import sys
 
-root = sys.argv[1]
-cfgs = collections.defaultdict(dict)
-for d in sorted(glob.glob(os.path.join(root, "t*_f*_d*.*"))):
-    if d.endswith(".log"):
-        continue
-    cfg = os.path.basename(d).rsplit(".", 1)[0]
-    f = os.path.join(d, "run_counter_collection.csv")
-    if not os.path.exists(f):
-        continue
-    acc = collections.defaultdict(list)
-    for r in csv.DictReader(open(f)):
-        name = r["Kernel_Name"]
-        kern = ("bounce" if "bounce_kernel" in name else "primary" if "primary_kernel" in name else
-                "render" if "render_kernel" in name and "true, true" not in name else None)
-        if kern:
-            acc[(kern, r["Counter_Name"])].append(float(r["Counter_Value"]))
-    for (kern, k), v in acc.items():
-        cfgs[cfg + "/" + kern][k] = statistics.median(v)
-for cfg, c in cfgs.items():
-    g = c.get("GRBM_GUI_ACTIVE", 0) / 8
-    print(cfg, "kernel_cycles(per XCD)", int(g))
-    for k in sorted(c):
-        print(f"   {k:40s} {c[k]:.4g}")
-    if g and "SQ_WAVE_CYCLES" in c:
+CLOCK_HZ = 2.4e9
+CUS, SIMDS, XCDS = 256, 1024, 8
+L2_PEAK_GBS = 34500.0
+HBM_PEAK_GBS = 8000.0
+
+
+def kernel_of(name):
+    if "bounce_kernel" in name:
+        return "bounce"
+    if "primary_kernel" in name:
+        return "primary"
+    return None
+
+
+def derive(c):
+    d = {}
+    g = c.get("GRBM_GUI_ACTIVE", 0) / XCDS
+    if not g:
+        return d
+    d["kernel_cycles"] = int(g)
+    d["kernel_ms_at_2400MHz"] = round(g / CLOCK_HZ * 1e3, 4)
+    sec = g / CLOCK_HZ
+    if "TD_TD_BUSY_sum" in c:
+        d["td_busy"] = round(c["TD_TD_BUSY_sum"] / (CUS * g), 4)
+    if "TA_TA_BUSY_sum" in c:
+        d["ta_busy"] = round(c["TA_TA_BUSY_sum"] / (CUS * g), 4)
+    if "SQ_INSTS_VALU" in c:
+        d["valu_busy"] = round(c["SQ_INSTS_VALU"] * 2 / (SIMDS * g), 4)
+    if "SQ_WAVE_CYCLES" in c:
         wc = c["SQ_WAVE_CYCLES"]
-        print("   derived: WAIT_ANY/WAVE %.2f  WAIT_INST/WAVE %.2f  ACTIVE/WAVE %.2f" % (
-            c["SQ_WAIT_ANY"] / wc, c["SQ_WAIT_INST_ANY"] / wc, c["SQ_ACTIVE_INST_ANY"] / wc))
-        print("   derived: VALU busy per SIMD %.3f" % (c["SQ_INSTS_VALU"] * 2 / (g * 1024)))
+        d["wait_any_per_wave_cycle"] = round(c["SQ_WAIT_ANY"] / wc, 4)
+        d["wait_inst_any_per_wave_cycle"] = round(c["SQ_WAIT_INST_ANY"] / wc, 4)
+        d["active_inst_any_per_wave_cycle"] = round(c["SQ_ACTIVE_INST_ANY"] / wc, 4)
     if "TCC_HIT_sum" in c:
-        print("   derived: L2 hit %.3f  TA busy frac %.3f" % (
-            c["TCC_HIT_sum"] / max(1, c["TCC_HIT_sum"] + c["TCC_MISS_sum"]), c.get("TA_TA_BUSY_sum", 0) / max(1, g * 256)))
+        d["l2_hit"] = round(c["TCC_HIT_sum"] / max(1.0, c["TCC_HIT_sum"] + c["TCC_MISS_sum"]), 4)
+    if "TCP_TCC_READ_REQ_sum" in c:
+        b = c["TCP_TCC_READ_REQ_sum"] * 128
+        d["l2_read_bytes_upper"] = int(b)
+        d["l2_read_gbs_upper"] = round(b / sec / 1e9, 1)
+        d["l2_frac_upper"] = round(b / sec / 1e9 / L2_PEAK_GBS, 4)
     if "TCP_TOTAL_CACHE_ACCESSES_sum" in c:
-        print("   derived: L1 miss->L2 requests / accesses %.3f" % (
-            c["TCP_TCC_READ_REQ_sum"] / max(1, c["TCP_TOTAL_CACHE_ACCESSES_sum"])))
+        d["l1_accesses_per_cu_cycle"] = round(c["TCP_TOTAL_CACHE_ACCESSES_sum"] / (CUS * g), 4)
+    if "TCP_TCC_READ_REQ_LATENCY_sum" in c and c.get("TCP_TCC_READ_REQ_sum"):
+        d["l2_read_latency_cycles"] = round(c["TCP_TCC_READ_REQ_LATENCY_sum"] / c["TCP_TCC_READ_REQ_sum"], 1)
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        b = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
+        d["hbm_bytes"] = int(b)
+        d["hbm_gbs"] = round(b / sec / 1e9, 2)
+        d["hbm_frac"] = round(b / sec / 1e9 / HBM_PEAK_GBS, 5)
+    units = {k: d[k] for k in ("td_busy", "ta_busy", "valu_busy", "l2_frac_upper", "hbm_frac") if k in d}
+    if units:
+        top = max(units, key=units.get)
+        d["busiest_unit"] = top
+    return d
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("root")
+    ap.add_argument("--json")
+    ap.add_argument("--copy", help="copy the raw counter CSVs here")
+    ap.add_argument("--workload", default="1920,1080,10000,5",
+                    help="W,H,spheres,depth the probe rendered (scripts/profile_kernel.py defaults)")
+    a = ap.parse_args()
+    cfgs = collections.defaultdict(dict)
+    for d in sorted(glob.glob(os.path.join(a.root, "t*_f*_d*.*"))):
+        if d.endswith(".log"):
+            continue
+        cfg = os.path.basename(d).rsplit(".", 1)[0]
+        f = os.path.join(d, "run_counter_collection.csv")
+        if not os.path.exists(f):
+            continue
+        if a.copy:
+            os.makedirs(a.copy, exist_ok=True)
+            shutil.copy(f, os.path.join(a.copy, os.path.basename(d) + ".csv"))
+        acc = collections.defaultdict(list)
+        names = {}
+        for r in csv.DictReader(open(f)):
+            kern = kernel_of(r["Kernel_Name"])
+            if kern:
+                acc[(kern, r["Counter_Name"])].append(float(r["Counter_Value"]))
+                names[kern] = r["Kernel_Name"]
+        for (kern, k), v in acc.items():
+            e = cfgs[cfg + "/" + kern]
+            e.setdefault("counters", {})[k] = statistics.median(v)
+            e.setdefault("launches", {})[k] = len(v)
+            e["kernel"] = names[kern]
+    out = {}
+    for cfg, e in sorted(cfgs.items()):
+        e["derived"] = derive(e["counters"])
+        out[cfg] = e
+        print(cfg, e["kernel"][:80])
+        for k, v in sorted(e["derived"].items()):
+            print(f"   {k:34s} {v}")
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump({"source": f"scripts/pmc_probe.sh -> {a.root}", "clock_hz": CLOCK_HZ,
+                       "workload": [int(v) for v in a.workload.split(",")],
+                       "l2_peak_gbs": L2_PEAK_GBS, "hbm_peak_gbs": HBM_PEAK_GBS,
+                       "method": __doc__.strip().split("\n\n", 2)[-1], "kernels": out}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,38 @@
+"""bench.py's launcher on CPU: `python bench.py --gpus N --dry` starts N rank
+processes itself (no torchrun), runs the shard geometry, the gloo gather and
+the max-over-ranks timing with synthetic slabs, and rank 0 prints one JSON
+line whose frame assembled correctly. No GPU, no measurement."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(*args):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=240, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_self_launch_dry(n):
+    d = _run("--gpus", str(n), "--dry", "--steps", "2", "--warmup", "1")
+    assert d["dry"] is True and d["value"] is None
+    assert d["n_gpus"] == n
+    assert d["frame_assembled_ok"] is True
+    assert d["metric"].startswith("Mrays/s at 1080p")
+
+
+def test_failing_rank_fails_the_launch():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry",
+                        "--workload", "no-such-workload"], capture_output=True, text=True, timeout=120, env=env)
+    assert p.returncode != 0

@@ -258,6 +258,44 @@ def test_double_buffered_frames_identical(gpu, mirt):
         r2.close()
 
 
+def test_async_host_frames_pipelined(gpu, mirt, golden):
+    """bench.py's host-inclusive loop: three ctxs take successive frames,
+    each frame's kernels and its D2H copy into page-locked memory enqueued
+    with mirt_render_frame_async; every frame that lands on the host equals
+    the blocking call's (and frame 0 the reference's golden 1080p frame)."""
+    s, b = _scene(mirt, "render", 10000)
+    gpu.upload(s, b)
+    extra = [mirt.Renderer(0), mirt.Renderer(0)]
+    rs = [gpu] + extra
+    bufs = [mirt.HostBuffer((1080, 1920, 4)) for _ in rs]
+    try:
+        for x in extra:
+            x.upload(s, b)
+        cam = mirt.default_camera()
+        got = []
+        for k in range(7):
+            i = k % 3
+            rs[i].wait()
+            if k >= 3:
+                got.append(bufs[i].array.copy())
+            rs[i].render_frame_async(cam, mirt.frame_desc(1920, 1080, depth=5, seed=1, sample=k), bufs[i])
+        for x in rs:
+            x.wait()
+        for k in range(4, 7):
+            got.append(bufs[k % 3].array.copy())
+        assert len(got) == 7
+        assert sha(got[0]) == golden["frames"]["1920x1080_render10000_d5_m1_b1_s1_c0_step1"]["sha"]
+        for k in (1, 6):
+            assert (got[k] == gpu.render_frame(cam, 1920, 1080, depth=5, seed=1, sample=k)).all(), k
+        with pytest.raises(mirt.MirtError):
+            gpu.render_frame_async(cam, mirt.frame_desc(1920, 1080), np.zeros(16, np.uint8))
+    finally:
+        for x in bufs:
+            x.close()
+        for x in extra:
+            x.close()
+
+
 def test_counts_match_oracle(gpu, mirt, oracle):
     s, b = _scene(mirt, "render", 10000)
     gpu.upload(s, b)
