@@ -44,6 +44,27 @@ class Camera(C.Structure):
         return cls.from_buffer_copy(np.asarray(rec, dtype=CAMERA).tobytes())
 
 
+class Ray(C.Structure):
+    """ray.h:5-8 (by value in the per-ray drop-in calls)"""
+    _fields_ = [("origin", Vec3), ("direction", Vec3)]
+
+
+class Aabb(C.Structure):
+    """bvh.h:7-10"""
+    _fields_ = [("min", Vec3), ("max", Vec3)]
+
+
+class Rgba8(C.Structure):
+    """SDL_Color"""
+    _fields_ = [("r", C.c_uint8), ("g", C.c_uint8), ("b", C.c_uint8), ("a", C.c_uint8)]
+
+
+class HitRecord(C.Structure):
+    """hit.h:8-14 (object: pointer into the caller's sphere array)"""
+    _fields_ = [("t", C.c_float), ("point", Vec3), ("normal", Vec3), ("hit_something", C.c_int),
+                ("object", C.c_void_p)]
+
+
 class RandState(C.Structure):
     """glibc TYPE_3 rand() state (mirt_rand_state)."""
     _fields_ = [("r", C.c_int32 * 34), ("f", C.c_int32), ("b", C.c_int32)]
@@ -121,6 +142,8 @@ SIGNATURES = [
     ("mirt_host_free", None, [P]),
     ("mirt_accum_download", I, [P, P, C.c_size_t]),
     ("mirt_trace_rays", I, [P, P, I, I, I, C.c_uint64, C.c_uint32, P]),
+    ("mirt_trace_rays_at", I, [P, P, I, I, I, C.c_uint64, C.c_uint32, C.c_uint32, P]),
+    ("mirt_camera_rays_uv", I, [P, P, I, I, P, I, P]),
     ("mirt_intersect_rays", I, [P, P, I, I, P]),
     ("mirt_any_hit_rays", I, [P, P, I, I, P]),
     ("mirt_sphere_pairs", I, [P, P, P, I, P]),
@@ -134,6 +157,17 @@ SIGNATURES = [
     ("mirt_bounce_stats", I, [P, P, P, P, I]),
     ("mirt_set_option", I, [P, I, I]),
     ("mirt_get_option", I, [P, I]),
+    # include/mirt_dropin.h: the per-ray surface
+    ("mirt_dropin_init", I, [I, I, I]),
+    ("mirt_dropin_release", None, []),
+    ("mirt_dropin_rng", None, [C.c_uint64, C.c_uint32]),
+    ("mirt_dropin_invalidate", None, []),
+    ("mirt_dropin_status", I, []),
+    ("mirt_get_camera_ray", Ray, [P, C.c_float, C.c_float]),
+    ("mirt_trace_ray", Rgba8, [Ray, P, I, I, P]),
+    ("mirt_ray_sphere_intersect", HitRecord, [Ray, P]),
+    ("mirt_ray_aabb_intersect", I, [Ray, Aabb]),
+    ("mirt_ray_bvh_intersect", HitRecord, [Ray, P]),
 ]
 
 OPT_TRAVERSAL, OPT_FAST_SLAB, OPT_BLOCK_WAVES, OPT_DEFER, OPT_BOUNCE_THRESHOLD, OPT_PRUNE, OPT_ORDERED = (

@@ -621,7 +621,7 @@ __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, 
 template <bool FAST>
 __global__ __launch_bounds__(256) void trace_rays_kernel(DevScene sc, const mirt_ray* __restrict__ rays, int n,
                                                          int depth, int use_bvh, uint64_t seed, uint32_t sample,
-                                                         uint32_t* __restrict__ out)
+                                                         uint32_t pixel0, uint32_t* __restrict__ out)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool alive = i < n;
@@ -631,7 +631,7 @@ __global__ __launch_bounds__(256) void trace_rays_kernel(DevScene sc, const mirt
     __shared__ uint32_t cstack[kMaxDepth * 256];
     __shared__ uint32_t wstack[kWideStack * kWideStride];
     const uint32_t c = trace_path<FAST, false>(sc, ray, alive, depth, use_bvh != 0,
-                                                  pixel_key(seed, (uint32_t)i, sample), cnt, cstack + threadIdx.x, 256,
+                                                  pixel_key(seed, pixel0 + (uint32_t)i, sample), cnt, cstack + threadIdx.x, 256,
                                                   wstack + threadIdx.x);
     if (alive) out[i] = c;
 }
@@ -796,6 +796,21 @@ __global__ void camera_rays_kernel(FrameConst f, mirt_ray* __restrict__ out)
     if (x >= f.width || r >= f.num_rows) return;
     const Ray ray = camera_ray(f, x, shard_row_to_y(f, r), row_sample(f, r));
     out[(size_t)r * f.width + x] = {{ray.ox, ray.oy, ray.oz}, {ray.dx, ray.dy, ray.dz}};
+}
+
+// get_camera_ray (ray.c:17-32) at caller-given (u, v): the batched form of
+// the per-ray call, for callers that build their own pixel loop.
+__global__ void camera_uv_kernel(FrameConst f, const float2* __restrict__ uv, int n, mirt_ray* __restrict__ out)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float u = uv[i].x, v = uv[i].y;
+    float dx = f.fx + f.hx * u, dy = f.fy + f.hy * u, dz = f.fz + f.hz * u;
+    dx = dx + f.vx * v;
+    dy = dy + f.vy * v;
+    dz = dz + f.vz * v;
+    normalize3(dx, dy, dz);
+    out[i] = {{f.px, f.py, f.pz}, {dx, dy, dz}};
 }
 
 }  // namespace
@@ -1577,6 +1592,12 @@ int mirt_camera_rays(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc*
 int mirt_trace_rays(mirt_ctx* c, const mirt_ray* rays, int n, int depth, int use_bvh, uint64_t seed,
                     uint32_t sample, mirt_rgba8* out)
 {
+    return mirt_trace_rays_at(c, rays, n, depth, use_bvh, seed, sample, 0, out);
+}
+
+int mirt_trace_rays_at(mirt_ctx* c, const mirt_ray* rays, int n, int depth, int use_bvh, uint64_t seed,
+                       uint32_t sample, uint32_t pixel0, mirt_rgba8* out)
+{
     if (!ctx_ok(c, true, "mirt_trace_rays")) return MIRT_E_NOSCENE;
     if (n < 0 || (n > 0 && (!rays || !out)) || depth < 0 || depth > kMaxDepth) {
         set_error("mirt_trace_rays: invalid arguments");
@@ -1598,9 +1619,9 @@ int mirt_trace_rays(mirt_ctx* c, const mirt_ray* rays, int n, int depth, int use
         const mirt_ray* in = (const mirt_ray*)c->d_in;
         uint32_t* res = (uint32_t*)c->d_res;
         if (c->fast_slab)
-            trace_rays_kernel<true><<<g, b, 0, c->stream>>>(sc, in, n, depth, use_bvh, seed, sample, res);
+            trace_rays_kernel<true><<<g, b, 0, c->stream>>>(sc, in, n, depth, use_bvh, seed, sample, pixel0, res);
         else
-            trace_rays_kernel<false><<<g, b, 0, c->stream>>>(sc, in, n, depth, use_bvh, seed, sample, res);
+            trace_rays_kernel<false><<<g, b, 0, c->stream>>>(sc, in, n, depth, use_bvh, seed, sample, pixel0, res);
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev1, c->stream));
@@ -1682,6 +1703,32 @@ int mirt_any_hit_rays(mirt_ctx* c, const mirt_ray* rays, int n, int use_bvh, int
     HIP_TRY(hipMemcpyAsync(out, c->d_res, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     HIP_TRY(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+    return MIRT_OK;
+}
+
+int mirt_camera_rays_uv(mirt_ctx* c, const mirt_camera* cam, int width, int height, const float* uv, int n,
+                        mirt_ray* out)
+{
+    if (!ctx_ok(c, false, "mirt_camera_rays_uv")) return MIRT_E_INVALID;
+    if (!cam || width <= 0 || height <= 0 || n < 0 || (n > 0 && (!uv || !out))) {
+        set_error("mirt_camera_rays_uv: invalid arguments");
+        return MIRT_E_INVALID;
+    }
+    if (n == 0) return MIRT_OK;
+    mirt_frame_desc fd{};
+    fd.width = width;
+    fd.height = height;
+    fd.row_block = 8;
+    fd.num_shards = 1;
+    const FrameConst f = make_frame_const(cam, &fd);
+    int rc = ensure(&c->d_in, &c->in_cap, 8 * (size_t)n);
+    if (!rc) rc = ensure(&c->d_res, &c->res_cap, sizeof(mirt_ray) * (size_t)n);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(c->d_in, uv, 8 * (size_t)n, hipMemcpyHostToDevice, c->stream));
+    camera_uv_kernel<<<(n + 255) / 256, 256, 0, c->stream>>>(f, (const float2*)c->d_in, n, (mirt_ray*)c->d_res);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(out, c->d_res, sizeof(mirt_ray) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
     return MIRT_OK;
 }
 

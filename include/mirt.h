@@ -264,6 +264,10 @@ int mirt_accum_download(mirt_ctx *ctx, float *out, size_t count);
    pixel index i. */
 int mirt_trace_rays(mirt_ctx *ctx, const mirt_ray *rays, int n, int depth, int use_bvh,
                     uint64_t seed, uint32_t sample, mirt_rgba8 *out);
+/* Same, ray i using RNG contract pixel index pixel0 + i (a caller's own pixel
+   loop in chunks: pixel0 = y * width + x of the chunk's first pixel). */
+int mirt_trace_rays_at(mirt_ctx *ctx, const mirt_ray *rays, int n, int depth, int use_bvh,
+                       uint64_t seed, uint32_t sample, uint32_t pixel0, mirt_rgba8 *out);
 
 /* Closest hit: ray_bvh_intersect (hit.c:91-109) when use_bvh, else the brute
    force loop of renderer.c:36-43. */
@@ -286,6 +290,11 @@ int mirt_aabb_pairs(mirt_ctx *ctx, const mirt_ray *rays, const mirt_aabb *boxes,
 /* The camera ray of every pixel of the shard (ray.c:17-32 with the pixel
    mapping of main.c:356-365). */
 int mirt_camera_rays(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_desc *fd, mirt_ray *out);
+/* get_camera_ray (ray.c:17-32) at n caller-given (u, v) pairs (uv[2i],
+   uv[2i+1]), for a frame of width x height (the reference's compile-time
+   WIDTH/HEIGHT, ray.c:18). */
+int mirt_camera_rays_uv(mirt_ctx *ctx, const mirt_camera *cam, int width, int height, const float *uv, int n,
+                        mirt_ray *out);
 
 /* Reference-DFS work counters of one frame (instrumented kernel build,
    untimed): the algorithmic-bytes numerator of SURVEY §8(d). */

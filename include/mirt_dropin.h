@@ -1,0 +1,75 @@
+/*
+ * include/mirt_dropin.h -- the reference's PER-RAY call surface, same
+ * arguments and by-value struct layouts, backed by libmirt's kernels
+ * (SURVEY.md §8(b) "per-ray call surface (kept)").
+ *
+ *   reference (file:line)                              here
+ *   Ray get_camera_ray(Camera*, float, float)          mirt_get_camera_ray       ray.h:11,   ray.c:17-32
+ *   SDL_Color trace_ray(Ray, Sphere*, int, int,        mirt_trace_ray            renderer.h:8, renderer.c:21-77
+ *                       BVHNode*)
+ *   HitRecord ray_sphere_intersect(Ray, Sphere*)       mirt_ray_sphere_intersect hit.h:16,   hit.c:19-39
+ *   int ray_aabb_intersect(Ray, AABB)                  mirt_ray_aabb_intersect   hit.h:17,   hit.c:49-82
+ *   HitRecord ray_bvh_intersect(Ray, BVHNode*)         mirt_ray_bvh_intersect    hit.h:18,   hit.c:91-109
+ *   BVHNode* build_bvh_node(Sphere*, int, int, int)    mirt_build_bvh_node       bvh.h:26 (mirt.h)
+ *   void free_bvh(BVHNode*)                            mirt_free_bvh             benchmark.c:81-88 (mirt.h)
+ *
+ * The exact names of the left column, taking the reference's own types, are
+ * defined by cs201_sah-bvh_ray_tracer_amd/dropin/reference_names.c: a C file a
+ * maintainer compiles with the reference's headers IN PLACE OF ray.c, hit.c
+ * and renderer.c, so main.c and benchmark.c build unchanged.
+ *
+ * Every call is one GPU launch on a process-wide context (device 0 unless
+ * mirt_dropin_init chose another), so the per-ray form is for callers that
+ * cannot batch; a pixel loop should call mirt_render_frame (mirt.h) instead,
+ * which replaces the whole loop of main.c:356-407 with one launch.
+ *
+ * Scenes: trace_ray / ray_bvh_intersect upload the caller's spheres and
+ * pointer tree on first sight (keyed by the sphere pointer, count and root
+ * pointer) and reuse them while the key is unchanged; call
+ * mirt_dropin_invalidate() after changing sphere contents in place.
+ * ray_bvh_intersect without a preceding trace_ray finds the sphere array from
+ * the tree's leaf pointers (the lowest to the highest leaf sphere).
+ *
+ * RNG: trace_ray's bounces draw from the per-pixel RNG contract
+ * with seed/sample from mirt_dropin_rng and pixel index = the number of
+ * trace_ray calls since then, so a caller that traces pixel (x, y) of a W-wide
+ * frame as call y * W + x gets exactly mirt_render_frame's colours.
+ *
+ * Errors: the reference's functions cannot report failure; these return the
+ * zero value (black / no hit / 0) and record the status: mirt_dropin_status()
+ * gives the last call's status (MIRT_OK or negative), mirt_last_error() the
+ * message. There is no CPU path.
+ */
+#ifndef MIRT_DROPIN_H
+#define MIRT_DROPIN_H
+
+#include "mirt.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Device for the process-wide context and the frame size get_camera_ray
+   assumes (the reference's compile-time WIDTH/HEIGHT, constants.h:7-8, used
+   at ray.c:18). Optional: the first call otherwise uses device 0, 800x600. */
+int mirt_dropin_init(int device, int width, int height);
+/* Release the context and every uploaded scene. */
+void mirt_dropin_release(void);
+/* RNG contract of trace_ray's bounces; restarts the pixel counter at 0. */
+void mirt_dropin_rng(uint64_t seed, uint32_t sample);
+/* Forget the uploaded scene (after changing sphere contents in place). */
+void mirt_dropin_invalidate(void);
+/* Status of the last drop-in call (MIRT_OK or a negative MIRT_E_*). */
+int mirt_dropin_status(void);
+
+mirt_ray mirt_get_camera_ray(mirt_camera *camera, float u, float v);
+mirt_rgba8 mirt_trace_ray(mirt_ray ray, mirt_sphere *spheres, int num_spheres, int depth, mirt_bvh_node *bvh);
+mirt_hit_record mirt_ray_sphere_intersect(mirt_ray ray, mirt_sphere *sphere);
+int mirt_ray_aabb_intersect(mirt_ray ray, mirt_aabb box);
+mirt_hit_record mirt_ray_bvh_intersect(mirt_ray ray, mirt_bvh_node *node);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MIRT_DROPIN_H */

@@ -1,0 +1,207 @@
+"""The drop-in boundary from C: programs written against include/mirt.h and
+include/mirt_dropin.h only (tests/c/), compiled with gcc at test time and
+linked to libmirt.so -- no ctypes between them and the library.
+
+CPU (here): both programs compile warning-free; the per-ray shim
+cs201_sah-bvh_ray_tracer_amd/dropin/reference_names.c compiles against the
+REFERENCE's own headers, where its static assertions pin every struct layout
+(Sphere, Ray, Camera, AABB, BVHNode, HitRecord, SDL_Color) to the mirt_*
+types, and links with the reference's untouched bvh.c / sphere.c / vec3.c /
+camera.c into a program that uses the reference's names (skipped where
+/root/reference is absent); without a GPU the C driver fails loudly.
+
+GPU: dropin_main replays main.c's frame loop (fresh / accumulating frames,
+camera moves, BVH toggle) -- every displayed frame equals the oracle's
+(render + main.c:394-401 accumulation), the 1080p first frame the reference's
+golden, a tree built by the REFERENCE's build_bvh_node (oracle/_ref) uploads
+and renders the golden frame, and the per-pixel loop through the per-ray
+surface reproduces the frame; dropin_bench replays benchmark.c's sweep and
+its per-ray hit flags equal the reference's goldens."""
+import hashlib
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT
+
+PKG = os.path.join(ROOT, "cs201_sah-bvh_ray_tracer_amd")
+CDIR = os.path.join(ROOT, "tests", "c")
+REF = "/root/reference"
+CFLAGS = ["-std=gnu11", "-O2", "-Wall", "-Wextra", "-Werror", "-ffp-contract=off"]
+
+
+def build(tmp, name):
+    exe = os.path.join(str(tmp), name)
+    subprocess.run(["gcc", *CFLAGS, "-I", os.path.join(ROOT, "include"), os.path.join(CDIR, name + ".c"), "-o", exe,
+                    "-L", PKG, "-lmirt", "-Wl,-rpath," + PKG, "-ldl", "-lm"], check=True)
+    return exe
+
+
+def run(cmd, timeout=240):
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+    return p.returncode, p.stdout, p.stderr
+
+
+@pytest.mark.parametrize("name", ["dropin_main", "dropin_bench"])
+def test_c_callers_compile(tmp_path, name):
+    assert os.path.exists(build(tmp_path, name))
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "src")), reason="reference sources absent (GPU box)")
+def test_reference_names_against_reference_headers(tmp_path):
+    """reference_names.c + the reference's own bvh.c, sphere.c, vec3.c,
+    camera.c (untouched, compiled where they lie) + a caller using only the
+    reference's names and types: compiles (layout assertions hold) and links
+    against libmirt.so in place of ray.c / hit.c / renderer.c."""
+    caller = tmp_path / "caller.c"
+    caller.write_text(
+        '#include "Custom/bvh.h"\n#include "Custom/hit.h"\n#include "Custom/renderer.h"\n'
+        '#include "mirt_dropin.h"\n#include <stdio.h>\n'
+        "int main(void) {\n"
+        "  Camera cam = {{0, 4, 50}, {0, 0, -1}, {1, 0, 0}, {0, 1, 0}, -3.14159265f, 0, 45.0f, 0};\n"
+        "  Sphere s[3] = {{{0, 0, 0}, 1, {255, 0, 0, 255}}, {{3, 0, 0}, 1, {0, 255, 0, 255}},\n"
+        "                 {{-3, 0, 0}, 1, {0, 0, 255, 255}}};\n"
+        "  BVHNode *root = build_bvh_node(s, 0, 3, 0);\n"
+        "  Ray r = get_camera_ray(&cam, 0.0f, 0.0f);\n"
+        "  SDL_Color c = trace_ray(r, s, 3, 5, root);\n"
+        "  HitRecord h = ray_bvh_intersect(r, root);\n"
+        "  int a = ray_aabb_intersect(r, root->bounds);\n"
+        "  HitRecord q = ray_sphere_intersect(r, &s[0]);\n"
+        '  printf("status %d color %d hit %d box %d sphere %d\\n", mirt_dropin_status(), c.r, h.hit_something, a,\n'
+        "         q.hit_something);\n"
+        "  return 0;\n}\n")
+    inc = ["-I", os.path.join(REF, "include"), "-I", os.path.join(ROOT, "include")]
+    srcs = [os.path.join(REF, "src", f + ".c") for f in ("bvh", "sphere", "vec3", "camera")]
+    exe = str(tmp_path / "caller")
+    subprocess.run(["gcc", "-std=gnu11", "-O2", "-ffp-contract=off", "-w", *inc, str(caller),
+                    os.path.join(PKG, "dropin", "reference_names.c"), *srcs, "-o", exe, "-L", PKG, "-lmirt",
+                    "-Wl,-rpath," + PKG, "-lm"], check=True)
+    # the shim itself builds warning-free against the reference's headers
+    subprocess.run(["gcc", "-std=gnu11", "-Wall", "-Wextra", "-Werror", "-c", *inc,
+                    os.path.join(PKG, "dropin", "reference_names.c"), "-o", str(tmp_path / "rn.o")], check=True)
+    import torch
+    if not torch.cuda.is_available():
+        rc, out, err = run([exe], 60)
+        # no GPU: the reference-named calls return zero values, no abort
+        assert rc == 0 and "status -4" in out, (rc, out, err)
+
+
+def test_c_driver_fails_loudly_without_gpu(tmp_path):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    exe = build(tmp_path, "dropin_main")
+    rc, out, err = run([exe, "64", "36", "100", "1", "R,", str(tmp_path / "o")], 60)
+    assert rc != 0 and "mirt_create failed" in err
+
+
+def _frames(out, W, H):
+    raw = np.fromfile(out + ".rgba", np.uint8).reshape(-1, H, W, 4)
+    log = [ln.split() for ln in open(out + ".txt")]
+    return raw, log
+
+
+def _camera(mirt, words):
+    b = b"".join(int(w, 16).to_bytes(4, "little") for w in words)
+    return mirt.abi.Camera.from_buffer_copy(b)
+
+
+@pytest.mark.gpu
+def test_c_main_loop_golden_1080p(tmp_path, golden):
+    """The C frame loop's first (fresh) frame at 1080p / 10k is the
+    reference's golden depth-5 frame; the next accumulate."""
+    exe = build(tmp_path, "dropin_main")
+    out = str(tmp_path / "f")
+    rc, so, se = run([exe, "1920", "1080", "10000", "1", "R,,", out])
+    assert rc == 0, se
+    raw, log = _frames(out, 1920, 1080)
+    assert len(raw) == 3 and [row[2:4] for row in log] == [["0", "1"], ["1", "2"], ["1", "3"]]
+    key = "1920x1080_render10000_d5_m1_b1_s1_c0_step1"
+    assert hashlib.sha256(raw[0].tobytes()).hexdigest() == golden["frames"][key]["sha"]
+
+
+@pytest.mark.gpu
+def test_c_main_loop_matches_oracle(tmp_path, mirt, oracle):
+    """A scripted session at 160x90 / 1000 spheres: first frame accumulating
+    onto the zero buffer (main.c's initial state: accumulated_frames = 1,
+    camera.move = 0), moves, a mouse drag (camera_update), the BVH toggled
+    off and on; every displayed frame equals the oracle's render + main.c
+    accumulation with the camera the C program logged."""
+    exe = build(tmp_path, "dropin_main")
+    out = str(tmp_path / "s")
+    W, H = 160, 90
+    script = ",,w,,m12:-7;,,aa,b,,b,u,m-30:40;,,"
+    rc, so, se = run([exe, str(W), str(H), "1000", "1", script, out])
+    assert rc == 0, se
+    raw, log = _frames(out, W, H)
+    assert len(raw) == script.count(",") + 1
+    s = oracle.render_scene(1, 1000)
+    t = oracle.build(s)
+    acc = np.zeros(W * H * 3, np.float32)
+    try:
+        for k, row in enumerate(log):
+            frame, sample, accumulate, frames, use_bvh = map(int, row[:5])
+            cam = _camera(mirt, row[5:21])
+            col = oracle.render(cam, W, H, s, t if use_bvh else None, depth=5, use_bvh=bool(use_bvh), mode=1,
+                                seed=1, sample=sample)
+            want = oracle.accumulate(col, acc, not accumulate, frames).reshape(H, W, 4)
+            assert (raw[k] == want).all(), (k, row[:5])
+    finally:
+        oracle.free(t)
+    moved = [_camera(mirt, row[5:21]) for row in log]
+    assert moved[-1].position.x != moved[0].position.x and moved[-1].yaw != moved[0].yaw
+
+
+@pytest.mark.gpu
+def test_c_per_pixel_loop_through_per_ray_surface(tmp_path):
+    """main.c:358-374 verbatim in structure: mirt_get_camera_ray +
+    mirt_trace_ray per pixel reproduce mirt_render_frame's fresh frame."""
+    exe = build(tmp_path, "dropin_main")
+    rc, so, se = run([exe, "64", "36", "1000", "1", "R", str(tmp_path / "p"), "--per-ray"])
+    assert rc == 0, so + se
+    assert "0 differ" in so
+
+
+@pytest.mark.gpu
+def test_c_reference_built_pointer_tree(tmp_path, golden):
+    """The REFERENCE's own build_bvh_node (oracle/_ref) builds the pointer
+    tree; mirt_scene_upload takes it unchanged and the frame is golden."""
+    lib = os.path.join(ROOT, "oracle", "_ref", "libref_160x90.so")
+    if not os.path.exists(lib):
+        pytest.skip("oracle/_ref not built")
+    exe = build(tmp_path, "dropin_main")
+    out = str(tmp_path / "r")
+    rc, so, se = run([exe, "160", "90", "10000", "1", "R", out, "--ref-build", lib])
+    assert rc == 0, se
+    assert "reference's build_bvh_node" in so
+    raw, _ = _frames(out, 160, 90)
+    assert hashlib.sha256(raw[0].tobytes()).hexdigest() == golden["frames"]["160x90_render10000_d5_m1_b1_s1_c0_step1"]["sha"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,per_ray", [("small", 32), ("reference", 0)])
+def test_c_benchmark_mode(tmp_path, name, per_ray):
+    """benchmark.c's sweep from C: per-ray hit flags of both loops equal the
+    reference's (tests/golden/bench_mode.json); on the small sweep the first
+    32 rays also go through the per-ray surface one call at a time."""
+    with open(os.path.join(GOLDEN, "bench_mode.json")) as f:
+        sw = json.load(f)["sweeps"][name]
+    pts = sw["points"]
+    nr = pts[0]["rays"]
+    exe = build(tmp_path, "dropin_bench")
+    out = str(tmp_path / "b")
+    cmd = [exe, str(sw["seed"]), str(nr), out] + [str(p["spheres"]) for p in pts]
+    if per_ray:
+        cmd += ["--per-ray", str(per_ray)]
+    rc, so, se = run(cmd)
+    assert rc == 0, so[-2000:] + se
+    flags = np.fromfile(out + ".bin", np.int32).reshape(len(pts), 2, nr)
+    for p, f in zip(pts, flags):
+        assert hashlib.sha256(f[0].tobytes()).hexdigest() == p["sha_hit_no_bvh"], p["spheres"]
+        assert hashlib.sha256(f[1].tobytes()).hexdigest() == p["sha_hit_bvh"], p["spheres"]
+        assert int(f[0].sum()) == p["hits_no_bvh"] and int(f[1].sum()) == p["hits_bvh"]
+    lines = open(out + ".txt").read().split("\n")
+    assert [int(ln.split()[0]) for ln in lines if ln] == [p["spheres"] for p in pts]

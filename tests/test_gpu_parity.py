@@ -556,3 +556,56 @@ def test_cached_tree_renders_golden_frame(gpu, mirt, golden, tmp_path):
     gpu.upload(s, b)
     img = gpu.render_frame(mirt.default_camera(), 1920, 1080, depth=5, seed=1)
     assert sha(img) == golden["frames"]["1920x1080_render10000_d5_m1_b1_s1_c0_step1"]["sha"]
+
+
+def test_per_ray_surface_matches_reference(mirt, small, golden):
+    """include/mirt_dropin.h by value, one launch per call, against the
+    reference's own outputs: get_camera_ray, ray_bvh_intersect on a pointer
+    tree (object pointers into the caller's array), trace_ray (contract pixel
+    = call order), ray_sphere_intersect and ray_aabb_intersect (empty boxes)."""
+    import ctypes as C
+    abi = mirt.abi
+    L = mirt.load()
+    assert L.mirt_dropin_init(0, 160, 90) == 0
+    try:
+        s = small["render_1000_1_pre"].copy()
+        root = mirt.build_bvh_node(s)
+        base = s.ctypes.data
+        rays = small["hits_rays"]
+        idx = list(range(0, 4000, 97)) + list(range(4000, len(rays)))[:60]
+        want = small["hits_render_1000"]
+        for i in idx:
+            h = L.mirt_ray_bvh_intersect(abi.Ray.from_buffer_copy(rays[i].tobytes()), root)
+            assert L.mirt_dropin_status() == 0
+            assert h.hit_something == want[i]["hit"], i
+            if h.hit_something:
+                assert (h.object - base) // abi.SPHERE.itemsize == want[i]["sphere"], i
+                assert np.float32(h.t).tobytes() == want[i]["t"].tobytes(), i
+        L.mirt_dropin_rng(3, 0)
+        tr = small["trace_d5_mode1"]
+        for i in range(48):
+            c = L.mirt_trace_ray(abi.Ray.from_buffer_copy(rays[i].tobytes()), C.c_void_p(base), len(s), 5, root)
+            assert bytes(c) == tr[i].tobytes(), i
+        ps, pw = small["pairs_spheres"], small["pairs_sphere_hits"]
+        for i in range(0, 400, 7):
+            sp = np.ascontiguousarray(ps[i:i + 1])
+            h = L.mirt_ray_sphere_intersect(abi.Ray.from_buffer_copy(rays[i].tobytes()), C.c_void_p(sp.ctypes.data))
+            assert h.hit_something == pw[i]["hit"] and (not h.hit_something or h.object == sp.ctypes.data), i
+            if h.hit_something:
+                assert np.float32(h.t).tobytes() == pw[i]["t"].tobytes(), i
+        bx, bw = small["pairs_boxes"], small["pairs_box_hits"]
+        for i in list(range(0, 70)) + list(range(70, 2000, 37)):
+            a = L.mirt_ray_aabb_intersect(abi.Ray.from_buffer_copy(rays[i].tobytes()),
+                                          abi.Aabb.from_buffer_copy(bx[i].tobytes()))
+            assert a == bw[i], i
+        cam = mirt.default_camera()
+        cr = small["camrays_160x90_cam0"]       # rows 0, 1, 45, 89 of the reference's camera rays
+        for ri, y in enumerate([0, 1, 45, 89]):
+            for x in (0, 1, 79, 80, 159):
+                u = np.float32((np.float32(x) / np.float32(160) - np.float32(0.5)) * (np.float32(160) / np.float32(90)))
+                v = np.float32(np.float32(y) / np.float32(90) - np.float32(0.5))
+                r = L.mirt_get_camera_ray(C.byref(cam), float(u), float(-v))
+                assert bytes(r) == cr[ri, x].tobytes(), (y, x)
+        mirt.free_bvh(root)
+    finally:
+        L.mirt_dropin_release()
