@@ -144,6 +144,7 @@ SIGNATURES = [
     ("mirt_trace_rays", I, [P, P, I, I, I, C.c_uint64, C.c_uint32, P]),
     ("mirt_trace_rays_at", I, [P, P, I, I, I, C.c_uint64, C.c_uint32, C.c_uint32, P]),
     ("mirt_camera_rays_uv", I, [P, P, I, I, P, I, P]),
+    ("mirt_bvh_overlay", I, [P, P, I, I, I, P]),
     ("mirt_intersect_rays", I, [P, P, I, I, P]),
     ("mirt_any_hit_rays", I, [P, P, I, I, P]),
     ("mirt_sphere_pairs", I, [P, P, P, I, P]),

@@ -294,6 +294,14 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask)
 // scattered, so they go through a queue to persistent waves in which every
 // lane owns one pixel's chain and refills from the queue when it ends.
 
+// Measured (scripts/ab_libs.py, 1080p/10k/depth 5, profiles/r02*_ab*.log): 192
+// nodes at 4 waves/SIMD 1659 Mrays/s; 96 nodes at 5 waves/SIMD (the LDS of
+// five workgroups then fits 160 KB) 1772; 6 waves/SIMD spills: 1587.
+#ifndef MIRT_HCACHE
+#define MIRT_HCACHE 96
+#endif
+constexpr uint32_t kHCache = MIRT_HCACHE;  // HNodes staged in LDS per bounce workgroup (64 B each)
+
 // First bounce of one pixel, produced by primary_kernel.
 struct BounceRec {
     float ox, oy, oz, dx, dy, dz;
@@ -388,6 +396,8 @@ struct BounceWalk<0> {
 template <>
 struct BounceWalk<2> {
     WideWalk w;
+    lds_uint4* hc = nullptr;  // the top HNodes staged in LDS (bounce_kernel)
+    uint32_t hc_n = 0;
     __device__ void start(const DevScene&) { w = wide_walk_start(true); }
     __device__ void stop() { w = wide_walk_start(false); }
     __device__ bool walking() const { return wide_walking(w); }
@@ -395,7 +405,7 @@ struct BounceWalk<2> {
     __device__ void step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr, uint32_t* stk,
                          float& bt, int& bs, Counters& cnt)
     {
-        wide_lane_step<FAST, false>(sc, sr, sp, pr, w, stk, bt, bs, cnt);
+        wide_lane_step<FAST, false>(sc, sr, sp, pr, w, stk, bt, bs, cnt, hc, hc_n);
     }
 };
 
@@ -443,8 +453,15 @@ __device__ __forceinline__ bool shade_level(const DevScene& sc, const FrameConst
 // finished four lanes per ray -- a sparse wave costs full issue slots per
 // step, so four lanes per ray make the drain's steps about four times
 // shorter at no extra cost.
+// Register budget of the bounce kernel: 5 waves per SIMD (<= 96 VGPRs; 4
+// without the attribute, at 114). The pipelined frames gain most: the
+// co-running primary pass gets the issue slots the fifth wave hides.
+#ifndef MIRT_BOUNCE_WAVES
+#define MIRT_BOUNCE_WAVES 5
+#endif
+#define MIRT_BOUNCE_ATTR __attribute__((amdgpu_waves_per_eu(MIRT_BOUNCE_WAVES)))
 template <bool FAST, int WALK, bool DIAG = false>
-__global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
+__global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
                                                      float* __restrict__ acc, const BounceRec* __restrict__ queue,
                                                      uint32_t* __restrict__ qctl, int threshold, int quad_drain,
                                                      uint64_t* __restrict__ diag = nullptr)
@@ -457,6 +474,17 @@ __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, 
     __shared__ uint32_t cstack[kMaxDepth * cstride];
     __shared__ uint32_t wstack[LANE4 ? kWideStack * kWideStride : 1];
     __shared__ uint32_t qsrc[LANE4 ? 4 * 16 : 1];  // quad drain: source lane of each quad, per wave
+    // the tree's top levels (the first kHCache HNodes, breadth-first) in LDS:
+    // every bounce walk starts there, so those steps skip the vector-memory
+    // path (TD, the kernel's busiest unit)
+    __shared__ uint4 hcache[LANE4 ? 4 * kHCache : 1];
+    uint32_t hc_n = 0;
+    if constexpr (LANE4) {
+        hc_n = min((uint32_t)kHCache, sc.num_hnodes);
+        const uint4* src = (const uint4*)sc.hnodes;
+        for (uint32_t i = threadIdx.x; i < 4 * hc_n; i += blockDim.x) hcache[i] = src[i];
+        __syncthreads();
+    }
     uint32_t* cs = cstack + threadIdx.x;
     uint32_t* stk = wstack + (LANE4 ? threadIdx.x : 0);
     Counters cnt{0, 0, 0, 0, 0};
@@ -467,6 +495,10 @@ __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, 
     SphRay sp = sph_ray(ray);
     Prune pr = prune_off();
     BounceWalk<WALK> w;
+    if constexpr (LANE4) {
+        w.hc = (lds_uint4*)hcache;
+        w.hc_n = hc_n;
+    }
     w.stop();
     uint32_t pixel = 0, k = 0, base0 = 0;
     int level = 0, best_s = -1;
@@ -581,7 +613,8 @@ __global__ __launch_bounds__(256) void bounce_kernel(DevScene sc, FrameConst f, 
             uint32_t* qcs = cstack + (threadIdx.x & ~63u) + src;
             while (__ballot(has)) {
                 if (has && qw.cur != kPNone)
-                    quad_step<FAST, kWideStride, kWideStack>(sc, sr, sp, pr, qw, qstk, best_t, best_s);
+                    quad_step<FAST, kWideStride, kWideStack>(sc, sr, sp, pr, qw, qstk, best_t, best_s,
+                                                             (lds_uint4*)hcache, hc_n);
                 if (has && qw.cur == kPNone) {
                     if (shade_level(sc, f, ray, best_t, best_s, level, k, key, qcs, kWideStride, base0, pixel, out,
                                     acc, (lane & 3) == 0)) {
@@ -813,6 +846,103 @@ __global__ void camera_uv_kernel(FrameConst f, const float2* __restrict__ uv, in
     out[i] = {{f.px, f.py, f.pz}, {dx, dy, dz}};
 }
 
+// ---------------------------------------------------------------- BVH overlay
+// The debug view of bvh_visualiser.c:16-126 ('o' in main.c:323-327): every
+// node's box (pre-order, bvh_visualiser.c:110-116) as 12 projected edges
+// (draw_aabb :71-99), each drawn 5 times offset by one pixel (draw_debug_line
+// :45-68), coloured by depth (:107-110) over a cleared black screen. Later
+// lines overwrite earlier ones, so a pixel shows the LAST line (in draw
+// order) that covers it: pass 1 rasterises every line and keeps the largest
+// draw index per pixel (atomicMax), pass 2 colours. Rasterisation (SDL's
+// depends on the backend; the reference marks the view "NOT WORKING") is the
+// build's definition: Bresenham over integer endpoints, both inclusive,
+// pixels off screen skipped.
+struct OverlayConst {
+    float px, py, pz, fx, fy, fz, rx, ry, rz, ux, uy, uz;
+    float half_w, half_h;  // host: tanf (glibc) as bvh_visualiser.c:27-30
+    int width, height, max_levels;
+};
+
+// (int)x of x86 (cvttss2si): NaN and out-of-range values give INT_MIN.
+__device__ __forceinline__ int x86_trunc(float x)
+{
+    return (x > -2147483648.0f && x < 2147483648.0f) ? (int)x : INT_MIN;
+}
+
+// world_to_screen, bvh_visualiser.c:16-41 (float arithmetic, no contraction)
+__device__ __forceinline__ int2 world_to_screen(const OverlayConst& o, float x, float y, float z)
+{
+    const float tx = x - o.px, ty = y - o.py, tz = z - o.pz;
+    const float zz = tx * o.fx + ty * o.fy + tz * o.fz;
+    if (zz <= 0.1f) return make_int2(-1, -1);
+    const float xx = tx * o.rx + ty * o.ry + tz * o.rz;
+    const float yy = tx * o.ux + ty * o.uy + tz * o.uz;
+    const float sx = (xx / (zz * o.half_w * 2.0f) + 0.5f) * (float)o.width;
+    const float sy = (-yy / (zz * o.half_h * 2.0f) + 0.5f) * (float)o.height;
+    if (sx < (float)-o.width || sx > (float)(o.width * 2) || sy < (float)-o.height || sy > (float)(o.height * 2))
+        return make_int2(-1, -1);
+    return make_int2(x86_trunc(sx), x86_trunc(sy));
+}
+
+__constant__ int kBoxEdge[12][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 0}, {4, 5}, {5, 6},
+                                    {6, 7}, {7, 4}, {0, 4}, {1, 5}, {2, 6}, {3, 7}};
+__constant__ int kLineOffset[5][2] = {{0, 0}, {1, 0}, {0, 1}, {-1, 0}, {0, -1}};
+
+// one thread per (node, edge, offset): draw index (node * 12 + edge) * 5 + offset
+__global__ void overlay_lines_kernel(OverlayConst o, const mirt_node* __restrict__ nodes,
+                                     const uint8_t* __restrict__ ndepth, uint32_t count, uint32_t* __restrict__ last)
+{
+    const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= count) return;
+    const uint32_t node = id / 60, edge = (id / 5) % 12, off = id % 5;
+    if (o.max_levels >= 0 && ndepth[node] >= o.max_levels) return;
+    const mirt_node nd = nodes[node];
+    auto corner = [&](int k) {  // draw_aabb's corner order (:73-82)
+        const int hx = (k == 1 || k == 2 || k == 5 || k == 6), hy = (k == 2 || k == 3 || k == 6 || k == 7), hz = k >= 4;
+        return world_to_screen(o, hx ? nd.bmax[0] : nd.bmin[0], hy ? nd.bmax[1] : nd.bmin[1],
+                               hz ? nd.bmax[2] : nd.bmin[2]);
+    };
+    const int2 a = corner(kBoxEdge[edge][0]), b = corner(kBoxEdge[edge][1]);
+    if (a.x == -1 || b.x == -1) return;  // :49 (tests x only)
+    const int W = o.width, H = o.height;
+    if (!(a.x >= -W && a.x <= W * 2 && a.y >= -H && a.y <= H * 2 && b.x >= -W && b.x <= W * 2 && b.y >= -H &&
+          b.y <= H * 2))
+        return;  // :51-54
+    int x0 = a.x + kLineOffset[off][0], y0 = a.y + kLineOffset[off][1];
+    const int x1 = b.x + kLineOffset[off][0], y1 = b.y + kLineOffset[off][1];
+    const uint32_t tag = id + 1;
+    const int dx = abs(x1 - x0), dy = -abs(y1 - y0), sx = x0 < x1 ? 1 : -1, sy = y0 < y1 ? 1 : -1;
+    int err = dx + dy;
+    for (;;) {
+        if (x0 >= 0 && x0 < W && y0 >= 0 && y0 < H) atomicMax(&last[(size_t)y0 * W + x0], tag);
+        if (x0 == x1 && y0 == y1) break;
+        const int e2 = 2 * err;
+        if (e2 >= dy) {
+            err += dy;
+            x0 += sx;
+        }
+        if (e2 <= dx) {
+            err += dx;
+            y0 += sy;
+        }
+    }
+}
+
+__global__ void overlay_colour_kernel(const uint32_t* __restrict__ last, const uint8_t* __restrict__ ndepth,
+                                      size_t n, uint32_t* __restrict__ out)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t v = last[i];
+    uint32_t c = 0xff000000u;  // SDL_RenderClear with (0, 0, 0, 255), main.c:342-343
+    if (v) {
+        const uint32_t d = ndepth[(v - 1) / 60];
+        const uint32_t r = 255 - (d * 40) % 200, g = (d * 80) % 200, b = (d * 120) % 200;  // :107-110
+        c = r | g << 8 | b << 16 | 180u << 24;
+    }
+    out[i] = c;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ context
@@ -859,6 +989,10 @@ struct mirt_ctx {
     HNode* d_hnodes = nullptr;  // four-wide layout (per-lane walks)
     HAux* d_haux = nullptr;
     LeafRec* d_leaves = nullptr;
+    uint32_t num_hnodes = 0;
+    uint8_t* d_ndepth = nullptr;  // depth of every flat node (BVH overlay colours)
+    uint32_t* d_overlay = nullptr;  // BVH overlay: per-pixel last line in draw order
+    size_t overlay_cap = 0;
     float r_max = 0.0f, c_max = 0.0f;
     int bounce_threshold = 32;  // wavefront: shade finished rays once fewer lanes walk
     int bounce_blocks = 0;      // wavefront: persistent workgroups (set in mirt_create)
@@ -1092,7 +1226,8 @@ DevScene dev_scene(const mirt_ctx* c)
     const bool prune = c->prune && c->prune_ok;
     const bool ordered = prune && c->ordered && c->ordered_ok && c->fast_slab;
     return DevScene{c->d_nodes, c->d_nodes32, c->d_geo, c->d_color, (uint32_t)c->num_nodes, c->num_spheres,
-                    prune, c->r_max, c->c_max, c->d_pnodes, ordered, c->d_hnodes, c->d_haux, c->d_leaves, ordered};
+                    prune, c->r_max, c->c_max, c->d_pnodes, ordered, c->d_hnodes, c->d_haux, c->d_leaves, ordered,
+                    ordered ? c->num_hnodes : 0u};
 }
 
 bool ctx_ok(mirt_ctx* c, bool need_scene, const char* fn)
@@ -1301,7 +1436,8 @@ void mirt_destroy(mirt_ctx* c)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : {(void*)c->d_nodes, (void*)c->d_nodes32, (void*)c->d_geo, (void*)c->d_color, (void*)c->d_out, (void*)c->d_acc,
                     c->d_in, c->d_res, (void*)c->d_counts, (void*)c->d_defer, c->d_queue, (void*)c->d_keys, (void*)c->d_pnodes,
-                    (void*)c->d_hnodes, (void*)c->d_haux, (void*)c->d_leaves})
+                    (void*)c->d_hnodes, (void*)c->d_haux, (void*)c->d_leaves, (void*)c->d_ndepth,
+                    (void*)c->d_overlay})
         if (p) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -1332,8 +1468,9 @@ try {
     geo[ns] = make_float4(NAN, NAN, NAN, NAN);  // &spheres[N] sentinel: never hits
     col[ns] = 0xff000000u;
     for (void* p : {(void*)c->d_nodes, (void*)c->d_nodes32, (void*)c->d_geo, (void*)c->d_color, (void*)c->d_pnodes,
-                    (void*)c->d_hnodes, (void*)c->d_haux, (void*)c->d_leaves})
+                    (void*)c->d_hnodes, (void*)c->d_haux, (void*)c->d_leaves, (void*)c->d_ndepth})
         if (p) (void)hipFree(p);
+    c->d_ndepth = nullptr;
     c->d_pnodes = nullptr;
     c->d_hnodes = nullptr;
     c->d_haux = nullptr;
@@ -1377,8 +1514,20 @@ try {
     HIP_TRY(hipMemcpy(c->d_hnodes, hn.data(), sizeof(HNode) * hn.size(), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_haux, hx.data(), sizeof(HAux) * hx.size(), hipMemcpyHostToDevice));
     if (!lr.empty()) HIP_TRY(hipMemcpy(c->d_leaves, lr.data(), sizeof(LeafRec) * lr.size(), hipMemcpyHostToDevice));
+    // node depths (pre-order: the children of inner node i are i + 1 and the
+    // left subtree's skip), clamped to 255 -- the overlay's colour key
+    std::vector<uint8_t> ndepth((size_t)std::max(nn, 1), 0);
+    for (int i = 0; i < nn; i++) {
+        if (nodes[i].sphere >= 0) continue;
+        const uint8_t d = ndepth[i] == 255 ? 255 : (uint8_t)(ndepth[i] + 1);
+        ndepth[i + 1] = d;
+        ndepth[nodes[i + 1].skip & MIRT_SKIP_MASK] = d;
+    }
+    HIP_TRY(hipMalloc((void**)&c->d_ndepth, ndepth.size()));
+    HIP_TRY(hipMemcpy(c->d_ndepth, ndepth.data(), ndepth.size(), hipMemcpyHostToDevice));
     c->num_nodes = nn;
     c->num_spheres = ns;
+    c->num_hnodes = (uint32_t)hn.size();
     c->ordered_ok = ordered;
     c->prune_ok = encloses;
     c->r_max = r_max;
@@ -1703,6 +1852,47 @@ int mirt_any_hit_rays(mirt_ctx* c, const mirt_ray* rays, int n, int use_bvh, int
     HIP_TRY(hipMemcpyAsync(out, c->d_res, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     HIP_TRY(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+    return MIRT_OK;
+}
+
+int mirt_bvh_overlay(mirt_ctx* c, const mirt_camera* cam, int width, int height, int max_levels, mirt_rgba8* out)
+{
+    if (!ctx_ok(c, true, "mirt_bvh_overlay")) return MIRT_E_NOSCENE;
+    if (!cam || width <= 0 || height <= 0 || !out || (size_t)width * height > ((size_t)1 << 31)) {
+        set_error("mirt_bvh_overlay: invalid arguments");
+        return MIRT_E_INVALID;
+    }
+    OverlayConst o{};
+    o.px = cam->position.x; o.py = cam->position.y; o.pz = cam->position.z;
+    o.fx = cam->forward.x; o.fy = cam->forward.y; o.fz = cam->forward.z;
+    o.rx = cam->right.x; o.ry = cam->right.y; o.rz = cam->right.z;
+    o.ux = cam->up.x; o.uy = cam->up.y; o.uz = cam->up.z;
+    const float fov_rad = (float)((double)cam->fov * (M_PI / 180.0));  // bvh_visualiser.c:26
+    o.half_h = tanf(fov_rad / 2.0f);                                    // :27 (float tanf)
+    o.half_w = (float)width / (float)height * o.half_h;                 // :28-29
+    o.width = width;
+    o.height = height;
+    o.max_levels = max_levels;
+    const size_t pixels = (size_t)width * height;
+    int rc = ensure((void**)&c->d_overlay, &c->overlay_cap, 4 * pixels);
+    if (!rc) rc = ensure((void**)&c->d_out, &c->out_cap, 4 * pixels + 4);
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(c->d_overlay, 0, 4 * pixels, c->stream));
+    const uint64_t lines = (uint64_t)c->num_nodes * 60;
+    if (lines > 0xffffffffull) {
+        set_error("mirt_bvh_overlay: too many nodes");
+        return MIRT_E_INVALID;
+    }
+    if (lines) {
+        overlay_lines_kernel<<<(unsigned)((lines + 255) / 256), 256, 0, c->stream>>>(o, c->d_nodes32, c->d_ndepth,
+                                                                                     (uint32_t)lines, c->d_overlay);
+        HIP_TRY(hipGetLastError());
+    }
+    overlay_colour_kernel<<<(unsigned)((pixels + 255) / 256), 256, 0, c->stream>>>(c->d_overlay, c->d_ndepth, pixels,
+                                                                                 c->d_out);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(out, c->d_out, 4 * pixels, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
     return MIRT_OK;
 }
 

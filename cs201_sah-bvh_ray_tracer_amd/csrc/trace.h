@@ -117,7 +117,17 @@ struct DevScene {
     const HAux* haux;
     const LeafRec* leaves;
     int wide;
+    uint32_t num_hnodes;  // HNodes, numbered breadth-first: the first ones are the top levels
 };
+
+// LDS-resident node data (address space 3: ds_read, never a flat load)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const u32x4 lds_uint4;
+__device__ __forceinline__ uint4 lds_load(lds_uint4* p)
+{
+    const u32x4 v = *p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
 
 struct Ray {
     float ox, oy, oz, dx, dy, dz;
@@ -894,22 +904,46 @@ __device__ __forceinline__ float h_hi(uint32_t v) { return (float)__builtin_bit_
 
 // The leaf gate of a leaf slot whose fp16 box passed: its exact box under
 // hit.c's test, then its sphere. COUNT: the sphere test counts.
+//
+// The gate's outcome is (box passes) AND (sphere hit that wins), so the
+// timed build tests the sphere first and reads the exact box (32 of the
+// record's 48 B) only for a winning hit -- rare: most gates end at the
+// sphere. Same box test, same prune state, same result; COUNT keeps the
+// reference's order so the box-gated sphere tests are what it counts.
 template <bool FAST, bool COUNT>
 __device__ __forceinline__ void wide_leaf(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
                                           uint32_t ref, float& best_t, int& best_s, Counters& cnt)
 {
     const float4* lp = (const float4*)(sc.leaves + (ref & ~kPLeaf));
-    const float4 l0 = lp[0], l1 = lp[1], g = lp[2];
     float e;
-    if (slab_box<FAST>(sr, pr, l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, e)) {
-        if (COUNT) cnt.spheres++;
-        consider_sphere<FAST>(sc, sp, pr, sr.ox, sr.oy, sr.oz, __float_as_int(l1.z), g, best_t, best_s);
+    if constexpr (COUNT) {
+        const float4 l0 = lp[0], l1 = lp[1], g = lp[2];
+        if (slab_box<FAST>(sr, pr, l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, e)) {
+            cnt.spheres++;
+            consider_sphere<FAST>(sc, sp, pr, sr.ox, sr.oy, sr.oz, __float_as_int(l1.z), g, best_t, best_s);
+        }
+    } else {
+        const float t = sphere_t<FAST>(sp, lp[2], best_t);
+        if (t > 0.0f) {
+            const float4 l0 = lp[0], l1 = lp[1];
+            const int si = __float_as_int(l1.z);
+            if ((t < best_t || si > best_s) && slab_box<FAST>(sr, pr, l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, e)) {
+                best_t = t;
+                best_s = si;
+                if (sc.prune) prune_update(pr, sc, sr.ox, sr.oy, sr.oz, sp.a4, t);
+            }
+        }
     }
 }
 
+// hc / hc_n: the first hc_n HNodes (the tree's top levels, visited by
+// every ray) staged in LDS by the caller; a node there is read from LDS
+// instead of through the vector-memory path (the bounce kernel's busiest
+// unit, TD: its cost is the bytes returned per lane, however coalesced).
 template <bool FAST, bool COUNT>
 __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
-                                               WideWalk& w, uint32_t* stk, float& best_t, int& best_s, Counters& cnt)
+                                               WideWalk& w, uint32_t* stk, float& best_t, int& best_s, Counters& cnt,
+                                               lds_uint4* hc = nullptr, uint32_t hc_n = 0)
 {
     if (COUNT) cnt.steps++;
     if (w.end) {
@@ -926,8 +960,20 @@ __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay
     bool h0, h1, h2, h3;
     uint4 q3;  // the slots' references
     {
-        const uint4* p = (const uint4*)(sc.hnodes + w.cur);
-        const uint4 s0 = p[0], s1 = p[1], s2 = p[2], s3 = p[3];
+        uint4 s0, s1, s2, s3;
+        if (w.cur < hc_n) {
+            lds_uint4* p = hc + 4 * w.cur;
+            s0 = lds_load(p);
+            s1 = lds_load(p + 1);
+            s2 = lds_load(p + 2);
+            s3 = lds_load(p + 3);
+        } else {
+            const uint4* p = (const uint4*)(sc.hnodes + w.cur);
+            s0 = p[0];
+            s1 = p[1];
+            s2 = p[2];
+            s3 = p[3];
+        }
         auto test = [&](const uint4& q, float& e) {
             if (COUNT && q.w != kPNone) cnt.nodes++;
             const bool pass = slab_cons(sr, pr, h_lo(q.x), h_lo(q.y), h_lo(q.z), h_hi(q.x), h_hi(q.y), h_hi(q.z), e);
@@ -1029,7 +1075,8 @@ __device__ __forceinline__ void cand_merge(float& t, int& si)
 // `stk`: this ray's LDS stack column (entry k at stk[k * STRIDE], CAP entries).
 template <bool FAST, int STRIDE, int CAP>
 __device__ __forceinline__ void quad_step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
-                                          QuadWalk& w, uint32_t* stk, float& best_t, int& best_s)
+                                          QuadWalk& w, uint32_t* stk, float& best_t, int& best_s,
+                                          lds_uint4* hc = nullptr, uint32_t hc_n = 0)
 {
     Counters cnt{0, 0, 0, 0, 0};
     if (w.end) {  // DFS segment (the stack was full): every lane of the quad walks it alike
@@ -1046,20 +1093,24 @@ __device__ __forceinline__ void quad_step(const DevScene& sc, const SlabRay& sr,
         return;
     }
     const uint32_t j = threadIdx.x & 3;
-    const uint4 q = ((const uint4*)(sc.hnodes + w.cur))[j];
+    uint4 q;
+    if (w.cur < hc_n)
+        q = lds_load(hc + 4 * w.cur + j);
+    else
+        q = ((const uint4*)(sc.hnodes + w.cur))[j];
     float e = 0.0f;
     const bool pass = slab_cons(sr, pr, h_lo(q.x), h_lo(q.y), h_lo(q.z), h_hi(q.x), h_hi(q.y), h_hi(q.z), e) &
                       (q.w != kPNone);
     // a passing leaf: its exact gate and sphere give this lane's candidate
     float ct = INFINITY;
     int cs = -1;
-    if (pass && (q.w & kPLeaf)) {
+    if (pass && (q.w & kPLeaf)) {  // sphere first, the exact box only for a hit (wide_leaf)
         const float4* lp = (const float4*)(sc.leaves + (q.w & ~kPLeaf));
-        const float4 l0 = lp[0], l1 = lp[1], g = lp[2];
-        float ee;
-        if (slab_box<FAST>(sr, pr, l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, ee)) {
-            const float t = sphere_t<FAST>(sp, g, best_t);
-            if (t > 0.0f) {
+        const float t = sphere_t<FAST>(sp, lp[2], best_t);
+        if (t > 0.0f) {
+            const float4 l0 = lp[0], l1 = lp[1];
+            float ee;
+            if (slab_box<FAST>(sr, pr, l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, ee)) {
                 ct = t;
                 cs = __float_as_int(l1.z);
             }

@@ -11,7 +11,8 @@ import subprocess
 from . import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmirt.so")
+# MIRT_LIB: another build of the same ABI (A/B measurements of kernel variants)
+LIB_PATH = os.environ.get("MIRT_LIB") or os.path.join(HERE, "libmirt.so")
 _lib = None
 
 
@@ -33,7 +34,12 @@ def load():
             raise MirtError(f"{LIB_PATH} is not built: run __graft_entry__.build() or `make -C csrc`")
         L = C.CDLL(LIB_PATH)
         for name, res, args in abi.SIGNATURES:
-            f = getattr(L, name)
+            try:
+                f = getattr(L, name)
+            except AttributeError:
+                if os.environ.get("MIRT_LIB"):
+                    continue  # an older build under A/B: entry points it lacks stay unbound
+                raise
             f.restype, f.argtypes = res, args
         _lib = L
     return _lib

@@ -335,6 +335,13 @@ class Renderer:
         check(self.L.mirt_last_phase_ms(self.h, out), "mirt_last_phase_ms")
         return float(out[0]), float(out[1])
 
+    def bvh_overlay(self, cam, width, height, max_levels=-1):
+        """The BVH debug view (bvh_visualiser.c:16-126) of the uploaded tree:
+        (height, width, 4) uint8."""
+        out = np.zeros((height, width, 4), np.uint8)
+        check(self.L.mirt_bvh_overlay(self.h, C.byref(cam), width, height, max_levels, ptr(out)), "mirt_bvh_overlay")
+        return out
+
     # ---- per-ray surface (batched)
     def get_camera_rays(self, cam, width, height, row_block=8, shard=0, num_shards=1):
         fd = frame_desc(width, height, 1, True, 1, 0, False, 1, row_block, shard, num_shards)

@@ -290,6 +290,15 @@ int mirt_aabb_pairs(mirt_ctx *ctx, const mirt_ray *rays, const mirt_aabb *boxes,
 /* The camera ray of every pixel of the shard (ray.c:17-32 with the pixel
    mapping of main.c:356-365). */
 int mirt_camera_rays(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_desc *fd, mirt_ray *out);
+/* The BVH debug overlay (bvh_visualiser.c:16-126, 'o' in main.c:323-327):
+   every node of the uploaded tree with depth < max_levels (all: -1) drawn as
+   its box's 12 projected edges, 5 one-pixel-offset lines each, coloured by
+   depth, over black; a pixel shows the last line drawn over it in the
+   reference's order (pre-order nodes, draw_aabb's edge order). Lines are
+   rasterised by Bresenham between the integer endpoints of world_to_screen
+   (the reference leaves that to SDL's backend). Writes width * height RGBA8. */
+int mirt_bvh_overlay(mirt_ctx *ctx, const mirt_camera *cam, int width, int height, int max_levels,
+                     mirt_rgba8 *out);
 /* get_camera_ray (ray.c:17-32) at n caller-given (u, v) pairs (uv[2i],
    uv[2i+1]), for a frame of width x height (the reference's compile-time
    WIDTH/HEIGHT, ray.c:18). */

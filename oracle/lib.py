@@ -53,6 +53,7 @@ class Oracle:
             "o_render_rows": (None, [P, I, I, P, I, P, I, I, I, C.c_uint64, C.c_uint32, P, I, P, I, P, I]),
             "o_trace_rays": (None, [P, I, P, I, P, I, I, I, C.c_uint64, C.c_uint32, P]),
             "o_accumulate": (None, [P, I, P, I, I, P]),
+            "o_bvh_overlay": (None, [P, P, I, I, I, P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -133,6 +134,12 @@ class Oracle:
             self.L.o_srand(seed)
         self.L.o_trace_rays(_p(rays), len(rays), _p(spheres), len(spheres), tree, depth, int(use_bvh),
                             mode, seed, sample, _p(out))
+        return out
+
+    def bvh_overlay(self, tree, cam, W, H, max_levels=-1):
+        """bvh_visualiser.c:16-126 on an RGBA8 canvas -> (H, W, 4) u8."""
+        out = np.zeros((H, W, 4), np.uint8)
+        self.L.o_bvh_overlay(tree, C.byref(cam), W, H, max_levels, _p(out))
         return out
 
     def accumulate(self, colors, acc, fresh, frames):

@@ -555,3 +555,86 @@ void o_accumulate(const mirt_rgba8 *color, int n, float *acc, int fresh, int fra
         }
     }
 }
+
+/* ------------------------------------------------------- BVH debug overlay */
+/* bvh_visualiser.c:16-126 restated on a W x H RGBA8 canvas cleared to
+   (0, 0, 0, 255) (main.c:342-343): draw_bvh_recursive's pre-order, draw_aabb's
+   12 edges, draw_debug_line's 5 offset lines, each a Bresenham line between
+   the integer endpoints (both inclusive, off-screen pixels skipped -- the
+   build's definition of SDL_RenderDrawLine), later lines overwriting
+   earlier ones. Nodes at depth >= max_levels are skipped (max_levels < 0:
+   none). */
+typedef struct { int x, y; } OPoint;
+
+static int o_x86_trunc(float x) { return (x > -2147483648.0f && x < 2147483648.0f) ? (int)x : INT32_MIN; }
+
+static OPoint o_world_to_screen(V3 p, const mirt_camera *cam, int W, int H, float half_w, float half_h)
+{                                                                   /* bvh_visualiser.c:16-41 */
+    OPoint none = {-1, -1};
+    V3 t = vsub(p, cam->position);
+    float z = vdot(t, cam->forward);
+    if (z <= 0.1f) return none;
+    float x = vdot(t, cam->right);
+    float y = vdot(t, cam->up);
+    float sx = (x / (z * half_w * 2.0f) + 0.5f) * (float)W;
+    float sy = (-y / (z * half_h * 2.0f) + 0.5f) * (float)H;
+    if (sx < (float)-W || sx > (float)(W * 2) || sy < (float)-H || sy > (float)(H * 2)) return none;
+    OPoint r = {o_x86_trunc(sx), o_x86_trunc(sy)};
+    return r;
+}
+
+static void o_plot_line(mirt_rgba8 *img, int W, int H, int x0, int y0, int x1, int y1, mirt_rgba8 c)
+{
+    int dx = abs(x1 - x0), dy = -abs(y1 - y0), sx = x0 < x1 ? 1 : -1, sy = y0 < y1 ? 1 : -1, err = dx + dy;
+    for (;;) {
+        if (x0 >= 0 && x0 < W && y0 >= 0 && y0 < H) img[(size_t)y0 * W + x0] = c;
+        if (x0 == x1 && y0 == y1) break;
+        int e2 = 2 * err;
+        if (e2 >= dy) { err += dy; x0 += sx; }
+        if (e2 <= dx) { err += dx; y0 += sy; }
+    }
+}
+
+static void o_overlay_rec(const ONode *nd, const mirt_camera *cam, int W, int H, float hw, float hh, int depth,
+                          int max_levels, mirt_rgba8 *img)
+{
+    static const int edge[12][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 0}, {4, 5}, {5, 6},
+                                    {6, 7}, {7, 4}, {0, 4}, {1, 5}, {2, 6}, {3, 7}};
+    static const int off[5][2] = {{0, 0}, {1, 0}, {0, 1}, {-1, 0}, {0, -1}};
+    if (!nd) return;
+    if (max_levels < 0 || depth < max_levels) {
+        mirt_rgba8 c;                                               /* bvh_visualiser.c:107-110 */
+        c.r = (uint8_t)(255 - (depth * 40) % 200);
+        c.g = (uint8_t)((depth * 80) % 200);
+        c.b = (uint8_t)((depth * 120) % 200);
+        c.a = 180;
+        const mirt_aabb *b = &nd->box;
+        V3 k[8] = {v3(b->min.x, b->min.y, b->min.z), v3(b->max.x, b->min.y, b->min.z),
+                   v3(b->max.x, b->max.y, b->min.z), v3(b->min.x, b->max.y, b->min.z),
+                   v3(b->min.x, b->min.y, b->max.z), v3(b->max.x, b->min.y, b->max.z),
+                   v3(b->max.x, b->max.y, b->max.z), v3(b->min.x, b->max.y, b->max.z)};
+        for (int e = 0; e < 12; e++) {                              /* draw_aabb :84-98 */
+            OPoint s = o_world_to_screen(k[edge[e][0]], cam, W, H, hw, hh);
+            OPoint t = o_world_to_screen(k[edge[e][1]], cam, W, H, hw, hh);
+            if (s.x == -1 || t.x == -1) continue;                   /* draw_debug_line :49 */
+            if (!(s.x >= -W && s.x <= W * 2 && s.y >= -H && s.y <= H * 2 && t.x >= -W && t.x <= W * 2 &&
+                  t.y >= -H && t.y <= H * 2))
+                continue;
+            for (int o = 0; o < 5; o++)                             /* :56-67 */
+                o_plot_line(img, W, H, s.x + off[o][0], s.y + off[o][1], t.x + off[o][0], t.y + off[o][1], c);
+        }
+    }
+    if (nd->first < 0) {                                            /* :115-116 */
+        o_overlay_rec(nd->kid[0], cam, W, H, hw, hh, depth + 1, max_levels, img);
+        o_overlay_rec(nd->kid[1], cam, W, H, hw, hh, depth + 1, max_levels, img);
+    }
+}
+
+void o_bvh_overlay(void *root, const mirt_camera *cam, int W, int H, int max_levels, mirt_rgba8 *img)
+{
+    for (size_t i = 0; i < (size_t)W * H; i++) { img[i].r = img[i].g = img[i].b = 0; img[i].a = 255; }
+    float fov_rad = (float)((double)cam->fov * (M_PI / 180.0));    /* bvh_visualiser.c:26-29 */
+    float hh = tanf(fov_rad / 2.0f);
+    float hw = (float)W / (float)H * hh;
+    o_overlay_rec((const ONode *)root, cam, W, H, hw, hh, 0, max_levels, img);
+}
