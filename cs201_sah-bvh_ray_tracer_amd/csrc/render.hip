@@ -300,7 +300,8 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask)
 #ifndef MIRT_HCACHE
 #define MIRT_HCACHE 96
 #endif
-constexpr uint32_t kHCache = MIRT_HCACHE;  // HNodes staged in LDS per bounce workgroup (64 B each)
+constexpr uint32_t kHCache = MIRT_HCACHE;
+constexpr int kBounceDiag = 10;  // mirt_bounce_stats words per wave  // HNodes staged in LDS per bounce workgroup (64 B each)
 
 // First bounce of one pixel, produced by primary_kernel.
 struct BounceRec {
@@ -466,7 +467,7 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                                                      uint32_t* __restrict__ qctl, int threshold, int quad_drain,
                                                      uint64_t* __restrict__ diag = nullptr)
 {
-    uint64_t dg_it = 0, dg_lanes = 0, dg_it_x = 0, dg_lanes_x = 0, dg_tx = 0;
+    uint64_t dg_it = 0, dg_lanes = 0, dg_it_x = 0, dg_lanes_x = 0, dg_tx = 0, dg_qit = 0, dg_tq = 0;
     const uint64_t dg_t0 = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
     uint32_t dg_steps = 0, dg_chain = 0, dg_walk_max = 0, dg_chain_max = 0;
     constexpr bool LANE4 = WALK == 2;  // four-wide, one ray per lane
@@ -611,7 +612,9 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
             // the ray's LDS stacks stay in its source lane's columns
             uint32_t* qstk = wstack + (threadIdx.x & ~63u) + src;
             uint32_t* qcs = cstack + (threadIdx.x & ~63u) + src;
+            if (DIAG) dg_tq = __builtin_amdgcn_s_memrealtime();
             while (__ballot(has)) {
+                if (DIAG) dg_qit++;
                 if (has && qw.cur != kPNone)
                     quad_step<FAST, kWideStride, kWideStack>(sc, sr, sp, pr, qw, qstk, best_t, best_s,
                                                              (lds_uint4*)hcache, hc_n);
@@ -637,7 +640,7 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
             dg_chain_max = max(dg_chain_max, (uint32_t)__shfl_xor((int)dg_chain_max, o));
         }
         if ((threadIdx.x & 63) == 0) {
-            uint64_t* d = diag + 8 * (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+            uint64_t* d = diag + kBounceDiag * (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
             d[0] = dg_it;
             d[1] = dg_lanes;
             d[2] = dg_it_x;
@@ -646,6 +649,8 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
             d[5] = dg_tx;
             d[6] = __builtin_amdgcn_s_memrealtime();
             d[7] = ((uint64_t)dg_chain_max << 32) | dg_walk_max;
+            d[8] = dg_qit;
+            d[9] = dg_tq;
         }
     }
 }
@@ -1705,15 +1710,17 @@ int mirt_bounce_stats(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc
     }
     const int waves = (c->bounce_blocks_opt ? c->bounce_blocks_opt : c->bounce_blocks) * 4;
     if (!out || cap < waves) return -waves;
+    static_assert(kBounceDiag == 10, "mirt.h documents 10 words per wave");
     FrameConst f = make_frame_const(cam, fd);
     f.accumulate = 0;
     const size_t pixels = (size_t)f.num_rows * f.width;
     int rc = ensure((void**)&c->d_out, &c->out_cap, pixels * 4 + 4);
-    if (!rc) rc = ensure(&c->d_res, &c->res_cap, 64 * (size_t)waves + 64);
+    if (!rc) rc = ensure(&c->d_res, &c->res_cap, 8 * kBounceDiag * (size_t)waves + 64);
     if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(c->d_res, 0, 8 * kBounceDiag * (size_t)waves, c->stream));
     rc = launch_render(c, f, c->d_out, nullptr, c->stream, false, nullptr, nullptr, (uint64_t*)c->d_res);
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(out, c->d_res, 64 * (size_t)waves, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(out, c->d_res, 8 * kBounceDiag * (size_t)waves, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return waves;
 }

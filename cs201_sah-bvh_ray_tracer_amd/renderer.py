@@ -298,15 +298,16 @@ class Renderer:
     def get_option(self, option):
         return check(self.L.mirt_get_option(self.h, option), "mirt_get_option")
 
-    def bounce_stats(self, cam, width, height, depth=5, seed=1, sample=0):
+    def bounce_stats(self, cam, width, height, depth=5, seed=1, sample=0, shard=0, num_shards=1):
         """Per-wave diagnostic of the bounce kernel: uint64 array of (iterations,
         walking lanes summed, iterations after the queue ran dry, their lanes,
-        t_start, t_dry, t_end [10 ns ticks], longest chain << 32 | longest walk)."""
-        fd = frame_desc(width, height, depth, True, seed, sample, False, 1, 8, 0, 1)
+        t_start, t_dry, t_end [10 ns ticks], longest chain << 32 | longest walk,
+        quad-drain iterations, t_quad_start)."""
+        fd = frame_desc(width, height, depth, True, seed, sample, False, 1, 8, shard, num_shards)
         n = -self.L.mirt_bounce_stats(self.h, C.byref(cam), C.byref(fd), None, 0)
         if n <= 0:
             check(-n, "mirt_bounce_stats")
-        out = np.zeros((n, 8), np.uint64)
+        out = np.zeros((n, 10), np.uint64)
         check(self.L.mirt_bounce_stats(self.h, C.byref(cam), C.byref(fd), ptr(out), n), "mirt_bounce_stats")
         return out
 
