@@ -328,6 +328,8 @@ def main():
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
                     help="weak: N frames in flight per step at N GPUs (default); strong: one frame split N ways")
     ap.add_argument("--dry", action="store_true", help="CPU plumbing check over gloo (no GPU, no measurement)")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="OPTION=VALUE (mirt_set_option on every context; A/B of schedule options), repeatable")
     args = ap.parse_args()
     global W, H, NSPH, KIND, SPP, JITTER
     wl = WORKLOADS[args.workload]
@@ -358,6 +360,9 @@ def main():
     rs = [mirt.Renderer(dev) for _ in range(max(1, args.pipeline))]
     for x in rs:
         x.upload(spheres, bvh)
+        for ov in args.opt:
+            o, v = (int(t) for t in ov.split("="))
+            x.set_option(o, v)
     r = rs[0]
     cam = mirt.default_camera()
     # frames (accumulated samples) in flight per step: SPP per frame x N at N GPUs (weak scaling)
@@ -506,6 +511,8 @@ def main():
             "depth1_mrays_s": round(W * H * frames * args.steps / elapsed_d1 / 1e6, 3),
             "bvh_build_s": round(build_s, 4),
         }
+        if args.opt:
+            line["options"] = args.opt
         if elapsed_other:
             other = W * H * frames_other * args.steps / elapsed_other / 1e6
             line["value_weak"] = round(value if args.scaling == "weak" else other, 3)
