@@ -10,6 +10,7 @@
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <vector>
 
 #include "../../include/mirt_dropin.h"
 #include "internal.h"
@@ -57,16 +58,20 @@ int bind(DropinState& s, const mirt_sphere* sp, int ns, const mirt_bvh_node* roo
 
 // Lowest and highest leaf sphere pointer of a pointer tree (bvh.c:131-137:
 // every leaf, empty ones included, points into the build's array).
-void leaf_range(const mirt_bvh_node* n, const mirt_sphere** lo, const mirt_sphere** hi)
+void leaf_range(const mirt_bvh_node* root, const mirt_sphere** lo, const mirt_sphere** hi)
 {
-    while (n) {
+    std::vector<const mirt_bvh_node*> todo{root};  // explicit stack: any tree depth
+    while (!todo.empty()) {
+        const mirt_bvh_node* n = todo.back();
+        todo.pop_back();
+        if (!n) continue;
         if (n->sphere) {
             if (!*lo || n->sphere < *lo) *lo = n->sphere;
             if (!*hi || n->sphere > *hi) *hi = n->sphere;
-            return;
+            continue;
         }
-        leaf_range(n->left, lo, hi);
-        n = n->right;
+        todo.push_back(n->right);
+        todo.push_back(n->left);
     }
 }
 
@@ -223,6 +228,10 @@ mirt_hit_record mirt_ray_bvh_intersect(mirt_ray ray, mirt_bvh_node* node)
             // a tree seen without its sphere array: the leaves span it
             const mirt_sphere *lo = nullptr, *hi = nullptr;
             leaf_range(node, &lo, &hi);
+            if (!lo) {
+                mirt::set_error("mirt_ray_bvh_intersect: tree without leaves");
+                return (int)MIRT_E_INVALID;
+            }
             if (int r = bind(s, lo, (int)(hi - lo) + 1, node)) return r;
         }
         base = s.spheres;
