@@ -4,6 +4,8 @@
 # pass runs under its own kill timeout and stays within 8 SQ / 4 TCC / 4 TCP /
 # 2 TA / 2 TD / 2 GRBM counters):
 #   scripts/pmc_probe.sh <tag> "<trav> <fast> <depth>" ...
+# PROBE_ARGS (environment): more scripts/profile_kernel.py arguments, e.g.
+#   PROBE_ARGS="--scene bench1000000 --W 3840 --H 2160"
 # Summarise with scripts/pmc_summary.py gpurun_out/<tag> [--json out.json].
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -28,7 +30,7 @@ for cfg in "$@"; do
   for cs in "${SETS[@]}"; do
     i=$((i+1))
     timeout -s KILL 90 rocprofv3 --pmc $cs --output-format csv -d "$OUT/$tag.$i" -o run -- \
-        python3 scripts/profile_kernel.py --trav $1 --fast $2 --depth $3 --frames 3 > "$OUT/$tag.$i.log" 2>&1
+        python3 scripts/profile_kernel.py --trav $1 --fast $2 --depth $3 --frames 3 ${PROBE_ARGS:-} > "$OUT/$tag.$i.log" 2>&1
     rc=$?
     if [ $rc -ne 0 ]; then echo "$tag set $i rc=$rc"; grep -m2 -i "error" "$OUT/$tag.$i.log"; [ $rc -gt 1 ] && exit $rc; fi
   done
