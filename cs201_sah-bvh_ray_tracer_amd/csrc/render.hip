@@ -1079,6 +1079,31 @@ bool tree_encloses(const mirt_sphere* sp, int ns, const mirt_node* nd, int nn, f
     return true;
 }
 
+// A leaf that can never report a hit: a 0-sphere leaf (its sphere is tested
+// by a real leaf under the same ancestors) or the &spheres[N] sentinel.
+bool dead_leaf(const mirt_node* nd, uint32_t i, int ns)
+{
+    return nd[i].sphere >= 0 && ((nd[i].skip & MIRT_NODE_EMPTY) || nd[i].sphere >= ns);
+}
+
+// The node a walk may take in place of flat node ci: an inner node one of
+// whose children is dead adds nothing but its box test, which its live
+// child's (nested, hence stricter) box test implies -- so the chains of
+// one-sided splits the reference's SAH fallback builds (bvh.c:139-141,
+// runs of nodes each with a 0-sphere leaf beside the rest of the range)
+// collapse to the subtree that can hit. kPNone: nothing below can hit.
+uint32_t live_node(const mirt_node* nd, uint32_t ci, int ns)
+{
+    for (;;) {
+        if (nd[ci].sphere >= 0) return dead_leaf(nd, ci, ns) ? kPNone : ci;
+        const uint32_t l = ci + 1, r = nd[ci + 1].skip & MIRT_SKIP_MASK;
+        const bool dl = dead_leaf(nd, l, ns), dr = dead_leaf(nd, r, ns);
+        if (dl && dr) return kPNone;
+        if (!dl && !dr) return ci;
+        ci = dl ? r : l;
+    }
+}
+
 // PNode layout (trace.h) of a validated flat tree. Returns whether ordered
 // walks may use it: hit-able leaves must carry strictly increasing sphere
 // indices in DFS order (then the index is hit.c:108's tie key -- true of the
@@ -1092,7 +1117,15 @@ bool build_pnodes(const mirt_node* nd, int nn, int ns, std::vector<PNode>& pn)
     for (int i = 0; i < nn; i++)
         if (nd[i].sphere < 0) pidx[i] = np++;
     pn.assign(np, PNode{});
-    auto set_child = [&](PNode& p, int k, uint32_t ci) {
+    auto set_child = [&](PNode& p, int k, uint32_t c) {
+        const uint32_t ci = live_node(nd, c, ns);
+        if (ci == kPNone) {  // nothing below can hit: an empty slot
+            float* slot = k ? p.c1 : p.c0;
+            std::memcpy(slot, nd[c].bmin, sizeof nd[c].bmin);
+            std::memcpy(slot + 3, nd[c].bmax, sizeof nd[c].bmax);
+            (k ? p.ref1 : p.ref0) = kPNone;
+            return;
+        }
         const mirt_node& n = nd[ci];
         float* slot = k ? p.c1 : p.c0;
         uint32_t ref = pidx[ci];
@@ -1175,9 +1208,13 @@ void build_hnodes(const mirt_node* nd, int nn, const mirt_sphere* sp, int ns, st
     aux.assign(1, HAux{0xffffffffu, (uint32_t)nn});  // flat + 1 == 0: the whole tree
     leaves.clear();
     std::vector<uint32_t> todo;  // inner nodes waiting for their HNode: HNode 1 + i is todo[i]
-    auto fill = [&](size_t hi, int k, uint32_t ci) {
+    auto fill = [&](size_t hi, int k, uint32_t c) {
         HNode& h = hn[hi];
-        src[4 * hi + k] = ci;
+        const uint32_t ci = live_node(nd, c, ns);
+        if (ci == kPNone) {
+            h.slot[k].ref = kPNone;
+            return;
+        }
         const mirt_node& n = nd[ci];
         for (int a = 0; a < 3; a++)
             h.slot[k].box[a] = (uint32_t)half_down(n.bmin[a]) | ((uint32_t)half_up(n.bmax[a]) << 16);
@@ -1213,9 +1250,13 @@ void build_hnodes(const mirt_node* nd, int nn, const mirt_sphere* sp, int ns, st
         hn.push_back(h);
         src.resize(4 * hn.size(), kPNone);
         aux.push_back(HAux{y, nd[y].skip & MIRT_SKIP_MASK});
-        const uint32_t kids[2] = {y + 1, nd[y + 1].skip & MIRT_SKIP_MASK};
+        const uint32_t kids[2] = {live_node(nd, y + 1, ns), live_node(nd, nd[y + 1].skip & MIRT_SKIP_MASK, ns)};
         int k = 0;
         for (uint32_t c : kids) {
+            if (c == kPNone) {
+                k++;  // an empty slot (ref kPNone already)
+                continue;
+            }
             if (nd[c].sphere < 0 && !(nd[c].skip & MIRT_NODE_EMPTY)) {
                 fill(hn.size() - 1, k++, c + 1);
                 fill(hn.size() - 1, k++, nd[c + 1].skip & MIRT_SKIP_MASK);
