@@ -1250,20 +1250,37 @@ void build_hnodes(const mirt_node* nd, int nn, const mirt_sphere* sp, int ns, st
         hn.push_back(h);
         src.resize(4 * hn.size(), kPNone);
         aux.push_back(HAux{y, nd[y].skip & MIRT_SKIP_MASK});
-        const uint32_t kids[2] = {live_node(nd, y + 1, ns), live_node(nd, nd[y + 1].skip & MIRT_SKIP_MASK, ns)};
-        int k = 0;
-        for (uint32_t c : kids) {
-            if (c == kPNone) {
-                k++;  // an empty slot (ref kPNone already)
-                continue;
+        // the four slots: y's live children, then the inner slot with the
+        // largest box replaced by its two live children while a slot is
+        // free (every slot stays inside y's flat subtree, which HAux walks)
+        uint32_t cut[4];
+        int m = 0;
+        auto add = [&](uint32_t c) {
+            const uint32_t ci = live_node(nd, c, ns);
+            if (ci != kPNone) cut[m++] = ci;
+        };
+        add(y + 1);
+        add(nd[y + 1].skip & MIRT_SKIP_MASK);
+        while (m < 4) {
+            int best = -1;
+            float best_area = -1.0f;
+            for (int j = 0; j < m; j++) {
+                const mirt_node& n = nd[cut[j]];
+                if (n.sphere >= 0) continue;
+                const float dx = n.bmax[0] - n.bmin[0], dy = n.bmax[1] - n.bmin[1], dz = n.bmax[2] - n.bmin[2];
+                const float area = dx * dy + dy * dz + dz * dx;
+                if (area > best_area || best < 0) {
+                    best = j;
+                    best_area = area;
+                }
             }
-            if (nd[c].sphere < 0 && !(nd[c].skip & MIRT_NODE_EMPTY)) {
-                fill(hn.size() - 1, k++, c + 1);
-                fill(hn.size() - 1, k++, nd[c + 1].skip & MIRT_SKIP_MASK);
-            } else {
-                fill(hn.size() - 1, k++, c);
-            }
+            if (best < 0) break;
+            const uint32_t c = cut[best];
+            cut[best] = cut[--m];
+            add(c + 1);
+            add(nd[c + 1].skip & MIRT_SKIP_MASK);
         }
+        for (int k = 0; k < m; k++) fill(hn.size() - 1, k, cut[k]);
     }
 }
 
