@@ -335,10 +335,27 @@ __global__ __launch_bounds__(256) void primary_kernel(DevScene sc, FrameConst f,
         return;
     }
     const int tile = (blockIdx.x - dfr.blocks) * 4 + wave;
-    const int tiles_x = (f.width + 7) >> 3;
-    const int x = (tile % tiles_x) * 8 + (lane & 7);
-    const int r = (tile / tiles_x) * 8 + (lane >> 3);
-    bool alive = x < f.width && r < f.num_rows;
+    int x, r;
+    bool alive;
+    if (ORD && f.samples >= 4) {
+        // four frames in flight or more (frames of one camera, or jittered
+        // samples of one pixel): a packet is 4x4 pixels x 4 successive frames,
+        // whose camera rays are the same or nearly so -- a quarter of an 8x8
+        // tile's footprint, so the packet's walk is the union of fewer paths
+        // (launch_render_body's ptiles counts these tiles)
+        const int txs = (f.width + 3) >> 2, tys = (f.shard_rows + 3) >> 2;
+        const int g = tile / (txs * tys), rem = tile - g * (txs * tys);
+        x = (rem % txs) * 4 + (lane & 3);
+        const int yr = (rem / txs) * 4 + ((lane >> 2) & 3);
+        const int j = g * 4 + (lane >> 4);
+        alive = x < f.width && yr < f.shard_rows && j < f.samples;
+        r = j * f.shard_rows + yr;
+    } else {
+        const int tiles_x = (f.width + 7) >> 3;
+        x = (tile % tiles_x) * 8 + (lane & 7);
+        r = (tile / tiles_x) * 8 + (lane >> 3);
+        alive = x < f.width && r < f.num_rows;
+    }
     const int y = alive ? shard_row_to_y(f, r) : 0;
     const Ray ray = camera_ray(f, alive ? x : 0, y, row_sample(f, r));
     if (!ORD && dfr.blocks > 0 && alive && slab_ray(ray).generic) alive = false;  // traced by a deferred wave
@@ -1379,7 +1396,12 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
         uint32_t* qctl = (uint32_t*)c->d_queue;                          // {count, head}
         BounceRec* queue = (BounceRec*)((char*)c->d_queue + 64);
         HIP_TRY(hipMemsetAsync(qctl, 0, 8, s));
-        const int pblocks = (tiles + 3) / 4 + dfr.blocks;
+        // primary_kernel's packets: 8x8 pixel tiles, or 4x4 pixels x 4 frames
+        // for an ordered walk over four frames or more
+        const int ptiles = c->fast_slab && sc.ordered && f.samples >= 4
+                               ? ((f.width + 3) / 4) * ((f.shard_rows + 3) / 4) * ((f.samples + 3) / 4)
+                               : tiles;
+        const int pblocks = (ptiles + 3) / 4 + dfr.blocks;
         const int bblocks = c->bounce_blocks_opt ? c->bounce_blocks_opt : c->bounce_blocks;
         if (c->fast_slab && sc.ordered)
             primary_kernel<true, true><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);

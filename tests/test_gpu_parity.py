@@ -499,6 +499,36 @@ def test_ties_go_to_the_later_leaf(gpu, mirt, oracle):
     assert hit.sum() > 10_000
 
 
+def test_one_sided_chains_frame(gpu, mirt, oracle):
+    """Spheres sharing one centre send bvh.c's SAH (bvh.c:139-170) into its
+    fallback: every plane leaves a side empty, so the split lands at x = 0 and
+    one child is a 0-sphere leaf -- a chain of one-sided nodes down to the
+    depth-40 cap, whose leaf tests only its first sphere. The derived walk
+    layouts skip such chains (render.hip live_node) and fill four-wide nodes
+    greedily; the frame, per-ray hits and traces must stay the reference's."""
+    abi = mirt.abi
+    base = mirt.create_random_spheres(3000, 7)
+    cl = np.repeat(base[:40], 6)                   # 40 clusters of 6 coincident spheres
+    cl["color"][:, 2] ^= (np.arange(len(cl)) % 6 * 37).astype(np.uint8)
+    s = np.concatenate([base, cl])
+    s2 = s.copy()
+    b = mirt.build_bvh(s)
+    flat = b.nodes
+    leaf = flat["sphere"] >= 0
+    empty = (flat["skip"] & abi.NODE_EMPTY) != 0
+    assert (leaf & empty).sum() > 1000             # long fallback chains are present
+    gpu.upload(s, b)
+    cam = mirt.default_camera()
+    img = gpu.render_frame(cam, 320, 180, depth=5, seed=1)
+    t = oracle.build(s2)
+    ref = oracle.render(cam, 320, 180, s2, t, depth=5, use_bvh=True, mode=1, seed=1)
+    rays = _hard_rays(np.random.default_rng(5), s2, 30_000)
+    hits = oracle.intersect(t, s2, rays)
+    oracle.free(t)
+    assert (img == ref).all(), int((img != ref).any(-1).sum())
+    assert gpu.ray_bvh_intersect(rays).tobytes() == hits.tobytes()
+
+
 def test_ordered_walk_stays_within_its_lanes(gpu, mirt):
     """The ordered packet walk may only carry lanes that passed every box on
     the path. A lane-mask leak lets inactive lanes (e.g. the deferred
