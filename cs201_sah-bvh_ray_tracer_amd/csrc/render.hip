@@ -1016,7 +1016,7 @@ struct mirt_ctx {
     uint32_t* d_overlay = nullptr;  // BVH overlay: per-pixel last line in draw order
     size_t overlay_cap = 0;
     float r_max = 0.0f, c_max = 0.0f;
-    int bounce_threshold = 24;  // wavefront: shade finished rays once fewer lanes walk (swept: profiles/r02r_threshold_sweep.txt)
+    int bounce_threshold = 20;  // wavefront: shade finished rays once fewer lanes walk (swept: profiles/r02thr_threshold_sweep.txt)
     int bounce_blocks = 0;      // wavefront: persistent workgroups (set in mirt_create)
     int bounce_blocks_opt = 0;  // MIRT_OPT_BOUNCE_BLOCKS override (0: occupancy x CUs)
     int quad_drain = 1;         // four-wide bounce walk: finish the drain four lanes per ray

@@ -362,7 +362,7 @@ int mirt_last_phase_ms(mirt_ctx *ctx, float *phase);
    0 = DFS order. */
 enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3, MIRT_OPT_DEFER = 4,
        MIRT_OPT_BOUNCE_THRESHOLD = 5, /* wavefront: shade finished bounce rays once fewer than
-                                         this many lanes of a wave still walk (0..64, default 24) */
+                                         this many lanes of a wave still walk (0..64, default 20) */
        MIRT_OPT_PRUNE = 6, MIRT_OPT_ORDERED = 7,
        MIRT_OPT_BOUNCE_BLOCKS = 9,  /* wavefront: persistent bounce workgroups, 0 = occupancy x CUs */
        MIRT_OPT_QUAD_DRAIN = 11     /* four-wide bounce walk: 1 (default) = once the queue is dry

@@ -2,7 +2,7 @@
 bounce queue runs dry, lanes per loop iteration, longest walks and chains
 (mirt_bounce_stats).
 
-    python scripts/bounce_stats.py [--threshold 24] [--spheres 10000]
+    python scripts/bounce_stats.py [--threshold 20] [--spheres 10000]
 """
 import argparse
 import importlib
@@ -19,7 +19,7 @@ mirt = importlib.import_module("cs201_sah-bvh_ray_tracer_amd")
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--spheres", type=int, default=10000)
-    ap.add_argument("--threshold", type=int, default=24)
+    ap.add_argument("--threshold", type=int, default=20)
     ap.add_argument("--dump", default=None, help="save the raw per-wave records (.npy)")
     ap.add_argument("--shards", default="1", help="comma list: shard 0 of N for each N")
     a = ap.parse_args()
