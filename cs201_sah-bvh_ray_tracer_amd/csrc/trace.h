@@ -868,7 +868,10 @@ struct DfsWalk {
 // entry k at stk[k * kWideStride]); a step pushes all passing inner slots but
 // the nearest, farthest first. When that would overflow kWideStack, the
 // node's whole subtree is walked as a DFS segment instead.
-constexpr int kWideStack = 16;
+#ifndef MIRT_WIDE_STACK
+#define MIRT_WIDE_STACK 16
+#endif
+constexpr int kWideStack = MIRT_WIDE_STACK;
 constexpr int kWideStride = 256;  // threads per workgroup of the bounce kernel
 struct WideWalk {
     uint32_t cur, end, top;
