@@ -413,20 +413,30 @@ __device__ __forceinline__ bool slab_box(const SlabRay& r, const Prune& p, float
 // applies the pruning bound, which holds for any box containing the subtree.
 // Branch-free, valid for rays without a zero/tiny direction component
 // (slab_cons handles those with the exact division test).
+//
+// A plane's t is one fma, t = fl(b ix - fl(o ix)) (ix = fl(1/d)): against
+// the exact T = (b - o) / d it is off by at most 2.01 u |T| (ix and the
+// fma's rounding) plus 1.01 u |o ix| (the rounding of o ix), and hit.c's
+// Q = fl(fl(b - o) / d) is within 2.01 u |T| of T. The relative part is
+// covered by slab_fast's margin 2^-20 (|tmin| + |tmax|) (16 u against the
+// 4.1 u needed), the absolute part by mo = 2^-22 max_k |o_k ix_k| (4 u, twice
+// the 2.02 u of two values), added to the margin and to the pruning growth.
 __device__ __forceinline__ bool slab_cons_fast(const SlabRay& r, const Prune& p, float x0, float y0, float z0,
                                                float x1, float y1, float z1, float& near)
 {
-    const float tx1 = (x0 - r.ox) * r.ix, tx2 = (x1 - r.ox) * r.ix;
-    const float ty1 = (y0 - r.oy) * r.iy, ty2 = (y1 - r.oy) * r.iy;
-    const float tz1 = (z0 - r.oz) * r.iz, tz2 = (z1 - r.oz) * r.iz;
+    const float oix = r.ox * r.ix, oiy = r.oy * r.iy, oiz = r.oz * r.iz;  // shared by a step's boxes (CSE)
+    const float mo = fmaxf(fabsf(oix), fmaxf(fabsf(oiy), fabsf(oiz))) * 0x1p-22f;
+    const float tx1 = fmaf(x0, r.ix, -oix), tx2 = fmaf(x1, r.ix, -oix);
+    const float ty1 = fmaf(y0, r.iy, -oiy), ty2 = fmaf(y1, r.iy, -oiy);
+    const float tz1 = fmaf(z0, r.iz, -oiz), tz2 = fmaf(z1, r.iz, -oiz);
     const float nx = fminf(tx1, tx2), ny = fminf(ty1, ty2), nz = fminf(tz1, tz2);
     constexpr float c = 1.0f - 0x1p-20f;
-    const float entry = fmaxf(fmaf(nx, c, -(p.m * fabsf(r.ix))),
-                              fmaxf(fmaf(ny, c, -(p.m * fabsf(r.iy))), fmaf(nz, c, -(p.m * fabsf(r.iz)))));
+    const float entry = fmaxf(fmaf(nx, c, -fmaf(p.m, fabsf(r.ix), mo)),
+                              fmaxf(fmaf(ny, c, -fmaf(p.m, fabsf(r.iy), mo)), fmaf(nz, c, -fmaf(p.m, fabsf(r.iz), mo))));
     const float tmin = fmaxf(nx, fmaxf(ny, nz));
     const float tmax = fminf(fmaxf(tx1, tx2), fminf(fmaxf(ty1, ty2), fmaxf(tz1, tz2)));
     near = tmin;
-    const float m = (fabsf(tmin) + fabsf(tmax)) * 0x1p-20f;
+    const float m = fmaf(fabsf(tmin) + fabsf(tmax), 0x1p-20f, 2.0f * mo);
     return !(entry > p.lim) & !(tmax - tmin < -m) & !(tmax - kEps < -m);
 }
 
