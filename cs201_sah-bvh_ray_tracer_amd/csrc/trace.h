@@ -342,18 +342,22 @@ __device__ __forceinline__ void prune_update(Prune& p, const DevScene& sc, float
 __device__ __forceinline__ bool slab_fast(const SlabRay& r, const Prune& p, float x0, float y0, float z0, float x1,
                                           float y1, float z1, float& near)
 {
-    const float tx1 = (x0 - r.ox) * r.ix, tx2 = (x1 - r.ox) * r.ix;
-    const float ty1 = (y0 - r.oy) * r.iy, ty2 = (y1 - r.oy) * r.iy;
-    const float tz1 = (z0 - r.oz) * r.iz, tz2 = (z1 - r.oz) * r.iz;
+    // one fma per plane, as slab_cons_fast (its error bound below): the
+    // margins cover it, so a decided comparison is still the reference's
+    const float oix = r.ox * r.ix, oiy = r.oy * r.iy, oiz = r.oz * r.iz;
+    const float mo = fmaxf(fabsf(oix), fmaxf(fabsf(oiy), fabsf(oiz))) * 0x1p-22f;
+    const float tx1 = fmaf(x0, r.ix, -oix), tx2 = fmaf(x1, r.ix, -oix);
+    const float ty1 = fmaf(y0, r.iy, -oiy), ty2 = fmaf(y1, r.iy, -oiy);
+    const float tz1 = fmaf(z0, r.iz, -oiz), tz2 = fmaf(z1, r.iz, -oiz);
     const float nx = fminf(tx1, tx2), ny = fminf(ty1, ty2), nz = fminf(tz1, tz2);
     constexpr float c = 1.0f - 0x1p-20f;
-    const float entry = fmaxf(fmaf(nx, c, -(p.m * fabsf(r.ix))),
-                              fmaxf(fmaf(ny, c, -(p.m * fabsf(r.iy))), fmaf(nz, c, -(p.m * fabsf(r.iz)))));
+    const float entry = fmaxf(fmaf(nx, c, -fmaf(p.m, fabsf(r.ix), mo)),
+                              fmaxf(fmaf(ny, c, -fmaf(p.m, fabsf(r.iy), mo)), fmaf(nz, c, -fmaf(p.m, fabsf(r.iz), mo))));
     if (entry > p.lim) return false;
     const float tmin = fmaxf(nx, fmaxf(ny, nz));
     near = tmin;
     const float tmax = fminf(fmaxf(tx1, tx2), fminf(fmaxf(ty1, ty2), fmaxf(tz1, tz2)));
-    const float m = (fabsf(tmin) + fabsf(tmax)) * 0x1p-20f;
+    const float m = fmaf(fabsf(tmin) + fabsf(tmax), 0x1p-20f, 2.0f * mo);
     const float gap = tmax - tmin, above = tmax - kEps;
     if (gap > m && above > m) return true;
     if (gap < -m || above < -m) return false;
@@ -437,7 +441,9 @@ __device__ __forceinline__ bool slab_cons_fast(const SlabRay& r, const Prune& p,
     const float tmax = fminf(fmaxf(tx1, tx2), fminf(fmaxf(ty1, ty2), fmaxf(tz1, tz2)));
     near = tmin;
     const float m = fmaf(fabsf(tmin) + fabsf(tmax), 0x1p-20f, 2.0f * mo);
-    return !(entry > p.lim) & !(tmax - tmin < -m) & !(tmax - kEps < -m);
+    // tmax - tmin >= -m and tmax - eps >= -m as one comparison (m has 4x slack
+    // over the rounding of either form; a NaN passes, as before)
+    return !(entry > p.lim) & !(tmax + m < fmaxf(tmin, kEps));
 }
 
 __device__ __forceinline__ bool slab_cons(const SlabRay& r, const Prune& p, float x0, float y0, float z0, float x1,
