@@ -298,7 +298,7 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask)
 // nodes at 4 waves/SIMD 1659 Mrays/s; 96 nodes at 5 waves/SIMD (the LDS of
 // five workgroups then fits 160 KB) 1772; 6 waves/SIMD spills: 1587.
 #ifndef MIRT_HCACHE
-#define MIRT_HCACHE 96
+#define MIRT_HCACHE 16
 #endif
 constexpr uint32_t kHCache = MIRT_HCACHE;
 constexpr int kBounceDiag = 10;  // mirt_bounce_stats words per wave  // HNodes staged in LDS per bounce workgroup (64 B each)

@@ -885,7 +885,7 @@ struct DfsWalk {
 // the nearest, farthest first. When that would overflow kWideStack, the
 // node's whole subtree is walked as a DFS segment instead.
 #ifndef MIRT_WIDE_STACK
-#define MIRT_WIDE_STACK 16
+#define MIRT_WIDE_STACK 20
 #endif
 constexpr int kWideStack = MIRT_WIDE_STACK;
 constexpr int kWideStride = 256;  // threads per workgroup of the bounce kernel
