@@ -23,15 +23,19 @@ per-GPU launch shrinks with N until the bounce pass's longest chains set the
 time); `--scaling strong` makes that the headline. value = W*H primary rays
 per frame * frames per step * K / (max over ranks of the timed region).
 
-Successive steps are triple-buffered (`--pipeline 3`, default): three device
-contexts with the scene resident in each take turns on their own streams, so
-step k + 1's launches fill the CU slots that step k's bounce pass frees while
-its last chains drain. Each frame is still rendered whole and its bytes do
+Successive steps are quadruple-buffered (`--pipeline 4`, default): four device
+contexts with the scene resident in each take turns on their own streams (one
+per hardware queue), so step k + 1's launches fill the CU slots that step k's
+bounce pass frees while its last chains drain. With frames in flight each
+context's persistent bounce pass runs 1.5 workgroups per CU
+(`--bounce-blocks`, MIRT_OPT_BOUNCE_BLOCKS; a launch alone keeps the full
+occupancy x CUs): the four frames' passes then share the chip instead of the
+first holding every slot. Each frame is still rendered whole and its bytes do
 not change; only the gap between frames closes. The timed region brackets all
 K steps (barrier + synchronize on both sides).
 
 Also in the line (N = 1): `host_inclusive_mrays_s`, SURVEY §8(d)'s t_frame
-(call -> RGBA8 frame in host memory): the same three contexts, each frame's
+(call -> RGBA8 frame in host memory): the same four contexts, each frame's
 D2H copy into page-locked memory enqueued behind its kernels
 (mirt_render_frame_async) so it overlaps the next frame; the blocking
 single-call rate into pageable memory beside it. `roofline`: the dominant
@@ -318,13 +322,16 @@ def load_pmc_bound():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-host", action="store_true", help="skip the host-inclusive (D2H) leg")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="1080p_10k")
-    ap.add_argument("--pipeline", type=int, default=3,
+    ap.add_argument("--pipeline", type=int, default=4,
                     help="device contexts alternating successive steps on their own streams (1 = serial)")
+    ap.add_argument("--bounce-blocks", type=int, default=-1,
+                    help="persistent bounce workgroups per launch (MIRT_OPT_BOUNCE_BLOCKS) in the timed loop; "
+                         "-1 = 1.5 per CU with frames in flight (--pipeline > 1), else 0 (occupancy x CUs)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
                     help="weak: N frames in flight per step at N GPUs (default); strong: one frame split N ways")
     ap.add_argument("--dry", action="store_true", help="CPU plumbing check over gloo (no GPU, no measurement)")
@@ -358,8 +365,15 @@ def main():
     build_s = time.perf_counter() - t0
     dev = local if world > 1 else 0
     rs = [mirt.Renderer(dev) for _ in range(max(1, args.pipeline))]
+    # bounce workgroups per launch with frames in flight (measured: 1080p/10k
+    # 2,400 -> 2,650 Mrays/s at 4 contexts, profiles/r02_ab/r02au_*); the
+    # serial measurement loop and the blocking call below use the full grid
+    blocks = args.bounce_blocks
+    if blocks < 0:
+        blocks = (3 * torch.cuda.get_device_properties(dev).multi_processor_count) // 2 if len(rs) > 1 else 0
     for x in rs:
         x.upload(spheres, bvh)
+        x.set_option(mirt.abi.OPT_BOUNCE_BLOCKS, blocks)
         for ov in args.opt:
             o, v = (int(t) for t in ov.split("="))
             x.set_option(o, v)
@@ -419,6 +433,7 @@ def main():
     slabs = torch.zeros((frames, sf.rows, W), dtype=torch.int32, device="cuda")
     acc = torch.zeros((sf.rows, W, 3), dtype=torch.float32, device="cuda") if frames > 1 else None
     phases, launch = [], []
+    r.set_option(mirt.abi.OPT_BOUNCE_BLOCKS, 0)   # one launch alone: the full persistent grid
     for _ in range(min(args.steps, 20)):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
@@ -430,6 +445,7 @@ def main():
         launch.append(e0.elapsed_time(e1))
     primary_ms, bounce_ms = (float(v) for v in np.mean(np.array(phases), axis=0))
     kernel_ms = float(np.mean(launch))
+    r.set_option(mirt.abi.OPT_BOUNCE_BLOCKS, blocks)
 
     t = torch.tensor([elapsed, kernel_ms, elapsed_d1, elapsed_other or 0.0], dtype=torch.float64, device="cuda")
     if world > 1:
@@ -467,7 +483,7 @@ def main():
             "config": {"workload": wl["desc"], "name": args.workload,
                        "width": W, "height": H, "spheres": NSPH, "scene": KIND, "max_depth": DEPTH, "spp": SPP,
                        "jitter": JITTER,
-                       "frames_per_step": frames, "pipeline": len(rs), "bvh_nodes": len(bvh),
+                       "frames_per_step": frames, "pipeline": len(rs), "bounce_blocks": blocks, "bvh_nodes": len(bvh),
                        "row_block": ROW_BLOCK,
                        "parallelism": f"row-block shard x{world}" + (" + RCCL gather" if world > 1 else "")
                                       + (f", {frames} accumulated frames in flight" if frames > 1 else "")},
@@ -503,8 +519,9 @@ def main():
                 "primary_algorithmic_bytes": int(ref_frame_bytes - ref_b),
                 "frame_ms": round(kernel_ms, 4), "frame_algorithmic_bytes": int(ref_frame_bytes),
                 "frame_executed_bytes": int(exec_frame_bytes),
-                "note": "kernel_ms / frame_ms: one launch alone (serial loop); the timed loop overlaps "
-                        "successive launches (pipeline)"},
+                "note": "kernel_ms / frame_ms: one launch alone (serial loop, full persistent grid); the "
+                        "timed loop overlaps `pipeline` successive launches of `bounce_blocks` bounce "
+                        "workgroups each"},
             "work": {k: int(v) for k, v in counts.items()},
             "work_reference_dfs": {k: int(v) for k, v in ref_counts.items() if k != "lane_steps"},
             "traced_rays_per_s_M": round(counts["rays"] * world / (kernel_ms_max / 1e3) / 1e6, 3),
@@ -557,7 +574,9 @@ def host_inclusive(rs, cam, steps):
     run(0, steps_h)
     el = time.perf_counter() - t0
     last = bufs[(steps_h - 1) % n].array.copy()
-    # the blocking call (pageable destination); median: page faults make single calls noisy
+    # the blocking call (pageable destination, one frame at a time: the full
+    # persistent grid); median: page faults make single calls noisy
+    rs[0].set_option(mirt.abi.OPT_BOUNCE_BLOCKS, 0)
     img = rs[0].render_frame(cam, W, H, depth=DEPTH, seed=SEED, samples=SPP, jitter=JITTER)
     dts = []
     for _ in range(11):

@@ -364,7 +364,9 @@ enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3,
        MIRT_OPT_BOUNCE_THRESHOLD = 5, /* wavefront: shade finished bounce rays once fewer than
                                          this many lanes of a wave still walk (0..64, default 20) */
        MIRT_OPT_PRUNE = 6, MIRT_OPT_ORDERED = 7,
-       MIRT_OPT_BOUNCE_BLOCKS = 9,  /* wavefront: persistent bounce workgroups, 0 = occupancy x CUs */
+       MIRT_OPT_BOUNCE_BLOCKS = 9,  /* wavefront: persistent bounce workgroups, 0 = occupancy x CUs
+                                       (default: best for one frame at a time); with several contexts
+                                       keeping frames in flight, ~1.5 per CU (384 on MI355X) */
        MIRT_OPT_QUAD_DRAIN = 11     /* four-wide bounce walk: 1 (default) = once the queue is dry
                                        and <= 16 lanes of a wave are busy, finish them as quads */ };
 enum { MIRT_TRAV_TILE = 0, MIRT_TRAV_WAVEFRONT = 1 };
