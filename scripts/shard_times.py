@@ -8,12 +8,19 @@ of an N-GPU step (the RCCL gather comes on top).
 --weak: the bench's default step -- at N GPUs every rank renders its rows
 of N frames in one launch (accumulated), so the per-rank work stays one
 frame's worth.
+
+--pipeline P: time the bench's timed loop instead of single launches -- P
+contexts take successive steps of shard k on their own streams, with
+--blocks persistent bounce workgroups per launch (the bench's defaults: 4 and
+1.5 per CU) -- and report each shard's per-rank Mrays/s (the RCCL gather
+comes on top).
 """
 import argparse
 import importlib
 import json
 import os
 import sys
+import time
 
 import numpy as np
 import torch
@@ -34,7 +41,12 @@ def main():
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--weak", action="store_true", help="N frames in flight at N shards (the bench default)")
     ap.add_argument("--opt", action="append", default=[], help="option=value (mirt_set_option), repeatable")
+    ap.add_argument("--pipeline", type=int, default=0, help="time P contexts in flight (bench loop)")
+    ap.add_argument("--blocks", type=int, default=-1, help="bounce workgroups with --pipeline (-1: 1.5 per CU)")
+    ap.add_argument("--steps", type=int, default=100)
     a = ap.parse_args()
+    if a.pipeline:
+        return pipelined(a)
     W, H = a.width, a.height
     s = mirt.create_random_spheres(a.spheres, 1)
     b = mirt.build_bvh(s)
@@ -72,6 +84,47 @@ def main():
                           "frames": frames,
                           "pred_mrays_s_no_gather": round(W * H * frames / max(per) / 1e3, 1)}), flush=True)
     r.close()
+
+
+def pipelined(a):
+    W, H = a.width, a.height
+    s = mirt.create_random_spheres(a.spheres, 1)
+    b = mirt.build_bvh(s)
+    blocks = a.blocks if a.blocks >= 0 else 3 * torch.cuda.get_device_properties(0).multi_processor_count // 2
+    rs = [mirt.Renderer(0) for _ in range(a.pipeline)]
+    for r in rs:
+        r.upload(s, b)
+        r.set_option(mirt.abi.OPT_BOUNCE_BLOCKS, blocks)
+    streams = [torch.cuda.ExternalStream(r.stream_handle) for r in rs]
+    cam = mirt.default_camera()
+    for world in (int(w) for w in a.worlds.split(",")):
+        rows = shard.slab_rows(H, 8, world)
+        frames = world if a.weak else 1
+        slabs = [torch.zeros((frames, rows, W), dtype=torch.int32, device="cuda") for _ in rs]
+        accs = [torch.zeros((rows, W, 3), dtype=torch.float32, device="cuda") if frames > 1 else None for _ in rs]
+        per = []
+        for k in range(world):
+            fd = mirt.frame_desc(W, H, a.depth, True, 1, 0, False, 1, 8, k, world, frames)
+
+            def run(n):
+                for i in range(n):
+                    j = i % len(rs)
+                    rs[j].render_frame_device(cam, fd, slabs[j].data_ptr(),
+                                              accs[j].data_ptr() if accs[j] is not None else None,
+                                              streams[j].cuda_stream)
+            run(2 * len(rs))
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            run(a.steps)
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            per.append(W * H * frames / world * a.steps / el / 1e6)
+        print(json.dumps({"spheres": a.spheres, "world": world, "frames": frames, "pipeline": a.pipeline,
+                          "blocks": blocks, "per_rank_mrays_s": [round(p, 1) for p in per],
+                          "min_per_rank_mrays_s": round(min(per), 1),
+                          "pred_job_mrays_s_no_gather": round(min(per) * world, 1)}), flush=True)
+    for r in rs:
+        r.close()
 
 
 if __name__ == "__main__":
