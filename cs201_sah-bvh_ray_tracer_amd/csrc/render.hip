@@ -316,7 +316,16 @@ struct BounceRec {
 // also takes zero-component rays -- that build has no deferred waves and no
 // other walk, so it keeps the register budget of the packet walk alone.
 template <bool FAST, bool ORD>
-__global__ __launch_bounds__(256) void primary_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
+// Register budget of the ordered camera-packet kernel (ORD): 8 waves per SIMD (64 VGPRs, no
+// scratch; 67 and 7 waves without the attribute). With four frames in flight
+// its waves share the CUs with the bounce passes, and the eighth wave hides
+// more of the packet walk's scalar-load latency (1080p/10k +0.3-1.1%,
+// 1080p/100k +3.7%, profiles/r02_ab/r02ax_primary_waves8_*).
+#ifndef MIRT_PRIMARY_WAVES
+#define MIRT_PRIMARY_WAVES 8
+#endif
+#define MIRT_PRIMARY_ATTR __attribute__((amdgpu_waves_per_eu(ORD ? MIRT_PRIMARY_WAVES : 1)))
+__global__ __launch_bounds__(256) MIRT_PRIMARY_ATTR void primary_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
                                                       float* __restrict__ acc, Deferred dfr,
                                                       BounceRec* __restrict__ queue, uint32_t* __restrict__ qctl)
 {
