@@ -554,10 +554,11 @@ def test_ordered_walk_stays_within_its_lanes(gpu, mirt):
 
 
 @pytest.mark.parametrize("drain", [0, 1])
-@pytest.mark.parametrize("threshold,blocks", [(40, 0), (8, 0), (56, 64)])
+@pytest.mark.parametrize("threshold,blocks", [(40, 0), (8, 0), (56, 64), (20, 384)])
 def test_bounce_modes_identical(gpu, mirt, golden, drain, threshold, blocks):
     """The bounce pass's modes (one ray per lane, with or without the quad
-    drain), refill thresholds and grid sizes give the golden 1080p frame."""
+    drain), refill thresholds and grid sizes (384: the bench's grid with
+    frames in flight) give the golden 1080p frame."""
     abi = mirt.abi
     s, b = _scene(mirt, "render", 10000)
     gpu.upload(s, b)
@@ -569,7 +570,7 @@ def test_bounce_modes_identical(gpu, mirt, golden, drain, threshold, blocks):
         img = gpu.render_frame(cam, 1920, 1080, depth=5, seed=1)
     finally:
         gpu.set_option(abi.OPT_QUAD_DRAIN, 1)
-        gpu.set_option(abi.OPT_BOUNCE_THRESHOLD, 32)
+        gpu.set_option(abi.OPT_BOUNCE_THRESHOLD, 20)   # the library default
         gpu.set_option(abi.OPT_BOUNCE_BLOCKS, 0)
     key = "1920x1080_render10000_d5_m1_b1_s1_c0_step1"
     assert sha(img) == golden["frames"][key]["sha"]
