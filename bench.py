@@ -87,7 +87,9 @@ PEAK_HBM_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level par
 PEAK_L2_GBS = 34500.0   # aggregate L2 (MI355X_MICROARCH.md §L2)
 NODE_B, SPHERE_B, COLOR_B, PIXEL_B = 32, 16, 4, 4
 KERNEL = "bounce_kernel<true, 2, false>"   # dominant kernel of the default (wavefront, four-wide) schedule
-PMC_BOUND = os.path.join(ROOT, "profiles", "r02_pmc_bound.json")
+# the PMC-derived bound of the timed launch shape, per workload
+# (scripts/pmc_bench.sh over this script's own command + scripts/pmc_summary.py)
+PMC_BOUND = {wl: os.path.join(ROOT, "profiles", f"r03_pmc_bound_{wl}.json") for wl in WORKLOADS}
 
 
 def algorithmic_bytes(c, pixels):
@@ -199,6 +201,17 @@ def cpu_baseline(target_s=10.0):
            "single_core_value": single["value"],
            "single_core_sample": f"every {single['step']}th row x {single['reps']} ({single['rows']} rows) "
                                  f"in {single['s']} s, -O2"}
+    # the whole host, for context: `cores` is this box's CPU share, not the machine
+    hc = out["host"]
+    avail = max(hc["nproc"] or 1, hc["affinity"] or 1)
+    eff = multi["value"] / max(single["value"] * threads, 1e-12)
+    out["cores_available"] = avail
+    out["thread_scaling_efficiency"] = round(eff, 3)
+    out["all_core_estimate"] = {
+        "value": round(multi["value"] * avail / threads, 4), "cores": avail, "kind": "estimate",
+        "note": f"linear extrapolation of the {threads}-thread rate to all {avail} cores of the host (not measured: "
+                f"the box grants {threads} CPUs; {threads} threads ran at {eff:.0%} of {threads} x one core, so this "
+                "is an upper bound for the reference on the whole machine)"}
     m0 = make(W, H, NSPH, KIND, "O0")
     if m0 is not None:
         run0, free0, _ = m0
@@ -309,14 +322,34 @@ def dry_main(args, world, rank):
 
 # ------------------------------------------------------------------ main
 
-def load_pmc_bound():
-    """The PMC-derived bound of the frame kernels (profiles/r02_pmc_bound.json,
-    scripts/pmc_probe.sh + scripts/pmc_summary.py) for this workload."""
-    if not os.path.exists(PMC_BOUND):
-        return None
-    with open(PMC_BOUND) as f:
+def load_pmc_bound(name):
+    """The PMC-derived bound of the frame kernels of workload `name` in the
+    timed launch shape (profiles/r03_pmc_bound_<name>.json: scripts/pmc_bench.sh
+    over `bench.py --workload name` + scripts/pmc_summary.py), or None."""
+    path = PMC_BOUND.get(name)
+    if not path or not os.path.exists(path):
+        return None, None
+    with open(path) as f:
         d = json.load(f)
-    return d if d.get("workload") == [W, H, NSPH, DEPTH] else None
+    return (d, path) if d.get("workload") == [W, H, NSPH, DEPTH] else (None, None)
+
+
+def bound_line(pb, exec_b, ref_b, ms):
+    """bound_measured: the busiest unit of a kernel and its utilisation, from
+    the committed counters."""
+    if not pb:
+        return None
+    return {"unit": {"td_busy": "TD (vector-memory data return)", "ta_busy": "TA (vector-memory address)",
+                     "valu_busy": "VALU issue", "l2_frac_upper": "L2 bandwidth",
+                     "hbm_frac": "HBM bandwidth"}.get(pb.get("busiest_unit"), pb.get("busiest_unit")),
+            "td_busy": pb.get("td_busy"), "ta_busy": pb.get("ta_busy"), "valu_busy": pb.get("valu_busy"),
+            "l2_hit": pb.get("l2_hit"), "l2_read_gbs_upper": pb.get("l2_read_gbs_upper"),
+            "l2_peak_gbs": PEAK_L2_GBS, "l2_frac_upper": pb.get("l2_frac_upper"),
+            "l2_read_latency_cycles": pb.get("l2_read_latency_cycles"),
+            "wait_any_per_wave_cycle": pb.get("wait_any_per_wave_cycle"),
+            "executed_bytes_per_launch": int(exec_b),
+            "executed_gbs": round(exec_b / (ms / 1e3) / 1e9, 1),
+            "executed_vs_reference_bytes": round(exec_b / max(ref_b, 1), 4)}
 
 
 def main():
@@ -332,8 +365,9 @@ def main():
     ap.add_argument("--bounce-blocks", type=int, default=-1,
                     help="persistent bounce workgroups per launch (MIRT_OPT_BOUNCE_BLOCKS) in the timed loop; "
                          "-1 = 1.5 per CU with frames in flight (--pipeline > 1), else 0 (occupancy x CUs)")
-    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
-                    help="weak: N frames in flight per step at N GPUs (default); strong: one frame split N ways")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="strong",
+                    help="strong (default): every step is ONE frame (the N = 1 workload) split N ways, frames in "
+                         "flight; weak: N frames per step at N GPUs (reported beside it as value_weak)")
     ap.add_argument("--dry", action="store_true", help="CPU plumbing check over gloo (no GPU, no measurement)")
     ap.add_argument("--opt", action="append", default=[],
                     help="OPTION=VALUE (mirt_set_option on every context; A/B of schedule options), repeatable")
@@ -411,6 +445,18 @@ def main():
         body()
     elapsed = timed(world, args.steps, body)
 
+    # the two passes of every timed frame, from the HIP events the library
+    # records on each frame's own stream around its primary and bounce
+    # kernels (mirt_phase_log): their durations UNDER the overlap of the timed
+    # loop (frames k % P on ctx k % P, warm-up frames first)
+    P = len(rs)
+    timed_phases = []
+    for i, x in enumerate(rs):
+        n_i = sum(1 for k in range(args.warmup, args.warmup + args.steps) if k % P == i)
+        if n_i:
+            timed_phases += x.phase_log(min(n_i, 64))
+    primary_ms, bounce_ms = (float(v) for v in np.mean(np.array(timed_phases), axis=0))
+
     # depth 1 alongside (camera rays and their shading only)
     body1 = step_fn(sf, sf.desc(depth=1, seed=SEED, jitter=JITTER))
     for _ in range(2):
@@ -427,9 +473,9 @@ def main():
             body2()
         elapsed_other = timed(world, args.steps, body2)
 
-    # per-kernel split of the same launch, one context, serial (untimed loop:
-    # each launch waits for its events): torch events around the launch and
-    # the HIP events the library records around the primary and bounce passes
+    # the same launch alone, one context, serial (untimed loop: each launch
+    # waits for its events): torch events around the launch and the HIP
+    # events the library records around the primary and bounce passes
     slabs = torch.zeros((frames, sf.rows, W), dtype=torch.int32, device="cuda")
     acc = torch.zeros((sf.rows, W, 3), dtype=torch.float32, device="cuda") if frames > 1 else None
     phases, launch = [], []
@@ -443,7 +489,7 @@ def main():
         phases.append(r.last_phase_ms())
         e1.synchronize()
         launch.append(e0.elapsed_time(e1))
-    primary_ms, bounce_ms = (float(v) for v in np.mean(np.array(phases), axis=0))
+    serial_primary_ms, serial_bounce_ms = (float(v) for v in np.mean(np.array(phases), axis=0))
     kernel_ms = float(np.mean(launch))
     r.set_option(mirt.abi.OPT_BOUNCE_BLOCKS, blocks)
 
@@ -464,9 +510,15 @@ def main():
         ref_b = bounce_bytes(ref_counts)
         exec_b = bounce_bytes(counts)
         achieved = ref_b / (bounce_ms / 1e3) / 1e9
-        pmc = load_pmc_bound() if world == 1 else None
-        pb = pmc["kernels"].get("t1_f1_d5/bounce", {}).get("derived", {}) if pmc else {}
+        pmc, pmc_path = load_pmc_bound(args.workload) if world == 1 else (None, None)
+        pb = pmc["kernels"].get("timed/bounce", {}).get("derived", {}) if pmc else {}
+        pp = pmc["kernels"].get("timed/primary", {}).get("derived", {}) if pmc else {}
         traffic = pb.get("hbm_bytes")
+        bm = bound_line(pb, exec_b, ref_b, bounce_ms)
+        if bm:
+            bm["source"] = (os.path.relpath(pmc_path, ROOT) + " (medians over the dispatches of the timed launch "
+                            "shape, one rocprofv3 --pmc pass of this command per counter set; rocprofv3 serialises "
+                            "the dispatches it counts)")
         line = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -491,40 +543,36 @@ def main():
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
                 "kernel": KERNEL, "kernel_ms": round(bounce_ms, 4),
+                "kernel_ms_source": f"mean over the {len(timed_phases)} timed frames of HIP events recorded on each "
+                                    "frame's own stream around its bounce launch (mirt_phase_log): the launch's "
+                                    "duration UNDER the timed loop's overlap of `pipeline` frames",
                 "algorithmic_bytes_per_launch": int(ref_b),
                 "definition": "SURVEY 8(d): bytes of the REFERENCE's exhaustive DFS (hit.c:91-109, no pruning) "
                               "for the bounce levels at 32 B/node test + 16 B/sphere test + 4 B/hit colour + "
-                              "4 B/pixel, / the bounce kernel's HIP-event time. The tree is L2/MALL-resident, so "
-                              "this effective rate exceeds the HBM peak by construction (frac > 1): it is not HBM "
-                              "use. Measured HBM use and the unit that does bound the kernel: hbm_measured, "
-                              "bound_measured.",
+                              "4 B/pixel, / the bounce kernel's HIP-event time in the timed loop. The tree is "
+                              "L2/MALL-resident, so this effective rate is not HBM use. Measured HBM use and the "
+                              "unit that does bound the kernel: hbm_measured, bound_measured.",
                 "hbm_measured": None if traffic is None else {
                     "bytes_per_launch": traffic, "gbs": round(traffic / (bounce_ms / 1e3) / 1e9, 2),
                     "frac": round(traffic / (bounce_ms / 1e3) / 1e9 / PEAK_HBM_GBS, 5)},
-                "bound_measured": None if not pb else {
-                    "unit": {"td_busy": "TD (vector-memory data return)", "ta_busy": "TA (vector-memory address)",
-                             "valu_busy": "VALU issue", "l2_frac_upper": "L2 bandwidth",
-                             "hbm_frac": "HBM bandwidth"}.get(pb.get("busiest_unit"), pb.get("busiest_unit")),
-                    "td_busy": pb.get("td_busy"), "ta_busy": pb.get("ta_busy"), "valu_busy": pb.get("valu_busy"),
-                    "l2_hit": pb.get("l2_hit"), "l2_read_gbs_upper": pb.get("l2_read_gbs_upper"),
-                    "l2_peak_gbs": PEAK_L2_GBS, "l2_frac_upper": pb.get("l2_frac_upper"),
-                    "l2_read_latency_cycles": pb.get("l2_read_latency_cycles"),
-                    "wait_any_per_wave_cycle": pb.get("wait_any_per_wave_cycle"),
-                    "executed_bytes_per_launch": int(exec_b),
-                    "executed_gbs": round(exec_b / (bounce_ms / 1e3) / 1e9, 1),
-                    "executed_vs_reference_bytes": round(exec_b / max(ref_b, 1), 4),
-                    "source": os.path.relpath(PMC_BOUND, ROOT) + " (medians over launches of "
-                              "scripts/profile_kernel.py, one rocprofv3 --pmc pass per counter set)"},
+                "bound_measured": bm,
                 "primary_kernel_ms": round(primary_ms, 4),
                 "primary_algorithmic_bytes": int(ref_frame_bytes - ref_b),
-                "frame_ms": round(kernel_ms, 4), "frame_algorithmic_bytes": int(ref_frame_bytes),
+                "primary_bound_measured": bound_line(pp, exec_frame_bytes - exec_b, ref_frame_bytes - ref_b,
+                                                     primary_ms),
+                "frame_algorithmic_bytes": int(ref_frame_bytes),
                 "frame_executed_bytes": int(exec_frame_bytes),
-                "note": "kernel_ms / frame_ms: one launch alone (serial loop, full persistent grid); the "
-                        "timed loop overlaps `pipeline` successive launches of `bounce_blocks` bounce "
-                        "workgroups each"},
+                "frame_period_ms": round(elapsed / args.steps * 1e3, 4),
+                "frame_algorithmic_gbs": round(ref_frame_bytes / (elapsed / args.steps) / 1e9, 1),
+                "serial_launch": {
+                    "note": "the same launch alone (untimed serial loop, the full persistent bounce grid): not "
+                            "the timed configuration",
+                    "frame_ms": round(kernel_ms, 4), "primary_ms": round(serial_primary_ms, 4),
+                    "bounce_ms": round(serial_bounce_ms, 4),
+                    "bounce_achieved_gbs": round(ref_b / (serial_bounce_ms / 1e3) / 1e9, 1)}},
             "work": {k: int(v) for k, v in counts.items()},
             "work_reference_dfs": {k: int(v) for k, v in ref_counts.items() if k != "lane_steps"},
-            "traced_rays_per_s_M": round(counts["rays"] * world / (kernel_ms_max / 1e3) / 1e6, 3),
+            "traced_rays_per_s_M": round(counts["rays"] * world / (elapsed / args.steps) / 1e6, 3),
             "depth1_mrays_s": round(W * H * frames * args.steps / elapsed_d1 / 1e6, 3),
             "bvh_build_s": round(build_s, 4),
         }
@@ -541,6 +589,7 @@ def main():
             line["cpu_baseline"] = cb
             line["speedup_vs_cpu"] = round(value / cb["value"], 1)
             line["speedup_vs_cpu_single_core"] = round(value / cb["single_core_value"], 1)
+            line["speedup_vs_cpu_all_core_estimate"] = round(value / cb["all_core_estimate"]["value"], 1)
             if host is not None:
                 line["host_inclusive_speedup_vs_cpu"] = round(host["host_inclusive_mrays_s"] / cb["value"], 1)
         print(json.dumps(line), flush=True)

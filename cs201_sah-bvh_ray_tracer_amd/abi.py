@@ -141,6 +141,7 @@ SIGNATURES = [
     ("mirt_host_alloc", I, [C.c_size_t, C.POINTER(P)]),
     ("mirt_host_free", None, [P]),
     ("mirt_accum_download", I, [P, P, C.c_size_t]),
+    ("mirt_ctx_share_accum", I, [P, P]),
     ("mirt_trace_rays", I, [P, P, I, I, I, C.c_uint64, C.c_uint32, P]),
     ("mirt_trace_rays_at", I, [P, P, I, I, I, C.c_uint64, C.c_uint32, C.c_uint32, P]),
     ("mirt_camera_rays_uv", I, [P, P, I, I, P, I, P]),
@@ -155,6 +156,7 @@ SIGNATURES = [
     ("mirt_ctx_stream", P, [P]),
     ("mirt_last_kernel_ms", C.c_float, [P]),
     ("mirt_last_phase_ms", I, [P, C.POINTER(C.c_float)]),
+    ("mirt_phase_log", I, [P, C.POINTER(C.c_float), I]),
     ("mirt_bounce_stats", I, [P, P, P, P, I]),
     ("mirt_set_option", I, [P, I, I]),
     ("mirt_get_option", I, [P, I]),
@@ -162,6 +164,7 @@ SIGNATURES = [
     ("mirt_dropin_init", I, [I, I, I]),
     ("mirt_dropin_release", None, []),
     ("mirt_dropin_rng", None, [C.c_uint64, C.c_uint32]),
+    ("mirt_dropin_scene", I, [P, I]),
     ("mirt_dropin_invalidate", None, []),
     ("mirt_dropin_status", I, []),
     ("mirt_get_camera_ray", Ray, [P, C.c_float, C.c_float]),
@@ -174,4 +177,4 @@ SIGNATURES = [
 OPT_TRAVERSAL, OPT_FAST_SLAB, OPT_BLOCK_WAVES, OPT_DEFER, OPT_BOUNCE_THRESHOLD, OPT_PRUNE, OPT_ORDERED = (
     1, 2, 3, 4, 5, 6, 7)
 OPT_BOUNCE_BLOCKS, OPT_QUAD_DRAIN = 9, 11
-TRAV_TILE, TRAV_WAVEFRONT = 0, 1
+TRAV_TILE, TRAV_WAVEFRONT = 0, 5

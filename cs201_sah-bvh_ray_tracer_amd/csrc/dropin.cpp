@@ -1,6 +1,10 @@
 // The reference's per-ray call surface (include/mirt_dropin.h) over the batch
 // C ABI: one launch per call on a process-wide context, the caller's scene
-// uploaded once per (sphere array, count, tree root) key.
+// uploaded once per (sphere array, count, tree root, content fingerprint)
+// key. The fingerprint matters because benchmark.c:306-324 frees the tree and
+// the spheres and mallocs the next size's: the allocator hands the same
+// addresses back (glibc's tcache is LIFO and the root is freed last), so the
+// pointers alone would keep walking the previous, freed scene.
 //
 //   mirt_get_camera_ray        ray.c:17-32      -> mirt_camera_rays_uv, n = 1
 //   mirt_trace_ray             renderer.c:21-77 -> mirt_trace_rays_at, pixel = call counter
@@ -25,7 +29,12 @@ struct DropinState {
     const mirt_sphere* spheres = nullptr;
     int num_spheres = -1;
     const mirt_bvh_node* root = nullptr;
+    uint64_t fingerprint = 0;
     bool bound = false;
+    // mirt_dropin_scene: the caller's whole sphere array, for trees built over
+    // part of it (benchmark.c:317 builds over [0, n - 1) of n spheres)
+    const mirt_sphere* decl = nullptr;
+    int decl_n = 0;
     uint64_t seed = 1;
     uint32_t sample = 0, pixel = 0;
     int status = MIRT_OK;
@@ -43,36 +52,85 @@ int ensure_ctx(DropinState& s)
     return mirt_create(s.device, &s.ctx);
 }
 
+// FNV-1a 64 over a byte range.
+uint64_t fnv(uint64_t h, const void* p, size_t n)
+{
+    const unsigned char* b = (const unsigned char*)p;
+    for (size_t i = 0; i < n; i++) h = (h ^ b[i]) * 0x100000001b3ull;
+    return h;
+}
+
+// A cheap content fingerprint of a scene, computed on every call: the first
+// 31 nodes of the tree in breadth-first order (bounds, sphere count, and the
+// sphere a non-empty leaf tests) and up to 32 spheres strided over the
+// array. Reading them costs ~60 small loads, against a GPU launch per call.
+uint64_t fingerprint(const mirt_sphere* sp, int ns, const mirt_bvh_node* root)
+{
+    uint64_t h = fnv(0xcbf29ce484222325ull, &ns, sizeof ns);
+    const mirt_bvh_node* q[31];
+    int head = 0, tail = 0;
+    if (root) q[tail++] = root;
+    while (head < tail) {
+        const mirt_bvh_node* n = q[head++];
+        h = fnv(h, &n->bounds, sizeof n->bounds);
+        h = fnv(h, &n->sphere_count, sizeof n->sphere_count);
+        if (n->sphere) {
+            if (n->sphere_count > 0) h = fnv(h, n->sphere, sizeof(mirt_sphere));
+            continue;
+        }
+        for (const mirt_bvh_node* c : {n->left, n->right})
+            if (c && tail < 31) q[tail++] = c;
+    }
+    if (sp && ns > 0) {
+        const int step = ns > 32 ? ns / 32 : 1;
+        for (int i = 0; i < ns; i += step) h = fnv(h, &sp[i], sizeof(mirt_sphere));
+        h = fnv(h, &sp[ns - 1], sizeof(mirt_sphere));
+    }
+    return h;
+}
+
 int bind(DropinState& s, const mirt_sphere* sp, int ns, const mirt_bvh_node* root)
 {
-    if (s.bound && s.spheres == sp && s.num_spheres == ns && s.root == root) return MIRT_OK;
+    const uint64_t fp = fingerprint(sp, ns, root);
+    if (s.bound && s.spheres == sp && s.num_spheres == ns && s.root == root && s.fingerprint == fp) return MIRT_OK;
     s.bound = false;
     const int rc = mirt_scene_upload(s.ctx, sp, ns, root);
     if (rc) return rc;
     s.spheres = sp;
     s.num_spheres = ns;
     s.root = root;
+    s.fingerprint = fp;
     s.bound = true;
     return MIRT_OK;
 }
 
-// Lowest and highest leaf sphere pointer of a pointer tree (bvh.c:131-137:
-// every leaf, empty ones included, points into the build's array).
-void leaf_range(const mirt_bvh_node* root, const mirt_sphere** lo, const mirt_sphere** hi)
+// The sphere array a pointer tree seen without one spans (bvh.c:131-137):
+// *lo = the lowest leaf sphere pointer (empty leaves included: a 0-sphere
+// leaf points at spheres[start] of its range), *count = up to the end of the
+// highest NON-empty leaf's range. A 0-sphere leaf at the very end of the
+// build range points one past it (&spheres[end]): that element
+// is not read -- its index is the never-hit sentinel (count) -- unless the
+// caller declared a longer array with mirt_dropin_scene.
+bool leaf_range(const mirt_bvh_node* root, const mirt_sphere** lo, int* count)
 {
+    const mirt_sphere *low = nullptr, *end = nullptr;
     std::vector<const mirt_bvh_node*> todo{root};  // explicit stack: any tree depth
     while (!todo.empty()) {
         const mirt_bvh_node* n = todo.back();
         todo.pop_back();
         if (!n) continue;
         if (n->sphere) {
-            if (!*lo || n->sphere < *lo) *lo = n->sphere;
-            if (!*hi || n->sphere > *hi) *hi = n->sphere;
+            if (!low || n->sphere < low) low = n->sphere;
+            if (n->sphere_count > 0 && (!end || n->sphere + n->sphere_count > end)) end = n->sphere + n->sphere_count;
             continue;
         }
         todo.push_back(n->right);
         todo.push_back(n->left);
     }
+    if (!low) return false;
+    *lo = low;
+    *count = end && end > low ? (int)(end - low) : 0;
+    return true;
 }
 
 mirt_hit_record to_record(const mirt_hit& h, mirt_sphere* base)
@@ -146,6 +204,19 @@ void mirt_dropin_rng(uint64_t seed, uint32_t sample)
     s.seed = seed;
     s.sample = sample;
     s.pixel = 0;
+}
+
+int mirt_dropin_scene(const mirt_sphere* spheres, int num_spheres)
+{
+    DropinState& s = state();
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (num_spheres < 0 || (num_spheres > 0 && !spheres)) {
+        mirt::set_error("mirt_dropin_scene: invalid arguments");
+        return s.status = MIRT_E_INVALID;
+    }
+    s.decl = num_spheres > 0 ? spheres : nullptr;
+    s.decl_n = num_spheres;
+    return s.status = MIRT_OK;
 }
 
 void mirt_dropin_invalidate(void)
@@ -224,15 +295,22 @@ mirt_hit_record mirt_ray_bvh_intersect(mirt_ray ray, mirt_bvh_node* node)
             mirt::set_error("mirt_ray_bvh_intersect: null tree");
             return (int)MIRT_E_INVALID;
         }
-        if (!(s.bound && s.root == node)) {
-            // a tree seen without its sphere array: the leaves span it
-            const mirt_sphere *lo = nullptr, *hi = nullptr;
-            leaf_range(node, &lo, &hi);
-            if (!lo) {
+        // the scene bound by the last trace_ray (or this call), if the tree
+        // is still the same (pointer and content)
+        if (!(s.bound && s.root == node && s.fingerprint == fingerprint(s.spheres, s.num_spheres, node))) {
+            // a tree seen without its sphere array: the leaves span it, or
+            // the array the caller declared (mirt_dropin_scene) holds them
+            const mirt_sphere* lo = nullptr;
+            int count = 0;
+            if (!leaf_range(node, &lo, &count)) {
                 mirt::set_error("mirt_ray_bvh_intersect: tree without leaves");
                 return (int)MIRT_E_INVALID;
             }
-            if (int r = bind(s, lo, (int)(hi - lo) + 1, node)) return r;
+            if (s.decl && lo >= s.decl && lo + count <= s.decl + s.decl_n) {
+                lo = s.decl;
+                count = s.decl_n;
+            }
+            if (int r = bind(s, lo, count, node)) return r;
         }
         base = s.spheres;
         return mirt_intersect_rays(s.ctx, &ray, 1, 1, &h);

@@ -248,11 +248,13 @@ __device__ __forceinline__ void store_pixel(const FrameConst& f, uint32_t* __res
     out[i] = shown;
 }
 
-// A launch of f.samples > 1 frames with an accumulation buffer: the kernels
-// wrote each frame's colours to its own slab of `out`; fold them into `acc`
-// in frame order, exactly as f.samples successive store_pixel calls would
-// (frame j: fresh if j == 0 and !f.accumulate, else divisor f.frames + j),
-// and leave the display after the last frame in slab 0.
+// A launch of f.samples > 1 frames with an accumulation buffer (or any frame
+// of a ctx whose accumulation buffer is shared, mirt_ctx_share_accum): the
+// kernels wrote each frame's colours to its own slab of `out`; fold them
+// into `acc` in frame order, exactly as f.samples successive store_pixel
+// calls would (frame j: fresh if j == 0 and !f.accumulate, else divisor
+// f.frames + j), leaving in slab j the display main.c:394-405 shows after
+// frame j.
 __global__ void fold_samples_kernel(FrameConst f, uint32_t* __restrict__ out, float* __restrict__ acc)
 {
     const size_t n = (size_t)f.shard_rows * f.width;
@@ -260,10 +262,9 @@ __global__ void fold_samples_kernel(FrameConst f, uint32_t* __restrict__ out, fl
     if (i >= n) return;
     float* a = acc + 3 * i;
     float a0 = a[0], a1 = a[1], a2 = a[2];
-    uint32_t shown = 0;
     for (int j = 0; j < f.samples; j++) {
         const uint32_t c = out[(size_t)j * n + i];
-        shown = c;
+        uint32_t shown = c;
         float* ch[3] = {&a0, &a1, &a2};
         for (int k = 0; k < 3; k++) {
             const float v = (float)((c >> (8 * k)) & 0xff) / 255.0f;       // main.c:368-370 / 394-396
@@ -276,11 +277,11 @@ __global__ void fold_samples_kernel(FrameConst f, uint32_t* __restrict__ out, fl
                 shown = (shown & ~(0xffu << (8 * k))) | ((q & 0xffu) << (8 * k));
             }
         }
+        out[(size_t)j * n + i] = shown;
     }
     a[0] = a0;
     a[1] = a1;
     a[2] = a2;
-    out[i] = shown;
 }
 
 __device__ __forceinline__ uint32_t lanes_below(uint64_t mask)
@@ -978,6 +979,26 @@ __global__ void overlay_colour_kernel(const uint32_t* __restrict__ last, const u
 
 // ------------------------------------------------------------------ context
 
+constexpr int kPhaseRing = 64;  // frames of pass timings kept per ctx (mirt_phase_log)
+
+// The float accumulation buffer of main.c:241-273 (x-major there, row-major
+// float3 here). One per ctx by default; mirt_ctx_share_accum lets the ctxs
+// that keep frames of one display loop in flight (main.c:379-408, one ctx
+// per hardware queue) use ONE buffer: every frame's colours then go to its
+// own slab and a fold kernel adds them to the buffer, the folds of
+// successive calls ordered across the ctxs' streams by `folded` (the event
+// of the last fold enqueued, on whichever stream) -- the tracing overlaps,
+// only the folds (a few microseconds each) run in call order.
+struct AccumShare {
+    int refs = 1;
+    int device = 0;
+    float* d_acc = nullptr;
+    size_t cap = 0;          // bytes allocated
+    size_t pixels = 0;       // pixels of the running accumulation (0: none yet)
+    hipEvent_t folded = nullptr;
+    bool has_fold = false;   // `folded` was recorded at least once
+};
+
 struct mirt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -985,7 +1006,12 @@ struct mirt_ctx {
     bool timed_recorded = false;  // ev0/ev1 bracket a launch (mirt_last_kernel_ms)
     float last_ms = 0.0f;
     // wavefront phase boundaries of the last frame (any API)
-    hipEvent_t ph0 = nullptr, ph1 = nullptr, ph2 = nullptr;
+    // (a ring of kPhaseRing frames: mirt_phase_log reads back the passes of
+    // frames that ran overlapped with other ctxs' frames, without a sync
+    // between them)
+    hipEvent_t ph0[kPhaseRing] = {}, ph1[kPhaseRing] = {}, ph2[kPhaseRing] = {};
+    uint32_t ph_next = 0;   // ring slot of the next wavefront frame
+    uint32_t ph_count = 0;  // wavefront frames recorded (saturates at kPhaseRing)
     bool phases_valid = false;
     // the frame scratch (queue, deferral list, phase events) is per ctx: a
     // launch on another stream than the previous one waits for it
@@ -1000,8 +1026,8 @@ struct mirt_ctx {
     int num_nodes = 0, num_spheres = -1;
     // frame buffers owned by the ctx (blocking API)
     uint32_t* d_out = nullptr;
-    float* d_acc = nullptr;
-    size_t out_cap = 0, acc_cap = 0, acc_pixels = 0;
+    size_t out_cap = 0;
+    AccumShare* acc = nullptr;  // accumulation buffer (own, or shared: mirt_ctx_share_accum)
     // staging for batch calls
     void* d_in = nullptr;
     void* d_res = nullptr;
@@ -1068,6 +1094,23 @@ int ensure(void** p, size_t* cap, size_t bytes)
 // inner box holds both children's boxes; the reference's own trees are built
 // that way. Also returns the scene constants of the bound. A NaN anywhere,
 // a non-finite sphere or a tree that does not nest turns pruning off.
+// A 0-sphere leaf whose sphere (hit.c:96-97 tests it) is no non-empty leaf's
+// tested sphere: a tree built over part of an array (benchmark.c:317 builds
+// over [0, n - 1)) whose SAH fallback left a last leaf empty points at the
+// element after the range, which only that leaf tests. The pruned and
+// ordered walks drop 0-sphere leaves (dead_leaf), so such a tree is walked
+// in the reference's DFS order instead.
+bool orphan_phantoms(const mirt_node* nd, int nn, int ns)
+{
+    std::vector<char> tested((size_t)ns + 1, 0);
+    for (int i = 0; i < nn; i++)
+        if (nd[i].sphere >= 0 && nd[i].sphere < ns && !(nd[i].skip & MIRT_NODE_EMPTY)) tested[nd[i].sphere] = 1;
+    for (int i = 0; i < nn; i++)
+        if (nd[i].sphere >= 0 && nd[i].sphere < ns && (nd[i].skip & MIRT_NODE_EMPTY) && !tested[nd[i].sphere])
+            return true;
+    return false;
+}
+
 bool tree_encloses(const mirt_sphere* sp, int ns, const mirt_node* nd, int nn, float* r_max, float* c_max)
 {
     float rm = 0.0f, cm = 0.0f;
@@ -1105,8 +1148,22 @@ bool tree_encloses(const mirt_sphere* sp, int ns, const mirt_node* nd, int nn, f
     return true;
 }
 
-// A leaf that can never report a hit: a 0-sphere leaf (its sphere is tested
-// by a real leaf under the same ancestors) or the &spheres[N] sentinel.
+// A leaf the fast walks may drop: the &spheres[N] sentinel (never hits), or
+// a 0-sphere leaf. hit.c:96-97 does test a 0-sphere leaf's sphere (its box,
+// create_empty_aabb's, always passes): spheres[start] of its range when the
+// SAH fallback split left it empty (mid == start: the first sphere of its
+// sibling's range), spheres[end] when it split right (mid == end: a sphere
+// of some LATER subtree). Dropping it is exact when that sphere is the
+// tested sphere of a non-empty leaf (upload checks this, `orphan_phantoms`;
+// otherwise only the reference-order DFS walk runs) and the ray reaches that
+// leaf whenever it hits the sphere: the leaf's box holds the sphere's box
+// fl(c -+ r) (checked, tree_encloses), the reference slab test is monotone
+// under containment, so this rests on ONE assumption -- hit.c:49-82's
+// division slab test passes the box fl(c -+ r) of every sphere that
+// hit.c:19-39 reports hit. Both are exact-rounding computations of the same
+// chord; tests/test_gpu_parity.py test_phantom_grazing_rays aims grazing rays
+// at the spheres of both kinds of 0-sphere leaf and compares the fast walks
+// with the DFS walk and the oracle.
 bool dead_leaf(const mirt_node* nd, uint32_t i, int ns)
 {
     return nd[i].sphere >= 0 && ((nd[i].skip & MIRT_NODE_EMPTY) || nd[i].sphere >= ns);
@@ -1319,6 +1376,48 @@ DevScene dev_scene(const mirt_ctx* c)
                     ordered ? c->num_hnodes : 0u};
 }
 
+AccumShare* accum_new(int device)
+{
+    AccumShare* a = new (std::nothrow) AccumShare();
+    if (!a) return nullptr;
+    a->device = device;
+    if (hipEventCreateWithFlags(&a->folded, hipEventDisableTiming) != hipSuccess) {
+        delete a;
+        return nullptr;
+    }
+    return a;
+}
+
+void accum_release(AccumShare* a)
+{
+    if (!a || --a->refs > 0) return;
+    if (a->d_acc) (void)hipFree(a->d_acc);
+    if (a->folded) (void)hipEventDestroy(a->folded);
+    delete a;
+}
+
+// The accumulation buffer for frames of `pixels` pixels, enqueued on stream
+// s: (re)allocated if too small, cleared when the frame geometry changes
+// (a new accumulation starts). Ordered behind the share's last fold.
+int accum_prepare(AccumShare* a, size_t pixels, hipStream_t s)
+{
+    if (a->cap < pixels * 12 + 4) {
+        // other ctxs' streams may still fold into the old buffer
+        if (a->d_acc) HIP_TRY(hipDeviceSynchronize());
+        int rc = ensure((void**)&a->d_acc, &a->cap, pixels * 12 + 4);
+        if (rc) return rc;
+        a->pixels = 0;
+    }
+    if (a->pixels != pixels) {
+        if (a->has_fold) HIP_TRY(hipStreamWaitEvent(s, a->folded, 0));
+        HIP_TRY(hipMemsetAsync(a->d_acc, 0, pixels * 12, s));
+        HIP_TRY(hipEventRecord(a->folded, s));
+        a->has_fold = true;
+        a->pixels = pixels;
+    }
+    return MIRT_OK;
+}
+
 bool ctx_ok(mirt_ctx* c, bool need_scene, const char* fn)
 {
     if (!c) {
@@ -1343,13 +1442,21 @@ void dispatch_render(bool fast, const DevScene& sc, const FrameConst& f, uint32_
 }
 
 int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_acc, hipStream_t s, bool timed,
-                       mirt_counts* d_counts, uint32_t* d_wave_stats, uint64_t* d_bdiag);
+                       mirt_counts* d_counts, uint32_t* d_wave_stats, uint64_t* d_bdiag, AccumShare* chain);
+
+// The accumulation chain of a frame of ctx c: its share when other ctxs hold
+// it too (their folds must be ordered), else none.
+AccumShare* accum_chain(const mirt_ctx* c)
+{
+    return c->acc && c->acc->refs > 1 ? c->acc : nullptr;
+}
 
 int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_acc, hipStream_t s, bool timed,
                   mirt_counts* d_counts, uint32_t* d_wave_stats = nullptr, uint64_t* d_bdiag = nullptr)
 {
     if (c->launched && c->last_stream != s) HIP_TRY(hipStreamWaitEvent(s, c->done, 0));
-    const int rc = launch_render_body(c, f, d_out, d_acc, s, timed, d_counts, d_wave_stats, d_bdiag);
+    const int rc = launch_render_body(c, f, d_out, d_acc, s, timed, d_counts, d_wave_stats, d_bdiag,
+                                      d_counts ? nullptr : accum_chain(c));
     if (rc) return rc;
     HIP_TRY(hipEventRecord(c->done, s));
     c->last_stream = s;
@@ -1358,7 +1465,7 @@ int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_ac
 }
 
 int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_acc, hipStream_t s, bool timed,
-                       mirt_counts* d_counts, uint32_t* d_wave_stats, uint64_t* d_bdiag)
+                       mirt_counts* d_counts, uint32_t* d_wave_stats, uint64_t* d_bdiag, AccumShare* chain)
 {
     const int tiles = ((f.width + 7) / 8) * ((f.num_rows + 7) / 8);
     const int bw = c->block_waves;
@@ -1368,22 +1475,34 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
         HIP_TRY(hipEventRecord(c->ev0, s));
         c->timed_recorded = true;
     }
-    // several frames and an accumulation buffer: raw colours per frame, then
-    // fold_samples_kernel accumulates them in order
-    float* const d_fold = f.samples > 1 ? d_acc : nullptr;
+    // several frames, or a buffer shared with other ctxs' frames in flight,
+    // and an accumulation buffer: raw colours per frame, then
+    // fold_samples_kernel accumulates them in order (behind the previous
+    // fold into a shared buffer, whichever stream enqueued it)
+    float* const d_fold = f.samples > 1 || chain ? d_acc : nullptr;
     if (d_fold) d_acc = nullptr;
     auto fold = [&]() -> int {
         if (!d_fold) return MIRT_OK;
         const size_t n = (size_t)f.shard_rows * f.width;
+        if (chain && chain->has_fold) HIP_TRY(hipStreamWaitEvent(s, chain->folded, 0));
         fold_samples_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(f, d_out, d_fold);
         HIP_TRY(hipGetLastError());
+        if (chain) {
+            HIP_TRY(hipEventRecord(chain->folded, s));
+            chain->has_fold = true;
+        }
         return MIRT_OK;
     };
     const bool wavefront = c->trav == kTravWavefront && f.use_bvh && f.depth >= 2 && !d_counts;
     const int dbw = wavefront ? 4 : bw;  // the wavefront kernels use 256-thread workgroups
     Deferred dfr{nullptr, nullptr, 0};
     c->phases_valid = wavefront;
-    if (wavefront) HIP_TRY(hipEventRecord(c->ph0, s));
+    const uint32_t ps = c->ph_next;
+    if (wavefront) {
+        HIP_TRY(hipEventRecord(c->ph0[ps], s));
+        c->ph_next = (ps + 1) % kPhaseRing;
+        c->ph_count = std::min<uint32_t>(c->ph_count + 1, kPhaseRing);
+    }
     const DevScene sc = dev_scene(c);
     // the ordered packet walk takes zero-component camera rays itself
     if (f.use_bvh && c->defer && !sc.ordered) {
@@ -1419,7 +1538,7 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
         else
             primary_kernel<false, false><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(c->ph1, s));
+        HIP_TRY(hipEventRecord(c->ph1[ps], s));
         if (d_bdiag && sc.wide)
             bounce_kernel<true, 2, true><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, d_bdiag);
         else if (d_bdiag)
@@ -1431,7 +1550,7 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
         else
             bounce_kernel<false, 0><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(c->ph2, s));
+        HIP_TRY(hipEventRecord(c->ph2[ps], s));
         if (int rc = fold()) return rc;
         if (timed) HIP_TRY(hipEventRecord(c->ev1, s));
         return MIRT_OK;
@@ -1502,11 +1621,17 @@ int mirt_create(int device, mirt_ctx** out)
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&c->ev0);
     if (e == hipSuccess) e = hipEventCreate(&c->ev1);
-    if (e == hipSuccess) e = hipEventCreate(&c->ph0);
-    if (e == hipSuccess) e = hipEventCreate(&c->ph1);
-    if (e == hipSuccess) e = hipEventCreate(&c->ph2);
+    for (int k = 0; k < kPhaseRing && e == hipSuccess; k++) {
+        e = hipEventCreate(&c->ph0[k]);
+        if (e == hipSuccess) e = hipEventCreate(&c->ph1[k]);
+        if (e == hipSuccess) e = hipEventCreate(&c->ph2[k]);
+    }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipMalloc((void**)&c->d_counts, sizeof(mirt_counts));
+    if (e == hipSuccess) {
+        c->acc = accum_new(device);
+        if (!c->acc) e = hipErrorOutOfMemory;
+    }
     if (e == hipSuccess) {
         int cus = 0, per_cu = 0;
         e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
@@ -1528,15 +1653,18 @@ void mirt_destroy(mirt_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (void* p : {(void*)c->d_nodes, (void*)c->d_nodes32, (void*)c->d_geo, (void*)c->d_color, (void*)c->d_out, (void*)c->d_acc,
+    accum_release(c->acc);
+    for (void* p : {(void*)c->d_nodes, (void*)c->d_nodes32, (void*)c->d_geo, (void*)c->d_color, (void*)c->d_out,
                     c->d_in, c->d_res, (void*)c->d_counts, (void*)c->d_defer, c->d_queue, (void*)c->d_keys, (void*)c->d_pnodes,
                     (void*)c->d_hnodes, (void*)c->d_haux, (void*)c->d_leaves, (void*)c->d_ndepth,
                     (void*)c->d_overlay})
         if (p) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
-    for (hipEvent_t ev : {c->ph0, c->ph1, c->ph2, c->done})
-        if (ev) (void)hipEventDestroy(ev);
+    for (int k = 0; k < kPhaseRing; k++)
+        for (hipEvent_t ev : {c->ph0[k], c->ph1[k], c->ph2[k]})
+            if (ev) (void)hipEventDestroy(ev);
+    if (c->done) (void)hipEventDestroy(c->done);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1552,7 +1680,7 @@ try {
     // out of bounds
     if (int rc = validate_flat(nodes, nn, ns, 0, "mirt_scene_upload_flat")) return rc;
     float r_max = 0.0f, c_max = 0.0f;
-    const bool encloses = tree_encloses(spheres, ns, nodes, nn, &r_max, &c_max);
+    const bool encloses = tree_encloses(spheres, ns, nodes, nn, &r_max, &c_max) && !orphan_phantoms(nodes, nn, ns);
     std::vector<float4> geo((size_t)ns + 1);
     std::vector<uint32_t> col((size_t)ns + 1);
     for (int i = 0; i < ns; i++) {
@@ -1682,18 +1810,16 @@ int enqueue_host_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_des
         return MIRT_E_NOSCENE;
     }
     const FrameConst f = make_frame_const(cam, fd);
-    const size_t pixels = (size_t)f.shard_rows * f.width;  // one frame (several: folded into slab 0)
+    const size_t pixels = (size_t)f.shard_rows * f.width;  // one frame (several: slab j = display after frame j)
     int rc = ensure((void**)&c->d_out, &c->out_cap, pixels * f.samples * 4 + 4);
     if (rc) return rc;
-    rc = ensure((void**)&c->d_acc, &c->acc_cap, pixels * 12 + 4);
+    // a new frame geometry starts a fresh accumulation buffer
+    rc = accum_prepare(c->acc, pixels, c->stream);
     if (rc) return rc;
-    if (c->acc_pixels != pixels) {  // a new frame geometry starts a fresh accumulation buffer
-        HIP_TRY(hipMemsetAsync(c->d_acc, 0, pixels * 12, c->stream));
-        c->acc_pixels = pixels;
-    }
-    rc = launch_render(c, f, c->d_out, c->d_acc, c->stream, true, nullptr);
+    rc = launch_render(c, f, c->d_out, c->acc->d_acc, c->stream, true, nullptr);
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(out, c->d_out, pixels * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(out, c->d_out + (size_t)(f.samples - 1) * pixels, pixels * 4, hipMemcpyDeviceToHost,
+                           c->stream));
     return MIRT_OK;
 }
 
@@ -1738,11 +1864,40 @@ void mirt_host_free(void* p)
 int mirt_accum_download(mirt_ctx* c, float* out, size_t count)
 {
     if (!ctx_ok(c, false, "mirt_accum_download") || !out) return MIRT_E_INVALID;
-    if (count > c->acc_pixels * 3) {
-        set_error("mirt_accum_download: %zu floats requested, %zu held", count, c->acc_pixels * 3);
+    AccumShare* a = c->acc;
+    if (count > a->pixels * 3) {
+        set_error("mirt_accum_download: %zu floats requested, %zu held", count, a->pixels * 3);
         return MIRT_E_INVALID;
     }
-    HIP_TRY(hipMemcpy(out, c->d_acc, count * sizeof(float), hipMemcpyDeviceToHost));
+    // after every fold enqueued so far, whichever ctx's stream carries it
+    if (a->has_fold) HIP_TRY(hipStreamWaitEvent(c->stream, a->folded, 0));
+    HIP_TRY(hipMemcpyAsync(out, a->d_acc, count * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return MIRT_OK;
+}
+
+int mirt_ctx_share_accum(mirt_ctx* c, mirt_ctx* owner)
+{
+    if (!ctx_ok(c, false, "mirt_ctx_share_accum")) return MIRT_E_INVALID;
+    if (owner && owner->device != c->device) {
+        set_error("mirt_ctx_share_accum: ctxs on devices %d and %d", c->device, owner->device);
+        return MIRT_E_INVALID;
+    }
+    AccumShare* next = owner && owner != c ? owner->acc : nullptr;
+    if (next == c->acc) return MIRT_OK;
+    if (!next) {
+        next = accum_new(c->device);
+        if (!next) {
+            set_error("mirt_ctx_share_accum: out of host memory");
+            return MIRT_E_NOMEM;
+        }
+    } else {
+        next->refs++;
+    }
+    // c's frames enqueued so far still use its old buffer
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    accum_release(c->acc);
+    c->acc = next;
     return MIRT_OK;
 }
 
@@ -2079,10 +2234,25 @@ int mirt_last_phase_ms(mirt_ctx* c, float* phase)
         return MIRT_E_INVALID;
     }
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipEventSynchronize(c->ph2));
-    HIP_TRY(hipEventElapsedTime(&phase[0], c->ph0, c->ph1));
-    HIP_TRY(hipEventElapsedTime(&phase[1], c->ph1, c->ph2));
+    const uint32_t k = (c->ph_next + kPhaseRing - 1) % kPhaseRing;
+    HIP_TRY(hipEventSynchronize(c->ph2[k]));
+    HIP_TRY(hipEventElapsedTime(&phase[0], c->ph0[k], c->ph1[k]));
+    HIP_TRY(hipEventElapsedTime(&phase[1], c->ph1[k], c->ph2[k]));
     return MIRT_OK;
+}
+
+int mirt_phase_log(mirt_ctx* c, float* out, int max)
+{
+    if (!c || max < 0 || (max > 0 && !out)) return MIRT_E_INVALID;
+    HIP_TRY(hipSetDevice(c->device));
+    const int n = std::min<int>(max, (int)c->ph_count);
+    for (int j = 0; j < n; j++) {  // oldest first
+        const uint32_t k = (c->ph_next + kPhaseRing - (uint32_t)(n - j)) % kPhaseRing;
+        HIP_TRY(hipEventSynchronize(c->ph2[k]));
+        HIP_TRY(hipEventElapsedTime(&out[2 * j], c->ph0[k], c->ph1[k]));
+        HIP_TRY(hipEventElapsedTime(&out[2 * j + 1], c->ph1[k], c->ph2[k]));
+    }
+    return n;
 }
 
 int mirt_set_option(mirt_ctx* c, int option, int value)

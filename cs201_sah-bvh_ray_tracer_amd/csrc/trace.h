@@ -1317,7 +1317,9 @@ __device__ __forceinline__ uint32_t blend_rgba(uint32_t base, uint32_t refl)
 // as a packet, bounces per lane). WAVEFRONT (default, depth >= 2): camera
 // rays as packets, then persistent per-lane bounce chains fed by a queue
 // (render.hip primary_kernel / bounce_kernel).
-enum Trav { kTravTile = 0, kTravWavefront = 1 };
+// (ids as in include/mirt.h: 5 is the round-1 value of WAVEFRONT, kept so
+// that the retired ids 1-4 are rejected rather than silently remapped)
+enum Trav { kTravTile = 0, kTravWavefront = 5 };
 
 // trace_ray (renderer.c:21-77) with the recursion turned into a loop over
 // bounce levels that the whole wave executes together (the traversal needs

@@ -277,6 +277,12 @@ class Renderer:
                                               C.c_void_p(d_acc) if d_acc else None,
                                               C.c_void_p(stream or 0)), "mirt_render_frame_device")
 
+    def share_accum(self, owner):
+        """Use `owner`'s accumulation buffer (mirt_ctx_share_accum): the ctxs
+        of one accumulating display loop with frames in flight; None: a
+        private buffer again."""
+        check(self.L.mirt_ctx_share_accum(self.h, owner.h if owner is not None else None), "mirt_ctx_share_accum")
+
     def accum(self, count):
         out = np.zeros(count, np.float32)
         check(self.L.mirt_accum_download(self.h, ptr(out), count), "mirt_accum_download")
@@ -335,6 +341,14 @@ class Renderer:
         out = (C.c_float * 2)()
         check(self.L.mirt_last_phase_ms(self.h, out), "mirt_last_phase_ms")
         return float(out[0]), float(out[1])
+
+    def phase_log(self, n=64):
+        """(primary ms, bounce ms) of each of the ctx's last <= n wavefront
+        frames, oldest first, from HIP events on each frame's own stream
+        (durations under whatever overlap the frames ran with); waits."""
+        out = (C.c_float * (2 * n))()
+        k = check(self.L.mirt_phase_log(self.h, out, n), "mirt_phase_log")
+        return [(float(out[2 * j]), float(out[2 * j + 1])) for j in range(k)]
 
     def bvh_overlay(self, cam, width, height, max_levels=-1):
         """The BVH debug view (bvh_visualiser.c:16-126) of the uploaded tree:

@@ -14,8 +14,8 @@ same bytes as one GPU.
 Frames in flight (`samples` > 1): one launch renders this rank's rows of
 `samples` successive frames of the accumulating display loop (main.c:379-408,
 RNG samples sample .. sample + samples - 1) and folds them into the rank's
-accumulation buffer on the device; only the display after the last frame is
-gathered. The bounce pass's latency tail (its longest chains) is then paid
+accumulation buffer on the device (slab j holds the display after frame j);
+only the display after the last frame is gathered. The bounce pass's latency tail (its longest chains) is then paid
 once per launch rather than once per frame, which is what lets the frame
 rate grow with the number of GPUs: at N GPUs with samples = N every rank
 traces one frame's worth of rays per step (weak scaling).
@@ -96,8 +96,9 @@ class ShardedFrame:
         self.samples = samples
         dev = torch.device("cuda", torch.cuda.current_device())
         self.rows = slab_rows(height, row_block, self.world)
-        # per context: one slab per frame in flight (slab 0 is the display
-        # that is gathered) and the accumulation buffer of a multi-frame launch
+        # per context: one slab per frame in flight (the last one is the
+        # display that is gathered) and the accumulation buffer of a
+        # multi-frame launch
         self.bufs = []
         for _ in self.rs:
             slabs = torch.zeros((samples, self.rows, width), dtype=torch.int32, device=dev)
@@ -108,7 +109,7 @@ class ShardedFrame:
         self.streams = ([torch.cuda.ExternalStream(x.stream_handle) for x in self.rs] if len(self.rs) > 1
                         else [None])
         self.k = 0
-        self.slab = self.bufs[0][0][0]
+        self.slab = self.bufs[0][0][-1]
         self.stream = None
 
     def desc(self, depth=5, use_bvh=True, seed=1, sample=0, accumulate=False, frames=1, jitter=False):
@@ -124,7 +125,7 @@ class ShardedFrame:
         self.stream = self.streams[i] or torch.cuda.current_stream()
         self.rs[i].render_frame_device(cam, fd, slabs.data_ptr(), acc.data_ptr() if acc is not None else None,
                                        self.stream.cuda_stream)
-        self.slab = slabs[0]
+        self.slab = slabs[-1]
         return self.slab
 
     def gather(self):

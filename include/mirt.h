@@ -107,7 +107,8 @@ typedef struct mirt_frame_desc {
                                 Output: `samples` consecutive slabs, one per frame; with an
                                 accumulation buffer, the frames are folded into it in order (as
                                 `samples` successive calls would: frame j has divisor frames + j)
-                                and slab 0 holds the display after the last one (main.c:379-408) */
+                                and slab j holds the display main.c:379-408 shows after frame j
+                                (the blocking / async calls return the last one) */
     int32_t jitter;          /* 1: camera rays through (x + jx, y + jy), j in [0, 1)^2 from the pixel's
                                 RNG contract stream (rng.h; BASELINE configs[4] "4 spp jittered" --
                                 the reference samples pixel corners only); 0: main.c:362-363 */
@@ -229,8 +230,10 @@ int mirt_render_frame(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_de
    into device memory: d_out = samples * num_rows * width packed RGBA8 (frame
    j's slab at j * num_rows * width). d_accum is a device float buffer of
    num_rows * width * 3 (may be NULL when fd->accumulate == 0); given with
-   samples > 1, the frames are folded into it and slab 0 receives the display
-   after the last. Inputs are already resident in HBM. The ctx's frame scratch
+   samples > 1, the frames are folded into it and slab j receives the display
+   after frame j. Given by ctxs that share their accumulation buffer
+   (mirt_ctx_share_accum), the folds into d_accum follow call order across
+   those ctxs' streams. Inputs are already resident in HBM. The ctx's frame scratch
    (bounce queue, deferral list) is one per ctx: a launch on a different
    stream than the ctx's previous launch first waits for that launch (an
    event), so frames of one ctx never overlap; use one ctx per stream for
@@ -248,7 +251,9 @@ int mirt_render_frame_device(mirt_ctx *ctx, const mirt_camera *cam, const mirt_f
    works too but the runtime stages it. Rotating two or three ctxs (each with
    the scene uploaded) keeps the GPU busy while earlier frames drain and
    copy: for frame k use ctx k % n, mirt_ctx_wait it first (its buffer from
-   frame k - n is then complete), then mirt_render_frame_async. */
+   frame k - n is then complete), then mirt_render_frame_async. For the
+   accumulating loop (main.c:379-408) the rotated ctxs must share ONE
+   accumulation buffer: mirt_ctx_share_accum(ctx[i], ctx[0]). */
 int mirt_render_frame_async(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_desc *fd, mirt_rgba8 *out);
 /* Block until every call enqueued on the ctx's stream has finished. */
 int mirt_ctx_wait(mirt_ctx *ctx);
@@ -257,8 +262,19 @@ int mirt_ctx_wait(mirt_ctx *ctx);
 int mirt_host_alloc(size_t bytes, void **out);
 void mirt_host_free(void *p);
 
-/* Download the ctx's accumulation buffer (row-major float3 of the shard). */
+/* Download the ctx's accumulation buffer (row-major float3 of the shard),
+   after every fold enqueued into it so far. */
 int mirt_accum_download(mirt_ctx *ctx, float *out, size_t count);
+
+/* Frames in flight of ONE accumulating display loop (main.c:379-408) on
+   several ctxs: ctx uses owner's accumulation buffer from now on (owner NULL
+   or ctx itself: a private buffer again). Each frame's colours then go to
+   the ctx's own slab and a fold kernel adds them to the shared buffer; the
+   folds run in call order across the ctxs' streams (events), the tracing
+   still overlaps. Without it every ctx accumulates only its own frames, so a
+   rotation of n ctxs would average 1/n of the frames. Both ctxs must be on
+   the same device; waits for ctx's enqueued frames first. */
+int mirt_ctx_share_accum(mirt_ctx *ctx, mirt_ctx *owner);
 
 /* trace_ray (renderer.c:21-77) on n arbitrary rays; ray i uses RNG contract
    pixel index i. */
@@ -336,6 +352,12 @@ float mirt_last_kernel_ms(mirt_ctx *ctx);
    phase[0] = deferral mark + primary kernel (camera rays), phase[1] = the
    bounce kernel. Returns MIRT_E_INVALID if no wavefront frame was launched. */
 int mirt_last_phase_ms(mirt_ctx *ctx, float *phase);
+/* The same two times for each of the ctx's last min(max, 64) wavefront
+   frames, oldest first (out[2j], out[2j + 1]), recorded by HIP events on the
+   frame's own stream -- so frames that ran while other ctxs' frames shared
+   the chip report their passes' durations under that overlap. Waits for
+   them; returns the number of frames written. */
+int mirt_phase_log(mirt_ctx *ctx, float *out, int max);
 
 /* Kernel schedule knobs (results are identical under every setting; only
    speed changes). MIRT_OPT_TRAVERSAL: MIRT_TRAV_WAVEFRONT (default: camera-ray
@@ -369,7 +391,10 @@ enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3,
                                        keeping frames in flight, ~1.5 per CU (384 on MI355X) */
        MIRT_OPT_QUAD_DRAIN = 11     /* four-wide bounce walk: 1 (default) = once the queue is dry
                                        and <= 16 lanes of a wave are busy, finish them as quads */ };
-enum { MIRT_TRAV_TILE = 0, MIRT_TRAV_WAVEFRONT = 1 };
+/* Traversal ids keep their first-release values (mirt 0.1: TILE 0, WAVEFRONT 5);
+   the retired ids 1-4 (per-lane / chunked / DFS-only schedules of mirt 0.1) and
+   the retired option ids 8, 10, 12, 13 return MIRT_E_INVALID. */
+enum { MIRT_TRAV_TILE = 0, MIRT_TRAV_WAVEFRONT = 5 };
 int mirt_set_option(mirt_ctx *ctx, int option, int value);
 int mirt_get_option(mirt_ctx *ctx, int option);
 

@@ -24,11 +24,19 @@
  * which replaces the whole loop of main.c:356-407 with one launch.
  *
  * Scenes: trace_ray / ray_bvh_intersect upload the caller's spheres and
- * pointer tree on first sight (keyed by the sphere pointer, count and root
- * pointer) and reuse them while the key is unchanged; call
- * mirt_dropin_invalidate() after changing sphere contents in place.
- * ray_bvh_intersect without a preceding trace_ray finds the sphere array from
- * the tree's leaf pointers (the lowest to the highest leaf sphere).
+ * pointer tree on first sight and reuse them while the key -- sphere
+ * pointer, count, root pointer AND a content fingerprint (the tree's top 31
+ * nodes, 32 strided spheres) -- is unchanged, so benchmark.c's free /
+ * malloc / rebuild loop (benchmark.c:306-324), whose new tree and array
+ * usually land at the old addresses, re-uploads without being told;
+ * mirt_dropin_invalidate() forces it (e.g. after changing a sphere in place
+ * that the fingerprint does not sample). ray_bvh_intersect without a
+ * preceding trace_ray finds the sphere array from the tree's leaf pointers:
+ * from the lowest leaf sphere to the end of the highest non-empty leaf's
+ * range -- or the whole array declared with mirt_dropin_scene, which a caller
+ * whose tree covers part of its array (benchmark.c:317 builds over
+ * [0, n - 1)) passes so that a 0-sphere leaf pointing at spheres[n - 1]
+ * tests it as hit.c:96-97 does.
  *
  * RNG: trace_ray's bounces draw from the per-pixel RNG contract
  * with seed/sample from mirt_dropin_rng and pixel index = the number of
@@ -57,6 +65,9 @@ int mirt_dropin_init(int device, int width, int height);
 void mirt_dropin_release(void);
 /* RNG contract of trace_ray's bounces; restarts the pixel counter at 0. */
 void mirt_dropin_rng(uint64_t seed, uint32_t sample);
+/* The caller's whole sphere array for ray_bvh_intersect calls whose tree lies
+   inside it (NULL / 0: none). Optional; see "Scenes" above. */
+int mirt_dropin_scene(const mirt_sphere *spheres, int num_spheres);
 /* Forget the uploaded scene (after changing sphere contents in place). */
 void mirt_dropin_invalidate(void);
 /* Status of the last drop-in call (MIRT_OK or a negative MIRT_E_*). */

@@ -90,12 +90,17 @@ def main():
     ap.add_argument("--copy", help="copy the raw counter CSVs here")
     ap.add_argument("--workload", default="1920,1080,10000,5",
                     help="W,H,spheres,depth the probe rendered (scripts/profile_kernel.py defaults)")
+    ap.add_argument("--pattern", default="t*_f*_d*.*",
+                    help="pass directories (scripts/pmc_probe.sh: t*_f*_d*.N; scripts/pmc_bench.sh: bench.N)")
+    ap.add_argument("--bounce-grid", type=int, default=0,
+                    help="count only bounce dispatches of this many work-items (the timed loop's launch shape)")
+    ap.add_argument("--name", default=None, help="config name for the output keys (default: the directory stem)")
     a = ap.parse_args()
     cfgs = collections.defaultdict(dict)
-    for d in sorted(glob.glob(os.path.join(a.root, "t*_f*_d*.*"))):
+    for d in sorted(glob.glob(os.path.join(a.root, a.pattern))):
         if d.endswith(".log"):
             continue
-        cfg = os.path.basename(d).rsplit(".", 1)[0]
+        cfg = a.name or os.path.basename(d).rsplit(".", 1)[0]
         f = os.path.join(d, "run_counter_collection.csv")
         if not os.path.exists(f):
             continue
@@ -106,6 +111,8 @@ def main():
         names = {}
         for r in csv.DictReader(open(f)):
             kern = kernel_of(r["Kernel_Name"])
+            if kern == "bounce" and a.bounce_grid and int(r["Grid_Size"]) != a.bounce_grid:
+                continue
             if kern:
                 acc[(kern, r["Counter_Name"])].append(float(r["Counter_Value"]))
                 names[kern] = r["Kernel_Name"]
@@ -123,7 +130,9 @@ def main():
             print(f"   {k:34s} {v}")
     if a.json:
         with open(a.json, "w") as f:
-            json.dump({"source": f"scripts/pmc_probe.sh -> {a.root}", "clock_hz": CLOCK_HZ,
+            json.dump({"source": f"{'scripts/pmc_bench.sh' if a.pattern.startswith('bench') else 'scripts/pmc_probe.sh'}"
+                                 f" -> {a.root}" + (f" (bounce dispatches of {a.bounce_grid} work-items)"
+                                                    if a.bounce_grid else ""), "clock_hz": CLOCK_HZ,
                        "workload": [int(v) for v in a.workload.split(",")],
                        "l2_peak_gbs": L2_PEAK_GBS, "hbm_peak_gbs": HBM_PEAK_GBS,
                        "method": __doc__.strip().split("\n\n", 2)[-1], "kernels": out}, f, indent=1)

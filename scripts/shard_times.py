@@ -44,6 +44,14 @@ def main():
     ap.add_argument("--pipeline", type=int, default=0, help="time P contexts in flight (bench loop)")
     ap.add_argument("--blocks", type=int, default=-1, help="bounce workgroups with --pipeline (-1: 1.5 per CU)")
     ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--scene", choices=("render", "bench"), default="render",
+                    help="create_random_sphere scene (main.c) or benchmark spheres (benchmark.c:307-314)")
+    ap.add_argument("--spp", type=int, default=1, help="jittered samples per frame (BASELINE configs[4]: 4)")
+    ap.add_argument("--batch", type=int, default=1,
+                    help="with --pipeline: consecutive frames per launch (each frame's display its own slab)")
+    ap.add_argument("--copy", action="store_true",
+                    help="with --pipeline: after every step a slab-sized D2D copy on one more stream, waiting "
+                         "for that step's frame (prices the RCCL gather's stream against the hardware queues)")
     a = ap.parse_args()
     if a.pipeline:
         return pipelined(a)
@@ -88,7 +96,8 @@ def main():
 
 def pipelined(a):
     W, H = a.width, a.height
-    s = mirt.create_random_spheres(a.spheres, 1)
+    s = (mirt.create_random_spheres(a.spheres, 1) if a.scene == "render"
+         else mirt.create_benchmark_spheres(a.spheres, 1))
     b = mirt.build_bvh(s)
     blocks = a.blocks if a.blocks >= 0 else 3 * torch.cuda.get_device_properties(0).multi_processor_count // 2
     rs = [mirt.Renderer(0) for _ in range(a.pipeline)]
@@ -99,12 +108,14 @@ def pipelined(a):
     cam = mirt.default_camera()
     for world in (int(w) for w in a.worlds.split(",")):
         rows = shard.slab_rows(H, 8, world)
-        frames = world if a.weak else 1
+        frames = a.spp * (world if a.weak else 1) * a.batch
         slabs = [torch.zeros((frames, rows, W), dtype=torch.int32, device="cuda") for _ in rs]
+        cstream = torch.cuda.Stream() if a.copy else None
+        dst = torch.zeros((rows, W), dtype=torch.int32, device="cuda") if a.copy else None
         accs = [torch.zeros((rows, W, 3), dtype=torch.float32, device="cuda") if frames > 1 else None for _ in rs]
         per = []
         for k in range(world):
-            fd = mirt.frame_desc(W, H, a.depth, True, 1, 0, False, 1, 8, k, world, frames)
+            fd = mirt.frame_desc(W, H, a.depth, True, 1, 0, False, 1, 8, k, world, frames, a.spp > 1)
 
             def run(n):
                 for i in range(n):
@@ -112,6 +123,10 @@ def pipelined(a):
                     rs[j].render_frame_device(cam, fd, slabs[j].data_ptr(),
                                               accs[j].data_ptr() if accs[j] is not None else None,
                                               streams[j].cuda_stream)
+                    if cstream is not None:
+                        cstream.wait_stream(streams[j])
+                        with torch.cuda.stream(cstream):
+                            dst.copy_(slabs[j][0])
             run(2 * len(rs))
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -119,7 +134,9 @@ def pipelined(a):
             torch.cuda.synchronize()
             el = time.perf_counter() - t0
             per.append(W * H * frames / world * a.steps / el / 1e6)
-        print(json.dumps({"spheres": a.spheres, "world": world, "frames": frames, "pipeline": a.pipeline,
+        print(json.dumps({"spheres": a.spheres, "scene": a.scene, "size": [W, H], "spp": a.spp, "copy": a.copy,
+                          "batch": a.batch,
+                          "world": world, "frames": frames, "pipeline": a.pipeline,
                           "blocks": blocks, "per_rank_mrays_s": [round(p, 1) for p in per],
                           "min_per_rank_mrays_s": round(min(per), 1),
                           "pred_job_mrays_s_no_gather": round(min(per) * world, 1)}), flush=True)

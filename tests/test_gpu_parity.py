@@ -153,7 +153,7 @@ def test_accumulate_matches_oracle(gpu, mirt, oracle, small):
     oracle.free(t)
 
 
-@pytest.mark.parametrize("depth,trav", [(5, 1), (1, 1), (5, 0)])
+@pytest.mark.parametrize("depth,trav", [(5, 5), (1, 5), (5, 0)])
 def test_frames_in_flight_match_successive_frames(gpu, mirt, oracle, small, depth, trav):
     """samples = 4 in one launch == 4 successive calls of the accumulating
     loop (main.c:379-408): same display, same accumulation buffer; checked
@@ -296,6 +296,61 @@ def test_async_host_frames_pipelined(gpu, mirt, golden):
             x.close()
 
 
+@pytest.mark.parametrize("W,H,n", [(160, 90, 1000), (1920, 1080, 10000)])
+def test_shared_accumulation_frames_in_flight(gpu, mirt, oracle, small, W, H, n):
+    """main.c:379-408 with frames in flight (INTEGRATION.md's interactive
+    recipe): four ctxs sharing ONE accumulation buffer (mirt_ctx_share_accum)
+    take successive frames of the still-camera loop with
+    mirt_render_frame_async, frame k waiting only for frame k - 4 on the
+    same ctx. Every host frame equals frame k of 8 successive blocking
+    mirt_render_frame calls on one ctx (and, at 160x90, the oracle's
+    accumulation, o_accumulate); the shared buffer equals the oracle's."""
+    s, b = _scene(mirt, "render", n)
+    cam = mirt.default_camera()
+    rs = [mirt.Renderer(0) for _ in range(4)]
+    bufs = [mirt.HostBuffer((H, W, 4)) for _ in rs]
+    try:
+        for x in rs:
+            x.upload(s, b)
+            x.share_accum(rs[0])
+            x.set_option(mirt.abi.OPT_BOUNCE_BLOCKS, 384)
+        got = [None] * 8
+        for k in range(8):
+            i = k % 4
+            rs[i].wait()
+            if k >= 4:
+                got[k - 4] = bufs[i].array.copy()
+            fd = mirt.frame_desc(W, H, depth=5, seed=4, sample=k, accumulate=k > 0, frames=k + 1)
+            rs[i].render_frame_async(cam, fd, bufs[i])
+        for k in range(4, 8):
+            rs[k % 4].wait()
+            got[k] = bufs[k % 4].array.copy()
+        acc_shared = rs[1].accum(W * H * 3)
+        gpu.upload(s, b)
+        for k in range(8):
+            seq = gpu.render_frame(cam, W, H, depth=5, seed=4, sample=k, accumulate=k > 0, frames=k + 1)
+            assert (got[k] == seq).all(), k
+        assert acc_shared.tobytes() == gpu.accum(W * H * 3).tobytes()
+        if n <= 1000:
+            t = oracle.build(small["render_1000_1_pre"].copy())
+            acc = np.zeros(W * H * 3, np.float32)
+            for k in range(8):
+                col = oracle.render(cam, W, H, s, t, depth=5, mode=1, seed=4, sample=k)
+                ref = oracle.accumulate(col, acc, k == 0, k + 1).reshape(H, W, 4)
+                assert (got[k] == ref).all(), k
+            oracle.free(t)
+            assert acc_shared.tobytes() == acc.tobytes()
+        # detached again: a private buffer
+        rs[1].share_accum(None)
+        with pytest.raises(mirt.MirtError):
+            rs[1].accum(W * H * 3)
+    finally:
+        for x in bufs:
+            x.close()
+        for x in rs:
+            x.close()
+
+
 def test_counts_match_oracle(gpu, mirt, oracle):
     s, b = _scene(mirt, "render", 10000)
     gpu.upload(s, b)
@@ -426,7 +481,7 @@ def test_sentinel_and_edge_scenes(gpu, mirt, oracle):
     assert (img == ref).all()
 
 
-@pytest.mark.parametrize("trav", [0, 1])
+@pytest.mark.parametrize("trav", [0, 5])
 @pytest.mark.parametrize("fast,prune,ordered", [(0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 1, 1)])
 @pytest.mark.parametrize("defer", [0, 1])
 def test_all_schedules_bit_identical(gpu, mirt, golden, small, scene1000, trav, fast, prune, ordered, defer):
@@ -640,3 +695,168 @@ def test_per_ray_surface_matches_reference(mirt, small, golden):
         mirt.free_bvh(root)
     finally:
         L.mirt_dropin_release()
+
+
+def _bench_like_phantom_scene(mirt):
+    """Three spheres at one centre (no SAH plane separates them: every
+    candidate cost is NaN, bvh.c:139-141 falls back to x < 0.0 and all go
+    left, so each level's right child is a 0-sphere leaf at &spheres[end])
+    plus a fourth sphere OUTSIDE the build range, as benchmark.c:317 builds
+    over [0, n - 1): the trailing 0-sphere leaves point at spheres[3], which
+    hit.c:96-97 tests whenever the ray passes the cluster's box."""
+    s = np.zeros(4, mirt.abi.SPHERE)
+    for i in range(3):
+        s[i]["center"] = (-1.0, 0.0, -10.0)
+        s[i]["radius"] = 1.0
+        s[i]["color"] = (200, 10 * i, 0, 255)
+    s[3]["center"] = (5.0, 0.0, -10.0)
+    s[3]["radius"] = 2.0
+    s[3]["color"] = (0, 0, 250, 255)
+    rays = np.zeros(6, mirt.abi.RAY)
+    rays["origin"] = [(-10, 0.9, -10.9), (-10, -0.9, -9.1), (-10, 0.0, -10.0), (-10, 0.9, -9.1), (-10, 1.5, -10),
+                      (-10, 0.95, -10.95)]
+    rays["direction"] = (1.0, 0.0, 0.0)
+    return s, rays
+
+
+def test_orphan_phantom_leaf_is_tested(gpu, mirt, oracle):
+    """A 0-sphere leaf pointing past its tree's range at a real sphere (the
+    benchmark.c:317 build over [0, n - 1)) is tested as hit.c:96-97 does --
+    the upload detects it and walks that tree in the reference's DFS order --
+    for the batch call (array of n) and for the drop-in ray_bvh_intersect
+    with the array declared (mirt_dropin_scene) or not (then spheres[n - 1]
+    lies past what the tree spans: the never-hit sentinel, not read)."""
+    import ctypes as C
+    s, rays = _bench_like_phantom_scene(mirt)
+    so = s.copy()
+    t = oracle.build(so, 0, 3, 20)
+    want4 = oracle.intersect(t, so, rays)
+    want3 = oracle.intersect(t, so[:3], rays)
+    oracle.free(t)
+    assert (want4["sphere"] == 3).sum() >= 2 and not (want3["sphere"] == 3).any()   # the case is real
+    root = mirt.build_bvh_node(s, 0, 3, 20)
+    try:
+        gpu.upload(s, root)
+        assert gpu.closest_hit(rays).tobytes() == want4.tobytes()
+        L = mirt.load()
+        abi = mirt.abi
+        base = s.ctypes.data
+        for declared, want in ((False, want3), (True, want4)):
+            assert L.mirt_dropin_scene(C.c_void_p(base) if declared else None, 4 if declared else 0) == 0
+            L.mirt_dropin_invalidate()
+            for i in range(len(rays)):
+                h = L.mirt_ray_bvh_intersect(abi.Ray.from_buffer_copy(rays[i].tobytes()), root)
+                assert L.mirt_dropin_status() == 0
+                assert h.hit_something == want[i]["hit"], (declared, i)
+                if h.hit_something:
+                    assert (h.object - base) // abi.SPHERE.itemsize == want[i]["sphere"], (declared, i)
+                    assert np.float32(h.t).tobytes() == want[i]["t"].tobytes(), (declared, i)
+    finally:
+        mirt.free_bvh(root)
+        mirt.load().mirt_dropin_scene(None, 0)
+        mirt.load().mirt_dropin_release()
+
+
+def test_dropin_rebinds_after_free_and_rebuild(mirt, oracle):
+    """benchmark.c:306-324's loop through the drop-in: free_bvh + free, then
+    the next point's spheres and tree -- here in the SAME sphere buffer and
+    with the same count, so the array pointer and count repeat and the root
+    usually comes back at the old address; the drop-in's content
+    fingerprint must re-upload (no mirt_dropin_invalidate), else it walks
+    the freed tree. Every hit equals the oracle's on that point's scene."""
+    import ctypes as C
+    abi = mirt.abi
+    L = mirt.load()
+    buf = np.zeros(400, abi.SPHERE)
+    base = buf.ctypes.data
+    st = mirt.RandState(7)
+    roots = []
+    try:
+        for n in (400, 400, 400, 300):
+            s = mirt.create_benchmark_spheres(n, state=st)
+            buf[:n] = s
+            root = mirt.build_bvh_node(buf, 0, n - 1, 20)      # benchmark.c:317
+            roots.append(root)
+            rays = mirt.create_bench_rays(64, st)
+            so = s.copy()
+            t = oracle.build(so, 0, n - 1, 20)
+            want = oracle.intersect(t, so, rays)
+            oracle.free(t)
+            for i in range(len(rays)):
+                h = L.mirt_ray_bvh_intersect(abi.Ray.from_buffer_copy(rays[i].tobytes()), root)
+                assert L.mirt_dropin_status() == 0
+                assert h.hit_something == want[i]["hit"], (n, i)
+                if h.hit_something:
+                    assert (h.object - base) // abi.SPHERE.itemsize == want[i]["sphere"], (n, i)
+                    assert np.float32(h.t).tobytes() == want[i]["t"].tobytes(), (n, i)
+            mirt.free_bvh(root)                               # benchmark.c:323-324
+            buf[:] = 0
+        print("root addresses", [hex(r) for r in roots], "repeated:", len(set(roots)) < len(roots))
+    finally:
+        L.mirt_dropin_release()
+
+
+def test_phantom_grazing_rays(gpu, mirt, oracle):
+    """The fast walks drop 0-sphere leaves (render.hip dead_leaf): exact if a
+    ray that hits a sphere always passes the box fl(c -+ r) of that sphere's
+    own leaf under hit.c:49-82's division test. Rays aimed at the silhouettes
+    (within 1e-3 .. 1e-6 of the radius) of the spheres that 0-sphere leaves of
+    both kinds point at (mid == start: spheres[start]; mid == end: spheres[end],
+    outside the leaf's subtree), from points inside the 0-sphere leaf's parent
+    box: the ordered / pruned walks == the reference-order DFS walk == the
+    oracle."""
+    s, b = _scene(mirt, "render", 10000)
+    nd = b.nodes
+    empty = np.nonzero((nd["sphere"] >= 0) & ((nd["skip"] & mirt.abi.NODE_EMPTY) != 0))[0]
+    assert len(empty) > 100
+    # parent of every node: pre-order, inner i has children i + 1 and skip(i + 1)
+    parent = np.full(len(nd), -1, np.int64)
+    for i in np.nonzero(nd["sphere"] < 0)[0]:
+        parent[i + 1] = i
+        parent[nd["skip"][i + 1] & mirt.abi.SKIP_MASK] = i
+    # the 0-sphere leaves that are their parent's right child point at
+    # spheres[end] of the parent's range (mid == end)
+    right = [e for e in empty if parent[e] >= 0 and e != parent[e] + 1]
+    left = [e for e in empty if parent[e] >= 0 and e == parent[e] + 1]
+    assert right and left
+    rng = np.random.default_rng(11)
+    pick = list(rng.choice(right, min(120, len(right)), replace=False)) + \
+        list(rng.choice(left, min(120, len(left)), replace=False))
+    rays = []
+    for e in pick:
+        j = nd["sphere"][e]
+        if j >= len(s):
+            continue
+        p = nd[parent[e]]
+        c = s[j]["center"].astype(np.float64)
+        r = float(s[j]["radius"])
+        for _ in range(8):
+            o = rng.uniform(p["bmin"], p["bmax"])
+            u = rng.normal(size=3)
+            to = c - o
+            to /= np.linalg.norm(to)
+            u -= u.dot(to) * to
+            u /= np.linalg.norm(u)
+            tgt = c + u * r * (1.0 - 10.0 ** rng.uniform(-6, -3))
+            d = tgt - o
+            d /= np.linalg.norm(d)
+            rays.append((o, d))
+    ray = np.zeros(len(rays), mirt.abi.RAY)
+    ray["origin"] = [o for o, _ in rays]
+    ray["direction"] = [d for _, d in rays]
+    gpu.upload(s, b)
+    fast = gpu.closest_hit(ray)
+    try:
+        gpu.set_option(mirt.abi.OPT_ORDERED, 0)
+        gpu.set_option(mirt.abi.OPT_PRUNE, 0)
+        dfs = gpu.closest_hit(ray)
+    finally:
+        gpu.set_option(mirt.abi.OPT_ORDERED, 1)
+        gpu.set_option(mirt.abi.OPT_PRUNE, 1)
+    s2 = mirt.create_random_spheres(10000, 1)
+    t = oracle.build(s2)
+    want = oracle.intersect(t, s2, ray)
+    oracle.free(t)
+    assert dfs.tobytes() == want.tobytes()
+    assert fast.tobytes() == want.tobytes()
+    assert int(want["hit"].sum()) > len(ray) // 4

@@ -325,3 +325,21 @@ def test_sanitizer_builds(tmp_path):
         p = subprocess.run([os.path.join(csrc, "build", exe), str(tmp_path)], capture_output=True, text=True,
                            timeout=600, env=env)
         assert p.returncode == 0 and "san_host: ok" in p.stdout, (exe, p.stdout[-1500:], p.stderr[-3000:])
+
+
+@pytest.mark.parametrize("kind,n,start,end,depth", [("render", 10000, 0, None, 0), ("render", 100000, 0, None, 0),
+                                                    ("bench", 20000, 0, None, 0), ("bench", 20000, 0, 19999, 20)])
+def test_phantom_leaves_are_covered(mirt, kind, n, start, end, depth):
+    """Every 0-sphere leaf of the BASELINE scenes' trees (and of a
+    benchmark.c:317-style build over [0, n - 1) from depth 20) points at a
+    sphere some non-empty leaf tests first, or at the never-hit index N: so
+    the upload keeps the fast walks (render.hip orphan_phantoms / dead_leaf)
+    on the trees the bench and the parity tests run."""
+    s = mirt.create_random_spheres(n, 1) if kind == "render" else mirt.create_benchmark_spheres(n, 1)
+    nd = mirt.build_bvh(s, start, end, depth).nodes
+    ns = (end if end is not None else n) - start
+    leaf = nd["sphere"] >= 0
+    empty = leaf & ((nd["skip"] & mirt.abi.NODE_EMPTY) != 0)
+    tested = set(nd["sphere"][leaf & ~empty].tolist())
+    pointed = set(nd["sphere"][empty].tolist())
+    assert pointed - tested <= {start + ns}, sorted(pointed - tested)[:5]
