@@ -86,6 +86,14 @@ WORKLOADS = {
 PEAK_HBM_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 PEAK_L2_GBS = 34500.0   # aggregate L2 (MI355X_MICROARCH.md §L2)
 NODE_B, SPHERE_B, COLOR_B, PIXEL_B = 32, 16, 4, 4
+# frames per launch by GPU count, measured at the driver's --steps 20: one
+# frame per launch is fastest at N = 1 (bench.py itself, profiles/r03c/:
+# 1 / 2 / 4 frames 2,358-2,408 / 2,142-2,206 / 2,062-2,064 Mrays/s); the
+# one-frame split at N ranks emulated shard by shard on one GPU
+# (scripts/shard_times.py --pipeline 4 --batch B, profiles/r03d/k20_*):
+# N = 2: 4,634 / 4,517 / 4,372, N = 4: 7,286 / 7,393 / 7,966, N = 8:
+# 9,460 / 11,243 / 13,735 Mrays/s before the gather
+DEFAULT_BATCH = {1: 1, 2: 1, 4: 4, 8: 4}
 KERNEL = "bounce_kernel<true, 2, false>"   # dominant kernel of the default (wavefront, four-wide) schedule
 # the PMC-derived bound of the timed launch shape, per workload
 # (scripts/pmc_bench.sh over this script's own command + scripts/pmc_summary.py)
@@ -267,16 +275,17 @@ def spawn_ranks(n):
     return rc
 
 
-def timed(world, steps, body):
-    """barrier + synchronize, `steps` bodies, synchronize + barrier; seconds."""
+def timed(world, launches, body):
+    """barrier + synchronize, body(*l) for every launch l of the timed steps,
+    synchronize + barrier; seconds."""
     cuda = torch.cuda.is_initialized()
     if world > 1:
         dist.barrier()
     if cuda:
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        body()
+    for launch in launches:
+        body(*launch)
     if cuda:
         torch.cuda.synchronize()
     if world > 1:
@@ -300,7 +309,7 @@ def dry_main(args, world, rank):
 
     for _ in range(args.warmup):
         step()
-    el = timed(world, args.steps, step)
+    el = timed(world, [()] * args.steps, step)
     t = torch.tensor([el], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -368,6 +377,11 @@ def main():
     ap.add_argument("--scaling", choices=("weak", "strong"), default="strong",
                     help="strong (default): every step is ONE frame (the N = 1 workload) split N ways, frames in "
                          "flight; weak: N frames per step at N GPUs (reported beside it as value_weak)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="steps' frames per launch (frames in flight inside a launch; 0 = DEFAULT_BATCH[N])")
+    ap.add_argument("--accumulate", action="store_true",
+                    help="time the still-camera accumulating display loop (shared accumulation buffer) instead "
+                         "of fresh frames")
     ap.add_argument("--dry", action="store_true", help="CPU plumbing check over gloo (no GPU, no measurement)")
     ap.add_argument("--opt", action="append", default=[],
                     help="OPTION=VALUE (mirt_set_option on every context; A/B of schedule options), repeatable")
@@ -413,19 +427,34 @@ def main():
             x.set_option(o, v)
     r = rs[0]
     cam = mirt.default_camera()
-    # frames (accumulated samples) in flight per step: SPP per frame x N at N GPUs (weak scaling)
-    frames = SPP * (world if args.scaling == "weak" else 1)
-    sf = shard.ShardedFrame(r, W, H, ROW_BLOCK, samples=frames, renderers=rs)
-    fd = sf.desc(depth=DEPTH, seed=SEED, jitter=JITTER)
+    # The steps are successive frames, `fps` per step: 1 (strong, the N = 1
+    # workload at every N) or N (weak). A frame is main.c:358-374's fresh
+    # frame (the camera moved), shown after its SPP samples (4k_1m_4spp: 4
+    # jittered samples folded like main.c:379-408's accumulation); with
+    # --accumulate the frames are instead successive frames of the
+    # still-camera display loop (main.c:379-408), the ctxs sharing one
+    # accumulation buffer (mirt_ctx_share_accum). A launch carries `batch`
+    # steps' frames (frames in flight inside one launch; each frame's display
+    # its own slab) and, at N > 1, every displayed frame is gathered to rank 0.
+    fps = world if args.scaling == "weak" else 1
+    batch = args.batch if args.batch > 0 else DEFAULT_BATCH.get(world, 1)
+    if SPP > 1 and not args.accumulate:
+        batch = 1          # one fresh frame of SPP samples per launch (the fold restarts per launch)
+    per_launch = fps * batch if SPP == 1 or args.accumulate else 1
+    if SPP > 1 and not args.accumulate and fps > 1:
+        raise SystemExit("--scaling weak with several samples per frame needs --accumulate")
+    sf = shard.ShardedFrame(r, W, H, ROW_BLOCK, samples=SPP * per_launch, renderers=rs,
+                            share_accum=args.accumulate, accum=SPP > 1 or args.accumulate)
     my_rows = shard.shard_row_count(H, ROW_BLOCK, world, rank)
 
-    # algorithmic work of this rank's launch (instrumented build, untimed):
-    # the walk as configured (pruned), and the reference's exhaustive DFS
+    # algorithmic work of one full launch of this rank (instrumented build,
+    # untimed): the walk as configured (pruned), and the reference's
+    # exhaustive DFS
     counts = r.count_frame(cam, W, H, depth=DEPTH, seed=SEED, row_block=ROW_BLOCK, shard=rank, num_shards=world,
-                           samples=frames, jitter=JITTER)
+                           samples=SPP * per_launch, jitter=JITTER)
     r.set_option(mirt.abi.OPT_PRUNE, 0)
     ref_counts = r.count_frame(cam, W, H, depth=DEPTH, seed=SEED, row_block=ROW_BLOCK, shard=rank,
-                               num_shards=world, samples=frames, jitter=JITTER)
+                               num_shards=world, samples=SPP * per_launch, jitter=JITTER)
     r.set_option(mirt.abi.OPT_PRUNE, 1)
 
     # a non-default stream for the serial measurement loop below (the timed
@@ -433,51 +462,69 @@ def main():
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
 
-    def step_fn(s, f):
-        def body():
-            s.render_local(cam, f)
+    def plan(f0, steps, per):
+        """(first frame, frames) of the launches covering `steps` steps from frame f0"""
+        out, f, end = [], f0, f0 + steps * fps
+        while f < end:
+            n = min(per, end - f)
+            out.append((f, n))
+            f += n
+        return out
+
+    def launcher(s, depth):
+        def run(f0, n):
+            acc = args.accumulate and f0 > 0
+            s.render_local(cam, s.desc(depth=depth, seed=SEED, sample=f0 * SPP, accumulate=acc,
+                                       frames=f0 * SPP + 1 if acc else 1, jitter=JITTER, samples=n * SPP))
             if world > 1:
-                s.gather()          # N = 1: the slab is the frame
-        return body
+                s.gather(every=SPP)       # every frame's display; N = 1: the slabs are the frames
+        return run
 
-    body = step_fn(sf, fd)
-    for _ in range(args.warmup):
-        body()
-    elapsed = timed(world, args.steps, body)
+    run = launcher(sf, DEPTH)
+    warm = plan(0, args.warmup, per_launch)
+    for p in warm:
+        run(*p)
+    timed_plan = plan(args.warmup * fps, args.steps, per_launch)
+    elapsed = timed(world, timed_plan, run)
 
-    # the two passes of every timed frame, from the HIP events the library
-    # records on each frame's own stream around its primary and bounce
+    # the two passes of every timed launch, from the HIP events the library
+    # records on each launch's own stream around its primary and bounce
     # kernels (mirt_phase_log): their durations UNDER the overlap of the timed
-    # loop (frames k % P on ctx k % P, warm-up frames first)
+    # loop (launch j on ctx j % P, the warm-up launches first)
     P = len(rs)
     timed_phases = []
     for i, x in enumerate(rs):
-        n_i = sum(1 for k in range(args.warmup, args.warmup + args.steps) if k % P == i)
+        n_i = sum(1 for j in range(len(warm), len(warm) + len(timed_plan)) if j % P == i)
         if n_i:
             timed_phases += x.phase_log(min(n_i, 64))
     primary_ms, bounce_ms = (float(v) for v in np.mean(np.array(timed_phases), axis=0))
 
     # SURVEY §8(d): depth 1 alongside (camera rays and their shading only)
-    body1 = step_fn(sf, sf.desc(depth=1, seed=SEED, jitter=JITTER))
-    for _ in range(2):
-        body1()
-    elapsed_d1 = timed(world, args.steps, body1)
+    run1 = launcher(sf, 1)
+    for p in plan(0, 2, per_launch):
+        run1(*p)
+    elapsed_d1 = timed(world, plan(0, args.steps, per_launch), run1)
 
     # the other scaling mode at N > 1 (same contexts, its own slabs)
-    elapsed_other, frames_other = None, None
+    elapsed_other, fps_other = None, None
     if world > 1:
-        frames_other = SPP * (1 if args.scaling == "weak" else world)
-        sf2 = shard.ShardedFrame(r, W, H, ROW_BLOCK, samples=frames_other, renderers=rs)
-        body2 = step_fn(sf2, sf2.desc(depth=DEPTH, seed=SEED, jitter=JITTER))
-        for _ in range(args.warmup):
-            body2()
-        elapsed_other = timed(world, args.steps, body2)
+        fps_other = 1 if args.scaling == "weak" else world
+        fps_main, fps = fps, fps_other
+        per_other = fps_other * batch if SPP == 1 or args.accumulate else 1
+        sf2 = shard.ShardedFrame(r, W, H, ROW_BLOCK, samples=SPP * per_other, renderers=rs,
+                                 share_accum=args.accumulate, accum=SPP > 1 or args.accumulate)
+        run2 = launcher(sf2, DEPTH)
+        for p in plan(0, args.warmup, per_other):
+            run2(*p)
+        elapsed_other = timed(world, plan(args.warmup * fps_other, args.steps, per_other), run2)
+        fps = fps_main
 
     # the same launch alone, one context, serial (untimed loop: each launch
     # waits for its events): torch events around the launch and the HIP
     # events the library records around the primary and bounce passes
-    slabs = torch.zeros((frames, sf.rows, W), dtype=torch.int32, device="cuda")
-    acc = torch.zeros((sf.rows, W, 3), dtype=torch.float32, device="cuda") if frames > 1 else None
+    fd = sf.desc(depth=DEPTH, seed=SEED, jitter=JITTER)          # one full launch
+    slabs = torch.zeros((SPP * per_launch, sf.rows, W), dtype=torch.int32, device="cuda")
+    acc = torch.zeros((sf.rows, W, 3), dtype=torch.float32, device="cuda") if SPP > 1 or args.accumulate else None
     phases, launch = [], []
     r.set_option(mirt.abi.OPT_BOUNCE_BLOCKS, 0)   # one launch alone: the full persistent grid
     for _ in range(min(args.steps, 20)):
@@ -500,11 +547,13 @@ def main():
 
     host = None
     if rank == 0 and world == 1 and not args.no_host:
+        for x in rs:
+            x.share_accum(None)          # a private buffer per ctx again (--accumulate shared one)
         host = host_inclusive(rs, cam, args.steps)
 
     if rank == 0:
-        value = W * H * frames * args.steps / elapsed / 1e6   # primary rays: W*H per sample
-        pixels = my_rows * W * frames
+        value = W * H * SPP * fps * args.steps / elapsed / 1e6   # primary rays: W*H per sample
+        pixels = my_rows * W * SPP * per_launch
         ref_frame_bytes = algorithmic_bytes(ref_counts, pixels)
         exec_frame_bytes = algorithmic_bytes(counts, pixels)
         ref_b = bounce_bytes(ref_counts)
@@ -535,17 +584,24 @@ def main():
             "config": {"workload": wl["desc"], "name": args.workload,
                        "width": W, "height": H, "spheres": NSPH, "scene": KIND, "max_depth": DEPTH, "spp": SPP,
                        "jitter": JITTER,
-                       "frames_per_step": frames, "pipeline": len(rs), "bounce_blocks": blocks, "bvh_nodes": len(bvh),
+                       "frames_per_step": fps, "frames_per_launch": per_launch, "launches": len(timed_plan),
+                       "pipeline": len(rs), "bounce_blocks": blocks, "bvh_nodes": len(bvh),
                        "row_block": ROW_BLOCK,
-                       "parallelism": f"row-block shard x{world}" + (" + RCCL gather" if world > 1 else "")
-                                      + (f", {frames} accumulated frames in flight" if frames > 1 else "")},
+                       "step": (f"{fps} frame(s) of the still-camera display loop (main.c:379-408), ctxs sharing "
+                                "one accumulation buffer (mirt_ctx_share_accum)" if args.accumulate else
+                                f"{fps} fresh frame(s) (main.c:358-374)")
+                               + f", {SPP} sample(s) each, {per_launch} frame(s) per launch with every frame's "
+                                 "display in its own slab, launches rotating over `pipeline` ctxs",
+                       "parallelism": f"row-block shard x{world}" + (" + RCCL gather of every frame" if world > 1
+                                                                     else "")},
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
                 "kernel": KERNEL, "kernel_ms": round(bounce_ms, 4),
-                "kernel_ms_source": f"mean over the {len(timed_phases)} timed frames of HIP events recorded on each "
-                                    "frame's own stream around its bounce launch (mirt_phase_log): the launch's "
-                                    "duration UNDER the timed loop's overlap of `pipeline` frames",
+                "kernel_ms_source": f"mean over the {len(timed_phases)} timed launches ({per_launch} frame(s) each) "
+                                    "of HIP events recorded on each launch's own stream around its bounce kernel "
+                                    "(mirt_phase_log): the launch's duration UNDER the timed loop's overlap of "
+                                    "`pipeline` launches",
                 "algorithmic_bytes_per_launch": int(ref_b),
                 "definition": "SURVEY 8(d): bytes of the REFERENCE's exhaustive DFS (hit.c:91-109, no pruning) "
                               "for the bounce levels at 32 B/node test + 16 B/sphere test + 4 B/hit colour + "
@@ -560,10 +616,10 @@ def main():
                 "primary_algorithmic_bytes": int(ref_frame_bytes - ref_b),
                 "primary_bound_measured": bound_line(pp, exec_frame_bytes - exec_b, ref_frame_bytes - ref_b,
                                                      primary_ms),
-                "frame_algorithmic_bytes": int(ref_frame_bytes),
-                "frame_executed_bytes": int(exec_frame_bytes),
+                "launch_algorithmic_bytes": int(ref_frame_bytes),
+                "launch_executed_bytes": int(exec_frame_bytes),
                 "frame_period_ms": round(elapsed / args.steps * 1e3, 4),
-                "frame_algorithmic_gbs": round(ref_frame_bytes / (elapsed / args.steps) / 1e9, 1),
+                "frame_algorithmic_gbs": round(ref_frame_bytes / batch / (elapsed / args.steps) / 1e9, 1),
                 "serial_launch": {
                     "note": "the same launch alone (untimed serial loop, the full persistent bounce grid): not "
                             "the timed configuration",
@@ -573,13 +629,13 @@ def main():
             "work": {k: int(v) for k, v in counts.items()},
             "work_reference_dfs": {k: int(v) for k, v in ref_counts.items() if k != "lane_steps"},
             "traced_rays_per_s_M": round(counts["rays"] * world / (elapsed / args.steps) / 1e6, 3),
-            "depth1_mrays_s": round(W * H * frames * args.steps / elapsed_d1 / 1e6, 3),
+            "depth1_mrays_s": round(W * H * SPP * fps * args.steps / elapsed_d1 / 1e6, 3),
             "bvh_build_s": round(build_s, 4),
         }
         if args.opt:
             line["options"] = args.opt
         if elapsed_other:
-            other = W * H * frames_other * args.steps / elapsed_other / 1e6
+            other = W * H * SPP * fps_other * args.steps / elapsed_other / 1e6
             line["value_weak"] = round(value if args.scaling == "weak" else other, 3)
             line["value_strong"] = round(other if args.scaling == "weak" else value, 3)
         if host is not None:

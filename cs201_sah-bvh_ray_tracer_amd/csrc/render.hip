@@ -1884,7 +1884,7 @@ int mirt_ctx_share_accum(mirt_ctx* c, mirt_ctx* owner)
         return MIRT_E_INVALID;
     }
     AccumShare* next = owner && owner != c ? owner->acc : nullptr;
-    if (next == c->acc) return MIRT_OK;
+    if (next == c->acc || (!next && c->acc->refs == 1)) return MIRT_OK;  // already so / already private
     if (!next) {
         next = accum_new(c->device);
         if (!next) {

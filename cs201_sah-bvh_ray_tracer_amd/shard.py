@@ -55,17 +55,23 @@ def assemble(stacked, height, row_block):
 
 
 def gather_frame(slab, height, row_block, group=None, dst=0):
-    """Gather every rank's (slab_rows, W) int32 slab to `dst` and assemble the
-    frame there. Returns the (height, W) int32 frame on dst, None elsewhere."""
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
+    """Gather every rank's (slab_rows, W) int32 slab -- or (frames, slab_rows,
+    W) slabs of several frames -- to `dst` and assemble the frame(s) there.
+    Returns the (height, W) / (frames, height, W) int32 frame(s) on dst, None
+    elsewhere."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
     if world == 1:
-        return assemble(slab.unsqueeze(0), height, row_block)
-    bufs = [torch.empty_like(slab) for _ in range(world)] if rank == dst else None
-    dist.gather(slab, bufs, dst=dst, group=group)
-    if rank != dst:
-        return None
-    return assemble(torch.stack(bufs), height, row_block)
+        bufs = [slab]
+    else:
+        bufs = [torch.empty_like(slab) for _ in range(world)] if rank == dst else None
+        dist.gather(slab.contiguous(), bufs, dst=dst, group=group)
+        if rank != dst:
+            return None
+    st = torch.stack(bufs)
+    if slab.dim() == 2:
+        return assemble(st, height, row_block)
+    return torch.stack([assemble(st[:, j], height, row_block) for j in range(slab.shape[0])])
 
 
 def as_rgba(frame_i32):
@@ -86,7 +92,8 @@ class ShardedFrame:
     stream carries the kernel and RCCL.
     """
 
-    def __init__(self, renderer, width, height, row_block=8, group=None, samples=1, renderers=None):
+    def __init__(self, renderer, width, height, row_block=8, group=None, samples=1, renderers=None,
+                 share_accum=False, accum=None):
         self.rs = list(renderers) if renderers else [renderer]
         self.r = self.rs[0]
         self.width, self.height, self.row_block = width, height, row_block
@@ -96,14 +103,23 @@ class ShardedFrame:
         self.samples = samples
         dev = torch.device("cuda", torch.cuda.current_device())
         self.rows = slab_rows(height, row_block, self.world)
-        # per context: one slab per frame in flight (the last one is the
-        # display that is gathered) and the accumulation buffer of a
-        # multi-frame launch
+        # per context: one slab per frame in flight (slab j: the display
+        # after frame j) and the accumulation buffer of a multi-frame launch.
+        # share_accum: the contexts render successive frames of ONE
+        # accumulating display loop (main.c:379-408) into one buffer, their
+        # folds ordered in call order (mirt_ctx_share_accum). accum=False: no
+        # accumulation buffer (a multi-frame launch leaves raw frames)
+        accum = samples > 1 if accum is None else accum
         self.bufs = []
-        for _ in self.rs:
+        shared = torch.zeros((self.rows, width, 3), dtype=torch.float32, device=dev) if share_accum else None
+        for x in self.rs:
             slabs = torch.zeros((samples, self.rows, width), dtype=torch.int32, device=dev)
-            acc = torch.zeros((self.rows, width, 3), dtype=torch.float32, device=dev) if samples > 1 else None
+            acc = shared if share_accum else (
+                torch.zeros((self.rows, width, 3), dtype=torch.float32, device=dev) if accum else None)
+            if share_accum and x is not self.rs[0]:
+                x.share_accum(self.rs[0])
             self.bufs.append((slabs, acc))
+        self.shared = share_accum
         # each context's own stream (created by mirt_create), seen by torch as
         # an external stream
         self.streams = ([torch.cuda.ExternalStream(x.stream_handle) for x in self.rs] if len(self.rs) > 1
@@ -112,28 +128,34 @@ class ShardedFrame:
         self.slab = self.bufs[0][0][-1]
         self.stream = None
 
-    def desc(self, depth=5, use_bvh=True, seed=1, sample=0, accumulate=False, frames=1, jitter=False):
+    def desc(self, depth=5, use_bvh=True, seed=1, sample=0, accumulate=False, frames=1, jitter=False, samples=None):
         from .renderer import frame_desc
         return frame_desc(self.width, self.height, depth, use_bvh, seed, sample, accumulate, frames, self.row_block,
-                          self.rank, self.world, self.samples, jitter)
+                          self.rank, self.world, self.samples if samples is None else samples, jitter)
 
     def render_local(self, cam, fd):
-        """Enqueue this rank's rows of the next frame; returns its display slab."""
+        """Enqueue this rank's rows of the next launch (fd.samples <= samples
+        frames); returns the display slab after its last frame."""
+        if max(fd.samples, 1) > self.samples:
+            raise ValueError(f"a launch of {fd.samples} frames, slabs for {self.samples}")
         i = self.k % len(self.rs)
         self.k += 1
         slabs, acc = self.bufs[i]
         self.stream = self.streams[i] or torch.cuda.current_stream()
         self.rs[i].render_frame_device(cam, fd, slabs.data_ptr(), acc.data_ptr() if acc is not None else None,
                                        self.stream.cuda_stream)
-        self.slab = slabs[-1]
+        self.launched = slabs[:max(fd.samples, 1)]
+        self.slab = self.launched[-1]
         return self.slab
 
-    def gather(self):
-        """Gather the last rendered slab (on its stream); the frame on rank 0."""
+    def gather(self, every=None):
+        """Gather the last launch's display slab (on its stream); the frame on
+        rank 0. every=k: the displays of every k-th frame of the launch (the
+        display after each group of k samples: one per displayed frame),
+        stacked."""
         with torch.cuda.stream(self.stream):
-            if self.world == 1:
-                return assemble(self.slab.unsqueeze(0), self.height, self.row_block)
-            return gather_frame(self.slab, self.height, self.row_block, self.group)
+            slab = self.slab if every is None else self.launched[every - 1::every]
+            return gather_frame(slab, self.height, self.row_block, self.group)
 
     def render(self, cam, fd):
         """Render this rank's rows and gather; the (H, W) int32 frame on rank 0."""

@@ -112,7 +112,10 @@ def pipelined(a):
         slabs = [torch.zeros((frames, rows, W), dtype=torch.int32, device="cuda") for _ in rs]
         cstream = torch.cuda.Stream() if a.copy else None
         dst = torch.zeros((rows, W), dtype=torch.int32, device="cuda") if a.copy else None
-        accs = [torch.zeros((rows, W, 3), dtype=torch.float32, device="cuda") if frames > 1 else None for _ in rs]
+        # an accumulation buffer folds the samples of a jittered frame / the
+        # frames of the weak step; batched fresh frames stay raw slabs
+        accs = [torch.zeros((rows, W, 3), dtype=torch.float32, device="cuda") if (a.spp > 1 or a.weak) else None
+                for _ in rs]
         per = []
         for k in range(world):
             fd = mirt.frame_desc(W, H, a.depth, True, 1, 0, False, 1, 8, k, world, frames, a.spp > 1)

@@ -860,3 +860,40 @@ def test_phantom_grazing_rays(gpu, mirt, oracle):
     assert dfs.tobytes() == want.tobytes()
     assert fast.tobytes() == want.tobytes()
     assert int(want["hit"].sum()) > len(ray) // 4
+
+
+@pytest.mark.parametrize("batch", [1, 4])
+def test_bench_launch_plan_displays(gpu, mirt, batch):
+    """bench.py's timed loop: successive frames of the still-camera display
+    loop, `batch` per launch, launches rotating over four ctxs that share one
+    accumulation buffer (ShardedFrame(share_accum=True)): the display of
+    every frame (its own slab) equals frame k of successive blocking
+    accumulate calls on one ctx."""
+    from importlib import import_module
+    import torch
+    shard = import_module("cs201_sah-bvh_ray_tracer_amd.shard")
+    s, b = _scene(mirt, "render", 10000)
+    W, H, F = 320, 180, 12
+    rs = [mirt.Renderer(0) for _ in range(4)]
+    try:
+        for x in rs:
+            x.upload(s, b)
+            x.set_option(mirt.abi.OPT_BOUNCE_BLOCKS, 384)
+        cam = mirt.default_camera()
+        sf = shard.ShardedFrame(rs[0], W, H, 8, samples=batch, renderers=rs, share_accum=True)
+        shown = []
+        for f0 in range(0, F, batch):
+            sf.render_local(cam, sf.desc(depth=5, seed=1, sample=f0, accumulate=f0 > 0, frames=f0 + 1,
+                                         samples=batch))
+            with torch.cuda.stream(sf.stream):
+                shown.append(sf.gather(every=1).clone())
+        torch.cuda.synchronize()
+        got = [shard.as_rgba(fr).cpu().numpy() for g in shown for fr in g]
+        assert len(got) == F
+        gpu.upload(s, b)
+        for k in range(F):
+            seq = gpu.render_frame(cam, W, H, depth=5, seed=1, sample=k, accumulate=k > 0, frames=k + 1)
+            assert (got[k] == seq).all(), k
+    finally:
+        for x in rs:
+            x.close()

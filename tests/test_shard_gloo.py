@@ -22,7 +22,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, result_path):
+def _worker(rank, world, port, result_path, frames=1):
     sys.path.insert(0, ROOT)
     import importlib
 
@@ -41,22 +41,28 @@ def _worker(rank, world, port, result_path):
     cam = mirt.default_camera()
     fd = mirt.frame_desc(W, H, depth=5, seed=2, row_block=RB, shard=rank, num_shards=world)
     rows = mirt.shard_rows(fd)
-    part = o.render(cam, W, H, s, t, depth=5, mode=1, seed=2, rows=rows, threads=1)
-    slab = np.zeros((shard.slab_rows(H, RB, world), W, 4), np.uint8)
-    slab[:len(rows)] = part
-    frame = shard.gather_frame(torch.from_numpy(slab.view(np.int32).reshape(-1, W)), H, RB)
+    slab = np.zeros((frames, shard.slab_rows(H, RB, world), W, 4), np.uint8)
+    for j in range(frames):
+        slab[j, :len(rows)] = o.render(cam, W, H, s, t, depth=5, mode=1, seed=2, sample=j, rows=rows, threads=1)
+    st = torch.from_numpy(slab.view(np.int32).reshape(frames, -1, W))
+    # one frame: a (rows, W) slab; several (bench.py's multi-frame launches): (frames, rows, W)
+    frame = shard.gather_frame(st[0] if frames == 1 else st, H, RB)
     if rank == 0:
-        full = o.render(cam, W, H, s, t, depth=5, mode=1, seed=2, threads=1)
-        got = shard.as_rgba(frame).numpy()
-        np.save(result_path, np.array([int((got == full).all()), int(got.shape == full.shape)]))
+        ok = shape = 1
+        for j in range(frames):
+            full = o.render(cam, W, H, s, t, depth=5, mode=1, seed=2, sample=j, threads=1)
+            got = shard.as_rgba(frame if frames == 1 else frame[j]).numpy()
+            ok &= int((got == full).all())
+            shape &= int(got.shape == full.shape)
+        np.save(result_path, np.array([ok, shape]))
     o.free(t)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_gather_matches_single_frame(tmp_path, world):
+@pytest.mark.parametrize("world,frames", [(2, 1), (3, 1), (2, 3)])
+def test_gloo_gather_matches_single_frame(tmp_path, world, frames):
     res = str(tmp_path / "res.npy")
-    mp.spawn(_worker, args=(world, _free_port(), res), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), res, frames), nprocs=world, join=True)
     ok = np.load(res)
     assert ok.tolist() == [1, 1]
