@@ -94,6 +94,11 @@ NODE_B, SPHERE_B, COLOR_B, PIXEL_B = 32, 16, 4, 4
 # N = 2: 4,634 / 4,517 / 4,372, N = 4: 7,286 / 7,393 / 7,966, N = 8:
 # 9,460 / 11,243 / 13,735 Mrays/s before the gather
 DEFAULT_BATCH = {1: 1, 2: 1, 4: 4, 8: 4}
+# at N > 1: contexts in flight per rank and the hardware queues that gives
+# them (emulated at N = 8, K = 20, 4 frames per launch: 4 ctxs / 4 queues with
+# a gather-sized copy on a fifth stream 11.9 Grays/s, 8 queues 13.2; 8 ctxs on
+# 8 queues without the copy 15.2; profiles/r03f/)
+PIPELINE_MULTI, HW_QUEUES_MULTI = 8, 16
 KERNEL = "bounce_kernel<true, 2, false>"   # dominant kernel of the default (wavefront, four-wide) schedule
 # the PMC-derived bound of the timed launch shape, per workload
 # (scripts/pmc_bench.sh over this script's own command + scripts/pmc_summary.py)
@@ -369,8 +374,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-host", action="store_true", help="skip the host-inclusive (D2H) leg")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="1080p_10k")
-    ap.add_argument("--pipeline", type=int, default=4,
-                    help="device contexts alternating successive steps on their own streams (1 = serial)")
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="device contexts alternating successive launches on their own streams (1 = serial; "
+                         "0 = 4 at N = 1, 8 at N > 1)")
     ap.add_argument("--bounce-blocks", type=int, default=-1,
                     help="persistent bounce workgroups per launch (MIRT_OPT_BOUNCE_BLOCKS) in the timed loop; "
                          "-1 = 1.5 per CU with frames in flight (--pipeline > 1), else 0 (occupancy x CUs)")
@@ -400,6 +406,14 @@ def main():
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if args.dry:
         return dry_main(args, world, rank)
+    if not args.pipeline:
+        args.pipeline = 4 if world == 1 else PIPELINE_MULTI
+    if world > 1:
+        # one hardware queue per context stream plus RCCL's (HIP's default is 4
+        # per process; read when the runtime starts, i.e. before the first GPU
+        # call below): the one-frame split emulated per shard with a slab copy
+        # on a fifth stream, profiles/r03f/, r03g/
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", str(HW_QUEUES_MULTI))
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))

@@ -325,6 +325,12 @@ template <bool FAST, bool ORD>
 #ifndef MIRT_PRIMARY_WAVES
 #define MIRT_PRIMARY_WAVES 8
 #endif
+// A/B (round 3): group each primary workgroup's first bounces by direction
+// octant in the queue (scripts/tree_quality.cpp's lockstep model: distinct
+// nodes per lane-step -9%, busy lanes per step +13%)
+#ifndef MIRT_PRIMARY_GROUP
+#define MIRT_PRIMARY_GROUP 1
+#endif
 #define MIRT_PRIMARY_ATTR __attribute__((amdgpu_waves_per_eu(ORD ? MIRT_PRIMARY_WAVES : 1)))
 __global__ __launch_bounds__(256) MIRT_PRIMARY_ATTR void primary_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
                                                       float* __restrict__ acc, Deferred dfr,
@@ -334,6 +340,16 @@ __global__ __launch_bounds__(256) MIRT_PRIMARY_ATTR void primary_kernel(DevScene
     Counters cnt{0, 0, 0, 0, 0};
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
+#if MIRT_PRIMARY_GROUP
+    // the workgroup's first bounces, grouped by direction octant before they
+    // enter the queue (the last of the four waves to finish writes them)
+    __shared__ BounceRec grec[ORD ? 256 : 1];
+    __shared__ uint32_t gcount[4], gdone;
+    if (ORD) {
+        if (threadIdx.x == 0) gdone = 0;
+        __syncthreads();
+    }
+#endif
     if (!ORD && (int)blockIdx.x < dfr.blocks) {  // zero-component camera rays: whole path in this wave
         const uint32_t n = __builtin_amdgcn_readfirstlane(*dfr.count);
         const uint32_t stride = (uint32_t)(dfr.blocks * 4);
@@ -394,6 +410,49 @@ __global__ __launch_bounds__(256) MIRT_PRIMARY_ATTR void primary_kernel(DevScene
         }
     }
     const uint64_t pm = __ballot(push);
+#if MIRT_PRIMARY_GROUP
+    if constexpr (ORD) {
+        if (push) grec[wave * 64 + lanes_below(pm)] = rec;
+        if (lane == 0) gcount[wave] = (uint32_t)__popcll(pm);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        uint32_t prev = 0;
+        if (lane == 0) prev = __hip_atomic_fetch_add(&gdone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (__builtin_amdgcn_readfirstlane(prev) != (blockDim.x >> 6) - 1) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        // the last wave: octant of each record's direction, counts per
+        // (wave, octant), then every record to base + its octant's offset
+        const int nw = blockDim.x >> 6;
+        uint32_t oct[4], tot[8] = {0, 0, 0, 0, 0, 0, 0, 0}, total = 0;
+        bool has[4];
+        for (int w = 0; w < nw; w++) {
+            const uint32_t n = gcount[w];
+            has[w] = (uint32_t)lane < n;
+            const BounceRec& r = grec[w * 64 + (has[w] ? lane : 0)];
+            oct[w] = (r.dx < 0.0f ? 1u : 0u) | (r.dy < 0.0f ? 2u : 0u) | (r.dz < 0.0f ? 4u : 0u);
+            for (uint32_t o = 0; o < 8; o++) tot[o] += (uint32_t)__popcll(__ballot(has[w] && oct[w] == o));
+            total += n;
+        }
+        if (!total) return;
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&qctl[0], total);
+        base = __builtin_amdgcn_readfirstlane(base);
+        uint32_t run[8];
+        for (uint32_t o = 0, acc = 0; o < 8; o++) {
+            run[o] = base + acc;
+            acc += tot[o];
+        }
+        for (int w = 0; w < nw; w++) {
+            uint32_t pos = 0;
+            for (uint32_t o = 0; o < 8; o++) {
+                const uint64_t m = __ballot(has[w] && oct[w] == o);
+                if (has[w] && oct[w] == o) pos = run[o] + lanes_below(m);
+                run[o] += (uint32_t)__popcll(m);
+            }
+            if (has[w]) queue[pos] = grec[w * 64 + lane];
+        }
+        return;
+    }
+#endif
     if (pm) {  // one atomic per wave; records stay in tile order
         const int leader = __builtin_ctzll(pm);
         uint32_t base = 0;

@@ -48,6 +48,7 @@ class Oracle:
             "o_build": (P, [P, I, I, I]), "o_free": (None, [P]),
             "o_node_count": (I, [P]), "o_flatten": (I, [P, P, I]),
             "o_intersect": (None, [P, P, I, P, I, I, P]),
+            "o_intersect_flat": (None, [P, I, P, I, P, I, P]),
             "o_sphere_pairs": (None, [P, P, I, P]), "o_aabb_pairs": (None, [P, P, I, P]),
             "o_camera_ray_px": (None, [P, I, I, I, I, P]),
             "o_render_rows": (None, [P, I, I, P, I, P, I, I, I, C.c_uint64, C.c_uint32, P, I, P, I, P, I]),
@@ -92,6 +93,13 @@ class Oracle:
     def intersect(self, tree, spheres, rays, use_bvh=True):
         out = np.zeros(len(rays), abi.HIT)
         self.L.o_intersect(tree, _p(spheres), len(spheres), _p(rays), len(rays), int(use_bvh), _p(out))
+        return out
+
+    def intersect_flat(self, nodes, spheres, rays):
+        """hit.c:91-109 over a flat tree (abi.NODE array)."""
+        out = np.zeros(len(rays), abi.HIT)
+        nodes = np.ascontiguousarray(nodes, abi.NODE)
+        self.L.o_intersect_flat(_p(nodes), len(nodes), _p(spheres), len(spheres), _p(rays), len(rays), _p(out))
         return out
 
     def sphere_pairs(self, rays, spheres):

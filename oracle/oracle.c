@@ -356,6 +356,30 @@ static OHit o_bvh_hit(const mirt_ray *r, const ONode *nd, const mirt_sphere *s, 
     return L.t < R.t ? L : R;
 }
 
+/* hit.c:91-109 over a FLAT pre-order tree (include/mirt.h mirt_node: left
+   child i + 1, right child = the left subtree's skip): the same recursion,
+   for trees too large for this file's own build (the 10M / 100M benchmark
+   sweep points, whose trees are pinned by their SHA tests) */
+static OHit o_flat_hit(const mirt_ray *r, const mirt_node *nd, uint32_t i, const mirt_sphere *s, int ns)
+{
+    OHit none;
+    memset(&none, 0, sizeof none);
+    none.sphere = -1;
+    mirt_aabb box;
+    memcpy(&box.min, nd[i].bmin, sizeof box.min);
+    memcpy(&box.max, nd[i].bmax, sizeof box.max);
+    if (!o_slab(r, &box)) return none;
+    if (nd[i].sphere >= 0) {
+        if (nd[i].sphere >= ns) return none;
+        return o_sphere_hit(r, &s[nd[i].sphere], nd[i].sphere);
+    }
+    OHit L = o_flat_hit(r, nd, i + 1, s, ns);
+    OHit R = o_flat_hit(r, nd, nd[i + 1].skip & MIRT_SKIP_MASK, s, ns);
+    if (!L.hit) return R;
+    if (!R.hit) return L;
+    return L.t < R.t ? L : R;
+}
+
 /* renderer.c:36-43: brute force, first sphere wins ties */
 static OHit o_brute_hit(const mirt_ray *r, const mirt_sphere *s, int ns)
 {
@@ -386,6 +410,21 @@ void o_intersect(void *root, const mirt_sphere *s, int ns, const mirt_ray *rays,
     for (int i = 0; i < n; i++) {
         OHit h = use_bvh ? o_bvh_hit(&rays[i], (const ONode *)root, s, ns, NULL) : o_brute_hit(&rays[i], s, ns);
         if (!use_bvh && !h.hit) h.t = 0.0f; /* report like a fresh HitRecord */
+        o_store_hit(&h, &out[i]);
+    }
+}
+
+void o_intersect_flat(const mirt_node *nodes, int nn, const mirt_sphere *s, int ns, const mirt_ray *rays, int n,
+                      mirt_hit *out)
+{
+    for (int i = 0; i < n; i++) {
+        OHit h;
+        if (nn > 0) {
+            h = o_flat_hit(&rays[i], nodes, 0, s, ns);
+        } else {
+            memset(&h, 0, sizeof h);
+            h.sphere = -1;
+        }
         o_store_hit(&h, &out[i]);
     }
 }

@@ -159,3 +159,23 @@ def test_accumulate_restatement(oracle):
     acc0 = np.zeros(500 * 3, np.float32)
     half = oracle.accumulate(c, acc0, False, 2)   # main.c first frame: camera.move == 0 -> frames = 2
     assert (np.abs(half[:, :3].astype(int) - c[:, :3] // 2) <= 1).all()
+
+
+def test_oracle_flat_dfs_equals_pointer_dfs(mirt, oracle, small):
+    """o_intersect_flat (hit.c:91-109 over a flat tree, used for the 10M /
+    100M benchmark-mode points) equals o_intersect on the oracle's own
+    pointer tree, on the render and the benchmark.c:317-style build."""
+    for kind, start_end_depth in (("render", (0, None, 0)), ("bench", (0, 999, 20))):
+        pre = small[f"{kind}_1000_1_pre"]
+        so = pre.copy()
+        st, en, d = start_end_depth
+        t = oracle.build(so, st, en, d)
+        s = pre.copy()
+        flat = mirt.build_bvh(s, st, en, d)
+        rays = small["hits_rays"] if kind == "render" else small["hits_bench_rays"]
+        ns = len(s) if en is None else en
+        want = oracle.intersect(t, so[:ns], rays)
+        oracle.free(t)
+        got = oracle.intersect_flat(flat.nodes, s[:ns], rays)
+        assert got.tobytes() == want.tobytes(), kind
+        assert int(want["hit"].sum()) > (50 if kind == "render" else 0), kind
