@@ -496,6 +496,93 @@ void coherence_study(const Tree& A, const std::vector<Leaf>& leaves, const mirt_
     score("random order", sh);
 }
 
+// Screen-space binning of the camera rays (all share the camera origin):
+// per 8x8 tile, the live leaves whose sphere's projected disc (conservative
+// bounding square, +2 px) overlaps the tile, sorted by the sphere's nearest
+// distance; walk them front to back until every lane's best hit is nearer
+// than the next candidate. Reports candidates walked per tile (each a
+// wave-uniform step: one sphere test per lane) and pairs binned.
+void binning_study(const std::vector<Leaf>& leaves, const mirt_sphere* sp, const mirt_camera& cam, int Wd, int Hd)
+{
+    const float aspect = (float)Wd / Hd;
+    const float fov = (float)((double)cam.fov * (M_PI / 180.0));
+    const float hh = (float)std::tan((double)(fov / 2.0f)), hw = aspect * hh;
+    const int tx = (Wd + 7) / 8, ty = (Hd + 7) / 8;
+    std::vector<std::vector<std::pair<float, int>>> bins((size_t)tx * ty);
+    const float* o = &cam.position.x;
+    const float* F = &cam.forward.x;
+    const float* R = &cam.right.x;
+    const float* U = &cam.up.x;
+    long pairs = 0, full = 0;
+    for (int li = 0; li < (int)leaves.size(); li++) {
+        const mirt_sphere& s = sp[leaves[li].sphere];
+        const float c[3] = {s.center.x - o[0], s.center.y - o[1], s.center.z - o[2]};
+        const float r = std::fabs(s.radius);
+        const float z = c[0] * F[0] + c[1] * F[1] + c[2] * F[2];
+        const float x = c[0] * R[0] + c[1] * R[1] + c[2] * R[2];
+        const float y = c[0] * U[0] + c[1] * U[1] + c[2] * U[2];
+        const float dist = std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+        int x0 = 0, x1 = tx - 1, y0 = 0, y1 = ty - 1;
+        if (z - r > 1e-3f) {  // wholly in front: bound the disc by its tangent cone
+            const float sa = r / std::sqrt(std::max(z * z - r * r, 1e-12f));  // tan of the half-angle, ~
+            // screen coords: u = x / (z * 2hw) + 0.5 (in W units), v = -y / (z * 2hh) + 0.5
+            const float ux = x / z, uy = y / z;
+            const float ext = sa * (1.0f + std::fabs(ux) + std::fabs(uy)) * 1.5f;  // generous
+            const float px0 = ((ux - ext) / (2 * hw) + 0.5f) * Wd - 2, px1 = ((ux + ext) / (2 * hw) + 0.5f) * Wd + 2;
+            const float py0 = (-(uy + ext) / (2 * hh) + 0.5f) * Hd - 2, py1 = (-(uy - ext) / (2 * hh) + 0.5f) * Hd + 2;
+            x0 = std::max(0, (int)std::floor(px0) / 8);
+            x1 = std::min(tx - 1, (int)std::floor(px1) / 8);
+            y0 = std::max(0, (int)std::floor(py0) / 8);
+            y1 = std::min(ty - 1, (int)std::floor(py1) / 8);
+            if (px1 < 0 || py1 < 0 || px0 >= Wd || py0 >= Hd) continue;
+        } else if (z + r < 0) {
+            continue;  // wholly behind
+        } else {
+            full++;
+        }
+        for (int b = y0; b <= y1; b++)
+            for (int a = x0; a <= x1; a++) {
+                bins[(size_t)b * tx + a].push_back({dist - r, li});
+                pairs++;
+            }
+    }
+    double walked = 0, tiles = 0, listed = 0;
+    Stats dummy;
+    for (int b = 0; b < ty; b++)
+        for (int a = 0; a < tx; a++) {
+            auto& L = bins[(size_t)b * tx + a];
+            std::sort(L.begin(), L.end());
+            listed += L.size();
+            float best[64];
+            bool any = false;
+            for (int l = 0; l < 64; l++) best[l] = INFINITY;
+            size_t k = 0;
+            for (; k < L.size(); k++) {
+                bool need = false;
+                for (int l = 0; l < 64; l++)
+                    if (best[l] >= L[k].first) need = true;
+                if (!need) break;
+                for (int l = 0; l < 64; l++) {
+                    const int x = a * 8 + (l & 7), y = b * 8 + (l >> 3);
+                    if (x >= Wd || y >= Hd) continue;
+                    const float u = ((float)x / Wd - 0.5f) * aspect, v = -((float)y / Hd - 0.5f);
+                    float d[3];
+                    for (int q = 0; q < 3; q++) d[q] = F[q] + R[q] * (2 * hw) * u + U[q] * (2 * hh) * v;
+                    const float len = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+                    Ray ray = make_ray(o[0], o[1], o[2], d[0] / len, d[1] / len, d[2] / len);
+                    const float t = sphere_t(ray, sp[leaves[L[k].second].sphere]);
+                    if (t > 0 && t < best[l]) best[l] = t;
+                    any = true;
+                }
+            }
+            (void)any;
+            walked += k;
+            tiles++;
+        }
+    printf("binning %dx%d: %ld tile-leaf pairs (%.1f per tile, %ld leaves cover the screen), candidates walked per "
+           "tile %.2f\n", Wd, Hd, pairs, listed / tiles, full, walked / tiles);
+}
+
 int main(int argc, char** argv)
 {
     const int n = argc > 1 ? atoi(argv[1]) : 10000;
@@ -526,6 +613,12 @@ int main(int argc, char** argv)
     Tree A;  // the root's HNode is the four-slot cut of flat node 0
     A.root_box = nbox(0);
     A.root_ref = build_a(A, 0);
+    if (argc > 6 && std::string(argv[6]) == "binning") {
+        mirt_camera cam;
+        mirt_camera_default(&cam);
+        binning_study(leaves, sp.data(), cam, argc > 7 ? atoi(argv[7]) : 1920, argc > 8 ? atoi(argv[8]) : 1080);
+        return 0;
+    }
     if (argc > 6 && std::string(argv[6]) == "coherence") {
         mirt_camera cam;
         mirt_camera_default(&cam);
