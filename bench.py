@@ -414,9 +414,18 @@ def main():
         # call below): the one-frame split emulated per shard with a slab copy
         # on a fifth stream, profiles/r03f/, r03g/
         os.environ.setdefault("GPU_MAX_HW_QUEUES", str(HW_QUEUES_MULTI))
+    # MIRT_BENCH_SHARE_GPU=1: a rehearsal of the N > 1 path on a one-GPU box --
+    # every rank on device 0 and gloo in place of RCCL (which refuses two ranks
+    # on one device); the same launches, shard geometry, gathers (staged
+    # through host memory) and max-over-ranks timing. Not a measurement.
+    rehearse = world > 1 and os.environ.get("MIRT_BENCH_SHARE_GPU") == "1"
+    dev = (0 if rehearse else local) if world > 1 else 0
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
 
@@ -425,7 +434,6 @@ def main():
     t0 = time.perf_counter()
     bvh = mirt.build_bvh(spheres)
     build_s = time.perf_counter() - t0
-    dev = local if world > 1 else 0
     rs = [mirt.Renderer(dev) for _ in range(max(1, args.pipeline))]
     # bounce workgroups per launch with frames in flight (measured: 1080p/10k
     # 2,400 -> 2,650 Mrays/s at 4 contexts, profiles/r02_ab/r02au_*); the
@@ -594,7 +602,8 @@ def main():
             "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (create_random_sphere scene, srand(1); default camera main.c:203-211)",
+            "data": "synthetic (create_random_sphere scene, srand(1); default camera main.c:203-211)"
+                    + ("; REHEARSAL: all ranks on one GPU over gloo, not a measurement" if rehearse else ""),
             "config": {"workload": wl["desc"], "name": args.workload,
                        "width": W, "height": H, "spheres": NSPH, "scene": KIND, "max_depth": DEPTH, "spp": SPP,
                        "jitter": JITTER,

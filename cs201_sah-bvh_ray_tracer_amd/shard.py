@@ -64,10 +64,16 @@ def gather_frame(slab, height, row_block, group=None, dst=0):
     if world == 1:
         bufs = [slab]
     else:
-        bufs = [torch.empty_like(slab) for _ in range(world)] if rank == dst else None
-        dist.gather(slab.contiguous(), bufs, dst=dst, group=group)
+        # gloo gathers host tensors (a rehearsal / CPU run): stage device slabs
+        # through host memory; RCCL gathers device memory directly
+        staged = slab.is_cuda and dist.get_backend(group) == "gloo"
+        src = slab.contiguous().cpu() if staged else slab.contiguous()
+        bufs = [torch.empty_like(src) for _ in range(world)] if rank == dst else None
+        dist.gather(src, bufs, dst=dst, group=group)
         if rank != dst:
             return None
+        if staged:
+            bufs = [b.to(slab.device) for b in bufs]
     st = torch.stack(bufs)
     if slab.dim() == 2:
         return assemble(st, height, row_block)

@@ -273,7 +273,9 @@ int mirt_accum_download(mirt_ctx *ctx, float *out, size_t count);
    folds run in call order across the ctxs' streams (events), the tracing
    still overlaps. Without it every ctx accumulates only its own frames, so a
    rotation of n ctxs would average 1/n of the frames. Both ctxs must be on
-   the same device; waits for ctx's enqueued frames first. */
+   the same device; waits for ctx's enqueued frames first. Ctxs that share a
+   buffer must be driven from ONE host thread (the call order is the fold
+   order). */
 int mirt_ctx_share_accum(mirt_ctx *ctx, mirt_ctx *owner);
 
 /* trace_ray (renderer.c:21-77) on n arbitrary rays; ray i uses RNG contract

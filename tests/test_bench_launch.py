@@ -36,3 +36,19 @@ def test_failing_rank_fails_the_launch():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry",
                         "--workload", "no-such-workload"], capture_output=True, text=True, timeout=120, env=env)
     assert p.returncode != 0
+
+
+@pytest.mark.gpu
+def test_multi_rank_bench_rehearsal_on_one_gpu():
+    """The N > 1 bench path on a one-GPU box (MIRT_BENCH_SHARE_GPU=1: both
+    ranks on device 0, gloo in place of RCCL): the strong split with frames
+    in flight, every frame's slabs gathered to rank 0, max-over-ranks timing
+    -- runs to its JSON line (a rehearsal, no measurement)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["MIRT_BENCH_SHARE_GPU"] = "1"
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "8", "--warmup",
+                        "2", "--no-cpu", "--no-host"], capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["value"] > 0
+    assert "REHEARSAL" in d["data"] and d["value_weak"] > 0 and d["value_strong"] == d["value"]
