@@ -22,6 +22,7 @@
 #include <cstring>
 #include <random>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "mirt.h"
@@ -50,11 +51,47 @@ struct Leaf {
 };
 
 // four-wide node: slot >= 0 inner node, slot < 0 leaf ~slot, INT32_MIN none
+constexpr int kMaxWide = 8;
+int g_quant = 0;  // argv[10]: 1 = 8-bit slot boxes in the node's frame (fp32 origin), 2 = fp16 origin
+int g_wide = 4;  // slots per node of tree A (argv[9]: 4 as the library, 8 to price an eight-wide layout)
 struct W4 {
-    Box box[4];
-    int ref[4];
+    Box box[kMaxWide];
+    int ref[kMaxWide];
+    int pos[kMaxWide];  // octant position of each slot (g_order 1)
     int n = 0;
 };
+int g_order = 0;  // argv[11]: 0 = passing slots sorted by entry; 1 = fixed octant order (no sort)
+int g_popcheck = 1;  // argv[12]: 1 = a popped entry beyond best is dropped unvisited; 0 = visited (the kernel)
+
+// Slots to octant positions 0..7 (bit a set: the slot's centre lies on the
+// + side of the node's centre on axis a), greedily by how far each slot lies
+// along each position's diagonal; a ray then takes its passing slots in the
+// order p ^ s (s: the sign bits of its direction), near side first.
+void assign_positions(W4& w)
+{
+    Box all;
+    for (int k = 0; k < w.n; k++) all.grow(w.box[k]);
+    float cen[3];
+    for (int a = 0; a < 3; a++) cen[a] = 0.5f * (all.lo[a] + all.hi[a]);
+    std::vector<std::tuple<float, int, int>> cand;
+    for (int k = 0; k < w.n; k++) {
+        float c[3];
+        for (int a = 0; a < 3; a++)
+            c[a] = (w.box[k].lo[a] <= w.box[k].hi[a]) ? 0.5f * (w.box[k].lo[a] + w.box[k].hi[a]) - cen[a] : 0.0f;
+        for (int p = 0; p < 8; p++) {
+            float d = 0;
+            for (int a = 0; a < 3; a++) d += ((p >> a) & 1) ? c[a] : -c[a];
+            cand.emplace_back(-d, k, p);
+        }
+    }
+    std::sort(cand.begin(), cand.end());
+    bool used_k[kMaxWide] = {}, used_p[8] = {};
+    for (auto& [cost, k, p] : cand) {
+        if (used_k[k] || used_p[p]) continue;
+        used_k[k] = used_p[p] = true;
+        w.pos[k] = p;
+    }
+}
 
 struct Tree {
     std::vector<W4> nodes;
@@ -89,7 +126,7 @@ Box nbox(uint32_t i)
 
 int build_a(Tree& t, uint32_t y)  // HNode of inner node y (its greedy four-slot cut)
 {
-    uint32_t cut[4];
+    uint32_t cut[kMaxWide + 1];
     int m = 0;
     auto add = [&](uint32_t c) {
         const uint32_t ci = live(c);
@@ -97,7 +134,7 @@ int build_a(Tree& t, uint32_t y)  // HNode of inner node y (its greedy four-slot
     };
     add(y + 1);
     add(g_nd[y + 1].skip & MIRT_SKIP_MASK);
-    while (m < 4) {
+    while (m < g_wide) {
         int best = -1;
         float ba = -1;
         for (int j = 0; j < m; j++) {
@@ -116,9 +153,34 @@ int build_a(Tree& t, uint32_t y)  // HNode of inner node y (its greedy four-slot
     }
     const int me = (int)t.nodes.size();
     t.nodes.emplace_back();
+    // g_quant: slot boxes stored as 8-bit codes in the node's own frame
+    // (origin = the slots' min corner, per axis a power-of-two step >=
+    // extent / 255), rounded outward: the looseness a 64-B eight-wide node costs
+    Box frame;
+    for (int k = 0; k < m; k++) frame.grow(nbox(cut[k]));
+    double step[3];
+    if (g_quant == 2)  // origin stored in fp16, rounded down (the 64-B eight-wide unit's header)
+        for (int a = 0; a < 3; a++) {
+            int e;
+            std::frexp(frame.lo[a], &e);
+            const double ulp = std::ldexp(1.0, std::max(e - 11, -24));
+            frame.lo[a] = (float)(std::floor((double)frame.lo[a] / ulp) * ulp);
+        }
+    for (int a = 0; a < 3; a++) {
+        const double ext = (double)frame.hi[a] - frame.lo[a];
+        step[a] = ext > 0 ? std::ldexp(1.0, (int)std::ceil(std::log2(ext / 255.0))) : 1.0;
+    }
     for (int k = 0; k < m; k++) {
         const uint32_t c = cut[k];
         Box b = nbox(c);
+        if (g_quant)
+            for (int a = 0; a < 3; a++) {
+                if (!(b.lo[a] <= b.hi[a])) continue;  // an inverted (empty) box stays as is
+                const double ql = std::floor(((double)b.lo[a] - frame.lo[a]) / step[a]);
+                const double qh = std::ceil(((double)b.hi[a] - frame.lo[a]) / step[a]);
+                b.lo[a] = std::nextafter((float)(frame.lo[a] + ql * step[a]), -INFINITY);
+                b.hi[a] = std::nextafter((float)(frame.lo[a] + qh * step[a]), INFINITY);
+            }
         int ref;
         if (g_nd[c].sphere >= 0)
             ref = ~g_leaf_of[c];
@@ -128,6 +190,7 @@ int build_a(Tree& t, uint32_t y)  // HNode of inner node y (its greedy four-slot
         t.nodes[me].ref[k] = ref;
     }
     t.nodes[me].n = m;
+    assign_positions(t.nodes[me]);
     return me;
 }
 
@@ -317,11 +380,11 @@ int walk(const Tree& t, const std::vector<Leaf>& L, const mirt_sphere* sp, const
         const float en = sentry.back();
         stack.pop_back();
         sentry.pop_back();
-        if (en > best) continue;
+        if (g_popcheck && en > best) continue;
         st.visits++;
         if (trace) trace->push_back(n);
         const W4& w = t.nodes[n];
-        std::pair<float, int> in[4];
+        std::pair<float, int> in[kMaxWide];
         int m = 0;
         for (int k = 0; k < w.n; k++) {
             float ek;
@@ -335,14 +398,16 @@ int walk(const Tree& t, const std::vector<Leaf>& L, const mirt_sphere* sp, const
                     bs = L[li].sphere;
                 }
             } else {
-                in[m++] = {ek, w.ref[k]};
+                in[m++] = {g_order ? (float)(w.pos[k] ^ ((r.d[0] < 0) | (r.d[1] < 0) << 1 | (r.d[2] < 0) << 2))
+                                   : ek,
+                           w.ref[k]};
             }
         }
         std::sort(in, in + m, [](auto& a, auto& b) { return a.first > b.first; });  // far first: near on top
         for (int k = 0; k < m; k++) {
-            if (in[k].first > best) continue;
+            if (!g_order && in[k].first > best) continue;
             stack.push_back(in[k].second);
-            sentry.push_back(in[k].first);
+            sentry.push_back(g_order ? -INFINITY : in[k].first);
             st.pushes++;
         }
         st.max_stack = std::max(st.max_stack, (int)stack.size());
@@ -590,6 +655,10 @@ int main(int argc, char** argv)
     const int stride = argc > 3 ? atoi(argv[3]) : 4;
     g_bins = argc > 4 ? atoi(argv[4]) : 16;
     g_leaf_max = argc > 5 ? atoi(argv[5]) : 1;
+    g_wide = argc > 9 ? atoi(argv[9]) : 4;
+    g_quant = argc > 10 ? atoi(argv[10]) : 0;
+    g_order = argc > 11 ? atoi(argv[11]) : 0;
+    g_popcheck = argc > 12 ? atoi(argv[12]) : 1;
     mirt_rand_state st;
     mirt_srand(&st, 1);
     std::vector<mirt_sphere> sp(n);
