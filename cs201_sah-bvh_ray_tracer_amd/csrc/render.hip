@@ -12,7 +12,6 @@
 #include <algorithm>
 #include <cstring>
 #include <new>
-#include <tuple>
 #include <vector>
 
 #include "internal.h"
@@ -497,22 +496,6 @@ struct BounceWalk<2> {
     }
 };
 
-template <>
-struct BounceWalk<3> {  // eight-wide quantised (WUnit, LDS stack)
-    WideWalk w;
-    lds_uint4* hc = nullptr;  // the top units staged in LDS (bounce_kernel)
-    uint32_t hc_n = 0;
-    __device__ void start(const DevScene&) { w = wide_walk_start(true); }
-    __device__ void stop() { w = wide_walk_start(false); }
-    __device__ bool walking() const { return wide_walking(w); }
-    template <bool FAST>
-    __device__ void step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr, uint32_t* stk,
-                         float& bt, int& bs, Counters&)
-    {
-        wide8_lane_step<FAST>(sc, sr, sp, pr, w, stk, bt, bs, hc, hc_n);
-    }
-};
-
 // DIAG (mirt_bounce_stats): per wave {loop iterations, walking lanes summed
 // over them, the same two after the queue ran dry, start / queue-dry / end
 // time (100 MHz clock), longest chain << 32 | longest walk (in steps)}.
@@ -573,20 +556,19 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
     uint64_t dg_it = 0, dg_lanes = 0, dg_it_x = 0, dg_lanes_x = 0, dg_tx = 0, dg_qit = 0, dg_tq = 0;
     const uint64_t dg_t0 = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
     uint32_t dg_steps = 0, dg_chain = 0, dg_walk_max = 0, dg_chain_max = 0;
-    constexpr bool LANE4 = WALK >= 2;  // four- or eight-wide, one ray per lane, LDS stack
-    constexpr bool QUAD = WALK == 2;   // the quad drain (four-wide only)
+    constexpr bool LANE4 = WALK == 2;  // four-wide, one ray per lane
     constexpr int cstride = 256;
     __shared__ uint32_t cstack[kMaxDepth * cstride];
     __shared__ uint32_t wstack[LANE4 ? kWideStack * kWideStride : 1];
-    __shared__ uint32_t qsrc[QUAD ? 4 * 16 : 1];  // quad drain: source lane of each quad, per wave
+    __shared__ uint32_t qsrc[LANE4 ? 4 * 16 : 1];  // quad drain: source lane of each quad, per wave
     // the tree's top levels (the first kHCache HNodes, breadth-first) in LDS:
     // every bounce walk starts there, so those steps skip the vector-memory
     // path (TD, the kernel's busiest unit)
     __shared__ uint4 hcache[LANE4 ? 4 * kHCache : 1];
     uint32_t hc_n = 0;
     if constexpr (LANE4) {
-        hc_n = min((uint32_t)kHCache, WALK == 3 ? sc.num_wunits : sc.num_hnodes);
-        const uint4* src = WALK == 3 ? (const uint4*)sc.wunits : (const uint4*)sc.hnodes;
+        hc_n = min((uint32_t)kHCache, sc.num_hnodes);
+        const uint4* src = (const uint4*)sc.hnodes;
         for (uint32_t i = threadIdx.x; i < 4 * hc_n; i += blockDim.x) hcache[i] = src[i];
         __syncthreads();
     }
@@ -642,7 +624,7 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
         }
         if (!__ballot(has)) break;
         if (DIAG && exhausted && !dg_tx) dg_tx = __builtin_amdgcn_s_memrealtime();
-        if (QUAD && quad_drain && exhausted && __popcll(__ballot(has)) <= 16) break;  // -> quad drain
+        if (LANE4 && quad_drain && exhausted && __popcll(__ballot(has)) <= 16) break;  // -> quad drain
         // walk until few lanes are still walking and the others can make progress
         for (;;) {
             const uint64_t walking = __ballot(has && w.walking());
@@ -684,7 +666,7 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
             }
         }
     }
-    if constexpr (QUAD) {
+    if constexpr (LANE4) {
         // quad drain (uniform control flow here: every lane is active)
         const uint64_t busy = __ballot(has);
         if (busy) {
@@ -1124,9 +1106,6 @@ struct mirt_ctx {
     HAux* d_haux = nullptr;
     LeafRec* d_leaves = nullptr;
     uint32_t num_hnodes = 0;
-    WUnit* d_wunits = nullptr;  // eight-wide bounce layout (null: the tree did not quantise)
-    HAux* d_waux = nullptr;
-    uint32_t num_wunits = 0;
     uint8_t* d_ndepth = nullptr;  // depth of every flat node (BVH overlay colours)
     uint32_t* d_overlay = nullptr;  // BVH overlay: per-pixel last line in draw order
     size_t overlay_cap = 0;
@@ -1135,7 +1114,6 @@ struct mirt_ctx {
     int bounce_blocks = 0;      // wavefront: persistent workgroups (set in mirt_create)
     int bounce_blocks_opt = 0;  // MIRT_OPT_BOUNCE_BLOCKS override (0: occupancy x CUs)
     int quad_drain = 1;         // four-wide bounce walk: finish the drain four lanes per ray
-    int bounce_walk = 4;        // MIRT_OPT_BOUNCE_WALK: 4 (HNode) or 8 (WUnit, when the tree quantised)
     void* d_queue = nullptr;    // wavefront: {count, head} + bounce records
     size_t queue_cap = 0;
     uint32_t* d_defer = nullptr;  // [count, list...]
@@ -1448,173 +1426,13 @@ void build_hnodes(const mirt_node* nd, int nn, const mirt_sphere* sp, int ns, st
     }
 }
 
-// Eight-wide quantised units (trace.h WUnit) of a validated flat tree: unit
-// 0 holds the first cut of the root, each inner slot's unit the cut of that
-// node -- its live children, then the inner slot with the largest box
-// replaced by its two live children while fewer than eight -- and each leaf
-// slot's unit its LeafRec. Children are allocated as consecutive blocks
-// breadth-first, so the first units are the top levels (the LDS-staged ones).
-// Returns false (no eight-wide walk) when a frame cannot be encoded: a box
-// beyond the fp16 range of the origin, an inverted or non-finite box, a step
-// beyond 2^40, or more units than 32-bit indices reach.
-bool build_wunits(const mirt_node* nd, int nn, const mirt_sphere* sp, int ns, std::vector<WUnit>& un,
-                  std::vector<HAux>& aux)
-{
-    un.assign(1, WUnit{});
-    aux.assign(1, HAux{0xffffffffu, (uint32_t)nn});
-    if (nn == 0) return true;
-    struct Todo {
-        uint32_t unit, node;  // node: the flat inner node the unit expands (kPNone: the root's cut)
-    };
-    std::vector<Todo> todo{{0u, kPNone}};
-    for (size_t next = 0; next < todo.size(); next++) {
-        const Todo td = todo[next];
-        uint32_t cut[8];
-        int m = 0;
-        auto add = [&](uint32_t c) {
-            const uint32_t ci = live_node(nd, c, ns);
-            if (ci != kPNone) cut[m++] = ci;
-        };
-        if (td.node == kPNone) {
-            add(0);
-        } else {
-            add(td.node + 1);
-            add(nd[td.node + 1].skip & MIRT_SKIP_MASK);
-        }
-        while (m < 8) {
-            int best = -1;
-            float best_area = -1.0f;
-            for (int j = 0; j < m; j++) {
-                const mirt_node& n = nd[cut[j]];
-                if (n.sphere >= 0) continue;
-                const float dx = n.bmax[0] - n.bmin[0], dy = n.bmax[1] - n.bmin[1], dz = n.bmax[2] - n.bmin[2];
-                const float area = dx * dy + dy * dz + dz * dx;
-                if (area > best_area || best < 0) {
-                    best = j;
-                    best_area = area;
-                }
-            }
-            if (best < 0 || m == 8) break;
-            const uint32_t c = cut[best];
-            cut[best] = cut[--m];
-            add(c + 1);
-            add(nd[c + 1].skip & MIRT_SKIP_MASK);
-        }
-        // the frame: origin = the slots' min corner rounded down to fp16, per
-        // axis the least power-of-two step whose code 255 reaches the max
-        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-        for (int k = 0; k < m; k++)
-            for (int a = 0; a < 3; a++) {
-                const float l = nd[cut[k]].bmin[a], h = nd[cut[k]].bmax[a];
-                if (!(std::isfinite(l) && std::isfinite(h) && l <= h)) return false;
-                lo[a] = std::min(lo[a], l);
-                hi[a] = std::max(hi[a], h);
-            }
-        uint16_t ob[3] = {0, 0, 0};
-        float org[3] = {0, 0, 0}, step[3] = {1, 1, 1};
-        int ex[3] = {0, 0, 0};
-        for (int a = 0; a < 3 && m > 0; a++) {
-            ob[a] = half_down(lo[a]);
-            org[a] = half_value(ob[a]);
-            if (!std::isfinite(org[a])) return false;
-            int e = -64;
-            const double need = ((double)hi[a] - org[a]) / 255.0;
-            if (need > 0) e = std::max(e, (int)std::ceil(std::log2(need)) - 1);
-            while (e <= 40 && std::fmaf(255.0f, std::ldexp(1.0f, e), org[a]) < hi[a]) e++;
-            if (e > 40) return false;
-            ex[a] = e;
-            step[a] = std::ldexp(1.0f, e);
-        }
-        // octant positions (bit a: the slot's centre on the + side of the frame's centre)
-        int pos[8];
-        {
-            std::vector<std::tuple<float, int, int>> cand;
-            for (int k = 0; k < m; k++) {
-                float c[3];
-                for (int a = 0; a < 3; a++)
-                    c[a] = 0.5f * (nd[cut[k]].bmin[a] + nd[cut[k]].bmax[a]) - 0.5f * (lo[a] + hi[a]);
-                for (int p = 0; p < 8; p++) {
-                    float d = 0.0f;
-                    for (int a = 0; a < 3; a++) d += ((p >> a) & 1) ? c[a] : -c[a];
-                    cand.emplace_back(-d, k, p);
-                }
-            }
-            std::sort(cand.begin(), cand.end());
-            bool used_k[8] = {}, used_p[8] = {};
-            for (auto& [cost, k, p] : cand) {
-                if (used_k[k] || used_p[p]) continue;
-                used_k[k] = used_p[p] = true;
-                pos[k] = p;
-            }
-        }
-        int at[8];  // slot position -> cut index
-        for (int p = 0; p < 8; p++) at[p] = -1;
-        for (int k = 0; k < m; k++) at[pos[k]] = k;
-        uint32_t valid = 0, leafm = 0;
-        for (int k = 0; k < m; k++) {
-            valid |= 1u << pos[k];
-            if (nd[cut[k]].sphere >= 0) leafm |= 1u << pos[k];
-        }
-        if (un.size() + (size_t)m >= (size_t)kPNone) return false;
-        const uint32_t base = (uint32_t)un.size();
-        WUnit& w = un[td.unit];
-        std::memset(&w, 0, sizeof w);
-        w.w[0] = (uint32_t)ob[0] | ((uint32_t)ob[1] << 16);
-        w.w[1] = (uint32_t)ob[2] | ((uint32_t)(uint8_t)(int8_t)ex[0] << 16) | ((uint32_t)(uint8_t)(int8_t)ex[1] << 24);
-        w.w[2] = (uint32_t)(uint8_t)(int8_t)ex[2] | (valid << 8) | (leafm << 16);
-        w.w[3] = base;
-        for (int p = 0; p < 8; p++) {
-            if (at[p] < 0) continue;
-            const mirt_node& n = nd[cut[at[p]]];
-            for (int a = 0; a < 3; a++) {
-                // largest code whose plane is <= lo, least whose plane is >= hi
-                uint32_t ql = (uint32_t)std::min(255.0, std::max(0.0, std::floor(((double)n.bmin[a] - org[a]) / step[a])));
-                while (ql > 0 && std::fmaf((float)ql, step[a], org[a]) > n.bmin[a]) ql--;
-                while (ql < 255 && std::fmaf((float)(ql + 1), step[a], org[a]) <= n.bmin[a]) ql++;
-                uint32_t qh = (uint32_t)std::min(255.0, std::max(0.0, std::ceil(((double)n.bmax[a] - org[a]) / step[a])));
-                while (qh < 255 && std::fmaf((float)qh, step[a], org[a]) < n.bmax[a]) qh++;
-                while (qh > 0 && std::fmaf((float)(qh - 1), step[a], org[a]) >= n.bmax[a]) qh--;
-                if (std::fmaf((float)ql, step[a], org[a]) > n.bmin[a] ||
-                    std::fmaf((float)qh, step[a], org[a]) < n.bmax[a])
-                    return false;
-                const int h = p >> 2, b = p & 3;
-                w.w[4 + 2 * a + h] |= ql << (8 * b);
-                w.w[10 + 2 * a + h] |= qh << (8 * b);
-            }
-        }
-        un.resize(un.size() + (size_t)m);
-        aux.resize(un.size(), HAux{0u, 0u});
-        for (int p = 0, r = 0; p < 8; p++) {
-            if (at[p] < 0) continue;
-            const uint32_t ci = cut[at[p]], u = base + (uint32_t)r++;
-            const mirt_node& n = nd[ci];
-            if (n.sphere >= 0) {
-                LeafRec l{};
-                std::memcpy(l.lo, n.bmin, sizeof l.lo);
-                std::memcpy(l.hi, n.bmax, sizeof l.hi);
-                l.sphere = n.sphere;
-                const mirt_sphere& s = sp[n.sphere];
-                l.geo = make_float4(s.center.x, s.center.y, s.center.z, s.radius);
-                std::memset(&un[u], 0, sizeof(WUnit));
-                std::memcpy(&un[u], &l, sizeof l);
-            } else {
-                aux[u] = HAux{ci, n.skip & MIRT_SKIP_MASK};
-                todo.push_back(Todo{u, ci});
-            }
-        }
-    }
-    return true;
-}
-
 DevScene dev_scene(const mirt_ctx* c)
 {
     const bool prune = c->prune && c->prune_ok;
     const bool ordered = prune && c->ordered && c->ordered_ok && c->fast_slab;
-    const bool w8 = ordered && c->bounce_walk == 8 && c->d_wunits;
     return DevScene{c->d_nodes, c->d_nodes32, c->d_geo, c->d_color, (uint32_t)c->num_nodes, c->num_spheres,
                     prune, c->r_max, c->c_max, c->d_pnodes, ordered, c->d_hnodes, c->d_haux, c->d_leaves, ordered,
-                    ordered ? c->num_hnodes : 0u, w8 ? c->d_wunits : nullptr, w8 ? c->d_waux : nullptr,
-                    w8 ? c->num_wunits : 0u};
+                    ordered ? c->num_hnodes : 0u};
 }
 
 AccumShare* accum_new(int device)
@@ -1784,8 +1602,6 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
             bounce_kernel<true, 2, true><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, d_bdiag);
         else if (d_bdiag)
             bounce_kernel<true, 0, true><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, d_bdiag);
-        else if (sc.wunits)
-            bounce_kernel<true, 3><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, 0);
         else if (sc.wide)
             bounce_kernel<true, 2><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain);
         else if (c->fast_slab)
@@ -1900,7 +1716,7 @@ void mirt_destroy(mirt_ctx* c)
     for (void* p : {(void*)c->d_nodes, (void*)c->d_nodes32, (void*)c->d_geo, (void*)c->d_color, (void*)c->d_out,
                     c->d_in, c->d_res, (void*)c->d_counts, (void*)c->d_defer, c->d_queue, (void*)c->d_keys, (void*)c->d_pnodes,
                     (void*)c->d_hnodes, (void*)c->d_haux, (void*)c->d_leaves, (void*)c->d_ndepth,
-                    (void*)c->d_overlay, (void*)c->d_wunits, (void*)c->d_waux})
+                    (void*)c->d_overlay})
         if (p) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -1933,12 +1749,8 @@ try {
     geo[ns] = make_float4(NAN, NAN, NAN, NAN);  // &spheres[N] sentinel: never hits
     col[ns] = 0xff000000u;
     for (void* p : {(void*)c->d_nodes, (void*)c->d_nodes32, (void*)c->d_geo, (void*)c->d_color, (void*)c->d_pnodes,
-                    (void*)c->d_hnodes, (void*)c->d_haux, (void*)c->d_leaves, (void*)c->d_ndepth,
-                    (void*)c->d_wunits, (void*)c->d_waux})
+                    (void*)c->d_hnodes, (void*)c->d_haux, (void*)c->d_leaves, (void*)c->d_ndepth})
         if (p) (void)hipFree(p);
-    c->d_wunits = nullptr;
-    c->d_waux = nullptr;
-    c->num_wunits = 0;
     c->d_ndepth = nullptr;
     c->d_pnodes = nullptr;
     c->d_hnodes = nullptr;
@@ -1983,17 +1795,6 @@ try {
     HIP_TRY(hipMemcpy(c->d_hnodes, hn.data(), sizeof(HNode) * hn.size(), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_haux, hx.data(), sizeof(HAux) * hx.size(), hipMemcpyHostToDevice));
     if (!lr.empty()) HIP_TRY(hipMemcpy(c->d_leaves, lr.data(), sizeof(LeafRec) * lr.size(), hipMemcpyHostToDevice));
-    {
-        std::vector<WUnit> wu;
-        std::vector<HAux> wx;
-        if (ordered && encloses && build_wunits(nodes, nn, spheres, ns, wu, wx)) {
-            HIP_TRY(hipMalloc((void**)&c->d_wunits, sizeof(WUnit) * wu.size()));
-            HIP_TRY(hipMalloc((void**)&c->d_waux, sizeof(HAux) * wx.size()));
-            HIP_TRY(hipMemcpy(c->d_wunits, wu.data(), sizeof(WUnit) * wu.size(), hipMemcpyHostToDevice));
-            HIP_TRY(hipMemcpy(c->d_waux, wx.data(), sizeof(HAux) * wx.size(), hipMemcpyHostToDevice));
-            c->num_wunits = (uint32_t)wu.size();
-        }
-    }
     // node depths (pre-order: the children of inner node i are i + 1 and the
     // left subtree's skip), clamped to 255 -- the overlay's colour key
     std::vector<uint8_t> ndepth((size_t)std::max(nn, 1), 0);
@@ -2544,10 +2345,6 @@ int mirt_set_option(mirt_ctx* c, int option, int value)
     case MIRT_OPT_QUAD_DRAIN:
         c->quad_drain = value != 0;
         return MIRT_OK;
-    case MIRT_OPT_BOUNCE_WALK:
-        if (value != 4 && value != 8) break;
-        c->bounce_walk = value;
-        return MIRT_OK;
     case MIRT_OPT_BLOCK_WAVES:
         if (value != 1 && value != 2 && value != 4 && value != 8) break;
         c->block_waves = value;
@@ -2571,7 +2368,6 @@ int mirt_get_option(mirt_ctx* c, int option)
     if (option == MIRT_OPT_ORDERED) return c->ordered;
     if (option == MIRT_OPT_BOUNCE_BLOCKS) return c->bounce_blocks_opt;
     if (option == MIRT_OPT_QUAD_DRAIN) return c->quad_drain;
-    if (option == MIRT_OPT_BOUNCE_WALK) return c->bounce_walk == 8 && c->d_wunits ? 8 : 4;  // the walk in effect
     set_error("mirt_get_option: bad option %d", option);
     return MIRT_E_INVALID;
 }

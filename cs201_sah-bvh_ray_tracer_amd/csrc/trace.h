@@ -118,11 +118,6 @@ struct DevScene {
     const LeafRec* leaves;
     int wide;
     uint32_t num_hnodes;  // HNodes, numbered breadth-first: the first ones are the top levels
-    // eight-wide quantised units (WUnit, below) for the bounce walk; null when
-    // the tree did not quantise (then the four-wide walk runs)
-    const struct WUnit* wunits;
-    const HAux* waux;
-    uint32_t num_wunits;
 };
 
 // LDS-resident node data (address space 3: ds_read, never a flat load)
@@ -936,11 +931,9 @@ __device__ __forceinline__ float h_hi(uint32_t v) { return (float)__builtin_bit_
 // reference's order so the box-gated sphere tests are what it counts.
 template <bool FAST, bool COUNT>
 __device__ __forceinline__ void wide_leaf(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
-                                          uint32_t ref, float& best_t, int& best_s, Counters& cnt,
-                                          const float4* rec = nullptr)
+                                          uint32_t ref, float& best_t, int& best_s, Counters& cnt)
 {
-    // the LeafRec: of the four-wide layout, or a unit of the eight-wide one
-    const float4* lp = rec ? rec : (const float4*)(sc.leaves + (ref & ~kPLeaf));
+    const float4* lp = (const float4*)(sc.leaves + (ref & ~kPLeaf));
     float e;
     if constexpr (COUNT) {
         const float4 l0 = lp[0], l1 = lp[1], g = lp[2];
@@ -1182,166 +1175,6 @@ __device__ __forceinline__ void quad_step(const DevScene& sc, const SlabRay& sr,
     w.cur = nx - 1;
 }
 
-// ------------------------------------------------------ eight-wide walk
-// The bounce walk over EIGHT-wide nodes in the same 64 B (round 3): a node's
-// slot boxes are 8-bit codes in the node's own frame, so a visit still costs
-// four dwordx4 loads but a walk makes about a third fewer of them (the
-// texture path, the bounce kernel's busiest unit, follows load instructions).
-// Unit layout (64 B; the children of a node are consecutive units from
-// `base`, in slot order, so slot k's unit is base + popcount(valid below k)):
-//   w[0]  origin.x | origin.y << 16     (fp16: the frame's corner, <= every slot's lo)
-//   w[1]  origin.z | ex << 16 | ey << 24 (int8 exponents: plane step 2^e per axis)
-//   w[2]  ez | valid << 8 | leaf << 16   (8-bit slot masks)
-//   w[3]  base
-//   w[4 + 2a], w[5 + 2a]: axis a's lo codes of slots 0-3 / 4-7 (a byte each);
-//   w[10 + 2a], w[11 + 2a]: its hi codes.
-// A slot's plane is P = fl(origin + q 2^e) (fmaf: q 2^e is exact); the
-// builder picks the codes so that these floats hold the slot's box
-// (outward), so the conservative test of §5 applies to the decoded box. A
-// leaf slot's unit is a LeafRec (exact box, sphere) padded to 64 B.
-// Slots sit at octant positions (bit a: the slot's centre lies on the +
-// side of the node's centre on axis a); a ray takes its passing inner slots
-// in the order i ^ s (s: its direction's sign bits), near side first --
-// an approximation of the four-wide walk's sort, for no sort at all.
-struct __attribute__((aligned(64))) WUnit {
-    uint32_t w[16];
-};
-static_assert(sizeof(WUnit) == 64, "eight-wide unit is 64 B");
-
-__device__ __forceinline__ float u8f(uint32_t v, int k) { return (float)((v >> (8 * k)) & 0xffu); }
-
-// bit i of the result = bit (i ^ s) of m (an 8-bit mask)
-__device__ __forceinline__ uint32_t perm8(uint32_t m, uint32_t s)
-{
-    if (s & 1u) m = ((m & 0x55u) << 1) | ((m >> 1) & 0x55u);
-    if (s & 2u) m = ((m & 0x33u) << 2) | ((m >> 2) & 0x33u);
-    if (s & 4u) m = ((m & 0x0fu) << 4) | ((m >> 4) & 0x0fu);
-    return m;
-}
-
-// One quantised slot, conservatively (as slab_cons_fast). A plane's t is
-// fl(q A + B), A = ix 2^e (exact: a power-of-two scaling), B = fl(origin ix
-// - fl(o ix)); against the exact T of the decoded plane P' = fl(origin +
-// q 2^e) it is off by at most 2.01 u |T| (ix and the final rounding) plus
-// u (|o ix| + |B| + |P ix|) (oix, B's rounding, P' - P), all < 2 u M with
-// M = |o ix| + |origin ix| + 255 |A| over the axes: mw = 2^-22 M (4 u M)
-// covers it twice, added to the margin and the pruning growth as mo is.
-__device__ __forceinline__ bool w8_slot(const Prune& p, float ix, float iy, float iz, float Ax, float Bx, float Ay,
-                                        float By, float Az, float Bz, float mw, float lx, float hx, float ly,
-                                        float hy, float lz, float hz)
-{
-    const float tx1 = fmaf(lx, Ax, Bx), tx2 = fmaf(hx, Ax, Bx);
-    const float ty1 = fmaf(ly, Ay, By), ty2 = fmaf(hy, Ay, By);
-    const float tz1 = fmaf(lz, Az, Bz), tz2 = fmaf(hz, Az, Bz);
-    const float nx = fminf(tx1, tx2), ny = fminf(ty1, ty2), nz = fminf(tz1, tz2);
-    constexpr float c = 1.0f - 0x1p-20f;
-    const float entry = fmaxf(fmaf(nx, c, -fmaf(p.m, fabsf(ix), mw)),
-                              fmaxf(fmaf(ny, c, -fmaf(p.m, fabsf(iy), mw)), fmaf(nz, c, -fmaf(p.m, fabsf(iz), mw))));
-    const float tmin = fmaxf(nx, fmaxf(ny, nz));
-    const float tmax = fminf(fmaxf(tx1, tx2), fminf(fmaxf(ty1, ty2), fmaxf(tz1, tz2)));
-    const float m = fmaf(fabsf(tmin) + fabsf(tmax), 0x1p-20f, 2.0f * mw);
-    return !(entry > p.lim) & !(tmax + m < fmaxf(tmin, kEps));
-}
-
-template <bool FAST>
-__device__ __forceinline__ void wide8_lane_step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
-                                                WideWalk& w, uint32_t* stk, float& best_t, int& best_s,
-                                                lds_uint4* hc = nullptr, uint32_t hc_n = 0)
-{
-    Counters cnt{0, 0, 0, 0, 0};
-    if (w.end) {
-        lane_step<FAST, false, true>(sc, sr, sp, pr, w.cur, best_t, best_s, cnt);
-        if (w.cur >= w.end) {
-            w.end = 0;
-            wide_walk_pop(w, stk);
-        }
-        return;
-    }
-    uint4 u0, u1, u2, u3;
-    if (w.cur < hc_n) {
-        lds_uint4* q = hc + 4 * w.cur;
-        u0 = lds_load(q);
-        u1 = lds_load(q + 1);
-        u2 = lds_load(q + 2);
-        u3 = lds_load(q + 3);
-    } else {
-        const uint4* q = (const uint4*)(sc.wunits + w.cur);
-        u0 = q[0];
-        u1 = q[1];
-        u2 = q[2];
-        u3 = q[3];
-    }
-    const float orx = h_lo(u0.x), ory = h_hi(u0.x), orz = h_lo(u0.y);
-    const int ex = (int)(int8_t)(uint8_t)(u0.y >> 16), ey = (int)(int8_t)(uint8_t)(u0.y >> 24);
-    const int ez = (int)(int8_t)(uint8_t)u0.z;
-    const uint32_t valid = (u0.z >> 8) & 0xffu, leafm = (u0.z >> 16) & 0xffu, base = u0.w;
-    // the fast test needs A = ix 2^e exact and normal: |ix| >= 2^-60 (e >=
-    // -64); other rays (a zero, tiny or huge direction component: none of
-    // the hemisphere's in practice) walk the unit's subtree as a DFS segment
-    if (sr.generic || fminf(fabsf(sr.ix), fminf(fabsf(sr.iy), fabsf(sr.iz))) < 0x1p-60f) {
-        const HAux ax = sc.waux[w.cur];
-        w.cur = ax.flat + 1;
-        w.end = ax.end;
-        return;
-    }
-    uint32_t pass = 0;
-    {
-        const float oix = sr.ox * sr.ix, oiy = sr.oy * sr.iy, oiz = sr.oz * sr.iz;
-        const float Ax = ldexpf(sr.ix, ex), Ay = ldexpf(sr.iy, ey), Az = ldexpf(sr.iz, ez);
-        const float Bx = fmaf(orx, sr.ix, -oix), By = fmaf(ory, sr.iy, -oiy), Bz = fmaf(orz, sr.iz, -oiz);
-        const float M = fmaxf(fabsf(oix) + fabsf(orx * sr.ix) + 255.0f * fabsf(Ax),
-                              fmaxf(fabsf(oiy) + fabsf(ory * sr.iy) + 255.0f * fabsf(Ay),
-                                    fabsf(oiz) + fabsf(orz * sr.iz) + 255.0f * fabsf(Az)));
-        const float mw = M * 0x1p-22f;
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const int h = k >> 2, b = k & 3;
-            const uint32_t lx = h ? u1.y : u1.x, ly = h ? u1.w : u1.z, lz = h ? u2.y : u2.x;
-            const uint32_t hx = h ? u2.w : u2.z, hy = h ? u3.y : u3.x, hz = h ? u3.w : u3.z;
-            const bool ok = w8_slot(pr, sr.ix, sr.iy, sr.iz, Ax, Bx, Ay, By, Az, Bz, mw, u8f(lx, b), u8f(hx, b),
-                                    u8f(ly, b), u8f(hy, b), u8f(lz, b), u8f(hz, b));
-            pass |= (uint32_t)ok << k;
-        }
-    }
-    pass &= valid;
-    // passing leaf slots: each lane works through its own list (as wide_lane_step)
-    uint32_t lm = pass & leafm;
-    const uint32_t inner = pass & ~leafm;
-    while (__ballot(lm != 0)) {
-        if (lm) {
-            const uint32_t k = __builtin_ctz(lm);
-            lm &= lm - 1;
-            const uint32_t unit = base + (uint32_t)__builtin_popcount(valid & ((1u << k) - 1u));
-            wide_leaf<FAST, false>(sc, sr, sp, pr, kPLeaf | 0u, best_t, best_s, cnt,
-                                   (const float4*)(sc.wunits + unit));
-        }
-    }
-    const uint32_t n = (uint32_t)__builtin_popcount(inner);
-    if (n == 0) {
-        wide_walk_pop(w, stk);
-        return;
-    }
-    if (w.top + n - 1 > (uint32_t)kWideStack) {
-        const HAux ax = sc.waux[w.cur];
-        w.cur = ax.flat + 1;
-        w.end = ax.end;
-        return;
-    }
-    // near side first: bit i of `ord` is position i ^ s
-    const uint32_t s = (sr.dx < 0.0f ? 1u : 0u) | (sr.dy < 0.0f ? 2u : 0u) | (sr.dz < 0.0f ? 4u : 0u);
-    uint32_t ord = perm8(inner, s);
-    // push all but the nearest, farthest first; the nearest is next
-    while (ord & (ord - 1)) {
-        const uint32_t i = 31u - (uint32_t)__builtin_clz(ord);
-        ord &= ~(1u << i);
-        const uint32_t k = i ^ s;
-        stk[w.top * kWideStride] = base + (uint32_t)__builtin_popcount(valid & ((1u << k) - 1u));
-        w.top++;
-    }
-    const uint32_t k = (uint32_t)__builtin_ctz(ord) ^ s;
-    w.cur = base + (uint32_t)__builtin_popcount(valid & ((1u << k) - 1u));
-}
-
 // Closest hit for every active lane: degenerate rays (a zero or tiny
 // direction component, `SlabRay::generic`) one at a time with the whole
 // wave (closest_bvh_chunked), the rest with the lane-parallel walk (or the
@@ -1357,18 +1190,6 @@ __device__ __forceinline__ void closest_hit(const DevScene& sc, const Ray& ray, 
         // packet like any other
         closest_packet_ordered<FAST, COUNT>(sc, ray, active, best_t, best_s, cnt);
         gen = false;
-    } else if (!UNIFORM && FAST && !COUNT && sc.wunits && wstk) {
-        // the eight-wide walk (MIRT_OPT_BOUNCE_WALK 8; no work counters)
-        const SlabRay sr = slab_ray(ray);
-        const SphRay sp = sph_ray(ray);
-        Prune pr = prune_off();
-        best_t = INFINITY;
-        best_s = -1;
-        WideWalk w = wide_walk_start(active && !gen);
-        while (__ballot(wide_walking(w))) {
-            if (!wide_walking(w)) continue;
-            wide8_lane_step<FAST>(sc, sr, sp, pr, w, wstk, best_t, best_s);
-        }
     } else if (!UNIFORM && FAST && sc.wide && wstk) {
         // the bounce kernel's walk (wstk: a kWideStack-entry LDS column)
         const SlabRay sr = slab_ray(ray);

@@ -391,12 +391,8 @@ enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3,
        MIRT_OPT_BOUNCE_BLOCKS = 9,  /* wavefront: persistent bounce workgroups, 0 = occupancy x CUs
                                        (default: best for one frame at a time); with several contexts
                                        keeping frames in flight, ~1.5 per CU (384 on MI355X) */
-       MIRT_OPT_QUAD_DRAIN = 11,    /* four-wide bounce walk: 1 (default) = once the queue is dry
-                                       and <= 16 lanes of a wave are busy, finish them as quads */
-       MIRT_OPT_BOUNCE_WALK = 12    /* ordered bounce walk over 4-wide fp16 nodes (4) or 8-wide nodes
-                                       with 8-bit slot boxes in the node's frame (8; used when the
-                                       tree's frames encode, else 4; no quad drain; mirt_get_option
-                                       reads back the walk in effect for the uploaded scene) */ };
+       MIRT_OPT_QUAD_DRAIN = 11     /* four-wide bounce walk: 1 (default) = once the queue is dry
+                                       and <= 16 lanes of a wave are busy, finish them as quads */ };
 /* Traversal ids keep their first-release values (mirt 0.1: TILE 0, WAVEFRONT 5);
    the retired ids 1-4 (per-lane / chunked / DFS-only schedules of mirt 0.1) and
    the retired option ids 8, 10, 12, 13 return MIRT_E_INVALID. */

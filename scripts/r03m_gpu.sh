@@ -1,6 +1,8 @@
 #!/bin/bash
 # Round 3: the eight-wide quantised bounce walk (MIRT_OPT_BOUNCE_WALK 8):
 # its parity tests, then bench A/B against the four-wide walk per workload.
+# (The variant lost and was removed after this run: commit 1cb0f72 holds it;
+# results in profiles/r03m_walk8_ab/ and DESIGN.md §8.)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp

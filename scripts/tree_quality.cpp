@@ -360,6 +360,7 @@ float sphere_t(const Ray& r, const mirt_sphere& s)
 
 struct Stats {
     double visits = 0, gates = 0, rays = 0, pushes = 0;
+    double over = 0;  // steps whose pushes would overflow a 20-entry stack (the kernel's kWideStack)
     int max_stack = 0;
 };
 
@@ -404,6 +405,7 @@ int walk(const Tree& t, const std::vector<Leaf>& L, const mirt_sphere* sp, const
             }
         }
         std::sort(in, in + m, [](auto& a, auto& b) { return a.first > b.first; });  // far first: near on top
+        if (m > 0 && (int)stack.size() + m - 1 > 20) st.over++;
         for (int k = 0; k < m; k++) {
             if (!g_order && in[k].first > best) continue;
             stack.push_back(in[k].second);
@@ -747,8 +749,8 @@ int main(int argc, char** argv)
             }
         }
     auto pr = [](const char* name, const Stats& s, size_t nodes) {
-        printf("  %-28s nodes %7zu  rays %8.0f  visits/ray %7.2f  gates/ray %6.2f  pushes/ray %6.2f  max stack %d\n",
-               name, nodes, s.rays, s.visits / s.rays, s.gates / s.rays, s.pushes / s.rays, s.max_stack);
+        printf("  %-28s nodes %7zu  rays %8.0f  visits/ray %7.2f  gates/ray %6.2f  pushes/ray %6.2f  max stack %d  overflow/ray %.4f\n",
+               name, nodes, s.rays, s.visits / s.rays, s.gates / s.rays, s.pushes / s.rays, s.max_stack, s.over / s.rays);
     };
     printf("%s %d spheres, %zu live leaves, %d flat nodes, pixel stride %d, SAH bins %d, leaf max %d\n",
            scene.c_str(), n, leaves.size(), nn, stride, g_bins, g_leaf_max);

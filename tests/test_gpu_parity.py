@@ -897,142 +897,3 @@ def test_bench_launch_plan_displays(gpu, mirt, batch):
     finally:
         for x in rs:
             x.close()
-
-
-def _walk8(gpu, mirt):
-    """Select the eight-wide bounce walk; True if the uploaded tree encoded."""
-    gpu.set_option(mirt.abi.OPT_BOUNCE_WALK, 8)
-    return gpu.get_option(mirt.abi.OPT_BOUNCE_WALK) == 8
-
-
-def test_walk8_golden_frames(gpu, mirt, golden, small):
-    """The eight-wide quantised walk (MIRT_OPT_BOUNCE_WALK 8) renders every
-    golden depth-5 BVH frame (wavefront schedule) and the 1080p 10k frame
-    under the tile schedule too, byte for byte."""
-    abi = mirt.abi
-    cs = cams(mirt, small)
-    try:
-        seen = 0
-        for key in sorted(golden["frames"]):
-            p = parse_frame_key(key)
-            if p["depth"] < 2 or p["mode"] != 1 or not p["use_bvh"]:
-                continue
-            s, b = _scene(mirt, p["kind"], p["n"])
-            gpu.upload(s, b)
-            assert _walk8(gpu, mirt), key
-            img = gpu.render_frame(cs[p["cam"]], p["W"], p["H"], depth=p["depth"], seed=p["seed"])[::p["step"]]
-            assert sha(img) == golden["frames"][key]["sha"], key
-            seen += 1
-        assert seen >= 3
-        gpu.set_option(abi.OPT_TRAVERSAL, abi.TRAV_TILE)
-        s, b = _scene(mirt, "render", 10000)
-        gpu.upload(s, b)
-        img = gpu.render_frame(mirt.default_camera(), 1920, 1080, depth=5, seed=1)
-        assert sha(img) == golden["frames"]["1920x1080_render10000_d5_m1_b1_s1_c0_step1"]["sha"]
-    finally:
-        gpu.set_option(abi.OPT_TRAVERSAL, abi.TRAV_WAVEFRONT)
-        gpu.set_option(abi.OPT_BOUNCE_WALK, 4)
-
-
-@pytest.mark.parametrize("kind,n", [("render", 10000), ("bench", 100000), ("bench", 1000000)])
-def test_walk8_hard_rays(gpu, mirt, oracle, kind, n):
-    """Closest hits of 300k hard rays (near-tangent, grazing, anywhere)
-    through the eight-wide walk == the four-wide walk == the reference-order
-    DFS, bit for bit; the oracle on a subset."""
-    abi = mirt.abi
-    s, b = _scene(mirt, kind, n)
-    gpu.upload(s, b)
-    rays = _hard_rays(np.random.default_rng(17), s, 300_000)
-    try:
-        four = gpu.ray_bvh_intersect(rays)
-        assert _walk8(gpu, mirt)
-        eight = gpu.ray_bvh_intersect(rays)
-        gpu.set_option(abi.OPT_ORDERED, 0)
-        gpu.set_option(abi.OPT_PRUNE, 0)
-        dfs = gpu.ray_bvh_intersect(rays)
-    finally:
-        gpu.set_option(abi.OPT_BOUNCE_WALK, 4)
-        gpu.set_option(abi.OPT_ORDERED, 1)
-        gpu.set_option(abi.OPT_PRUNE, 1)
-    assert eight.tobytes() == dfs.tobytes()
-    assert four.tobytes() == dfs.tobytes()
-    if n <= 100000:
-        s2 = mirt.create_random_spheres(n, 1) if kind == "render" else mirt.create_benchmark_spheres(n, 1)
-        t = oracle.build(s2)
-        sub = np.ascontiguousarray(rays[::20])
-        ref = oracle.intersect(t, s2, sub)
-        oracle.free(t)
-        assert eight[::20].tobytes() == ref.tobytes()
-
-
-def test_walk8_frames_and_fallback(gpu, mirt, oracle):
-    """Scenes at the edges of the eight-bit frames: tiny spheres far from
-    the origin (fp16 frame corners far below the boxes, fine steps), spheres
-    of radius 0 (degenerate boxes), and a scene beyond the fp16 range (does
-    not encode: the four-wide walk runs). Each frame and each hard-ray hit
-    equals the reference-order DFS (and a frame the oracle)."""
-    abi = mirt.abi
-    rng = np.random.default_rng(23)
-    cam = mirt.default_camera()
-
-    def scene(centre, spread, rmin, rmax, n=3000):
-        s = np.zeros(n, abi.SPHERE)
-        s["center"] = centre + rng.uniform(-spread, spread, (n, 3))
-        s["radius"] = rng.uniform(rmin, rmax, n)
-        s["color"] = rng.integers(0, 256, (n, 4))
-        return s
-
-    cases = [(scene(np.array([3000.0, -2000.0, -4000.0]), 2.0, 1e-3, 2e-2), True),
-             (scene(np.array([0.0, 0.0, -20.0]), 10.0, 0.0, 0.0), True),
-             (scene(np.array([0.0, 1e5, -1e5]), 1e4, 10.0, 500.0), False)]
-    try:
-        for k, (s0, encodes) in enumerate(cases):
-            s = s0.copy()
-            b = mirt.build_bvh(s)
-            gpu.upload(s, b)
-            assert _walk8(gpu, mirt) == encodes, k
-            rays = _hard_rays(np.random.default_rng(k), s, 60_000)
-            eight = gpu.ray_bvh_intersect(rays)
-            gpu.set_option(abi.OPT_ORDERED, 0)
-            gpu.set_option(abi.OPT_PRUNE, 0)
-            dfs = gpu.ray_bvh_intersect(rays)
-            gpu.set_option(abi.OPT_ORDERED, 1)
-            gpu.set_option(abi.OPT_PRUNE, 1)
-            assert eight.tobytes() == dfs.tobytes(), k
-            # a frame looking at the cluster from outside it
-            c = s["center"].mean(0)
-            view = mirt.default_camera()                       # looking down -z
-            view.position.x, view.position.y = float(c[0]), float(c[1])
-            view.position.z = float(c[2] + 3.0 * np.ptp(s["center"][:, 2]) + 1.0)
-            img = gpu.render_frame(view, 96, 64, depth=5, seed=2)
-            gpu.set_option(abi.OPT_BOUNCE_WALK, 4)
-            ref = gpu.render_frame(view, 96, 64, depth=5, seed=2)
-            assert (img == ref).all(), k
-            if k == 0:
-                so = s0.copy()
-                t = oracle.build(so)
-                want = oracle.render(view, 96, 64, so, t, depth=5, seed=2, mode=1)
-                oracle.free(t)
-                assert (img == want).all()
-    finally:
-        gpu.set_option(abi.OPT_BOUNCE_WALK, 4)
-        gpu.set_option(abi.OPT_ORDERED, 1)
-        gpu.set_option(abi.OPT_PRUNE, 1)
-
-
-def test_walk8_phantom_scenes(gpu, mirt, oracle):
-    """The orphan-phantom tree (reference DFS order kept: no eight-wide walk
-    may run on it) and the grazing rays at 0-sphere leaves under walk 8."""
-    s, rays = _bench_like_phantom_scene(mirt)
-    so = s.copy()
-    t = oracle.build(so, 0, 3, 20)
-    want = oracle.intersect(t, so, rays)
-    oracle.free(t)
-    root = mirt.build_bvh_node(s, 0, 3, 20)
-    try:
-        gpu.upload(s, root)
-        assert not _walk8(gpu, mirt)
-        assert gpu.closest_hit(rays).tobytes() == want.tobytes()
-    finally:
-        mirt.free_bvh(root)
-        gpu.set_option(mirt.abi.OPT_BOUNCE_WALK, 4)
