@@ -408,17 +408,24 @@ def main():
         return dry_main(args, world, rank)
     if not args.pipeline:
         args.pipeline = 4 if world == 1 else PIPELINE_MULTI
-    if world > 1:
-        # one hardware queue per context stream plus RCCL's (HIP's default is 4
-        # per process; read when the runtime starts, i.e. before the first GPU
-        # call below): the one-frame split emulated per shard with a slab copy
-        # on a fifth stream, profiles/r03f/, r03g/
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", str(HW_QUEUES_MULTI))
     # MIRT_BENCH_SHARE_GPU=1: a rehearsal of the N > 1 path on a one-GPU box --
     # every rank on device 0 and gloo in place of RCCL (which refuses two ranks
     # on one device); the same launches, shard geometry, gathers (staged
     # through host memory) and max-over-ranks timing. Not a measurement.
     rehearse = world > 1 and os.environ.get("MIRT_BENCH_SHARE_GPU") == "1"
+    if world > 1 and not rehearse:
+        # one hardware queue per context stream plus RCCL's, read when the HIP
+        # runtime starts (before the first GPU call below). The GPU boxes export
+        # GPU_MAX_HW_QUEUES=4 (HIP's default), which would put the 8 contexts
+        # and RCCL on 4 queues: the one-frame split emulated per shard ran 11.9
+        # Grays/s at N = 8 there against 13.8 on 16 (profiles/r03f/, r03g/), so
+        # a lower value is raised to HW_QUEUES_MULTI (one rank per GPU)
+        try:
+            have = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
+        except ValueError:
+            have = 0
+        if have < HW_QUEUES_MULTI:
+            os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES_MULTI)
     dev = (0 if rehearse else local) if world > 1 else 0
     if world > 1:
         torch.cuda.set_device(dev)
@@ -609,7 +616,7 @@ def main():
                        "jitter": JITTER,
                        "frames_per_step": fps, "frames_per_launch": per_launch, "launches": len(timed_plan),
                        "pipeline": len(rs), "bounce_blocks": blocks, "bvh_nodes": len(bvh),
-                       "row_block": ROW_BLOCK,
+                       "row_block": ROW_BLOCK, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                        "step": (f"{fps} frame(s) of the still-camera display loop (main.c:379-408), ctxs sharing "
                                 "one accumulation buffer (mirt_ctx_share_accum)" if args.accumulate else
                                 f"{fps} fresh frame(s) (main.c:358-374)")

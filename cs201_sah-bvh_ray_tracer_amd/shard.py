@@ -61,7 +61,7 @@ def gather_frame(slab, height, row_block, group=None, dst=0):
     elsewhere."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    if world == 1:
+    if not dist.is_initialized():
         bufs = [slab]
     else:
         # gloo gathers host tensors (a rehearsal / CPU run): stage device slabs

@@ -52,3 +52,51 @@ def test_multi_rank_bench_rehearsal_on_one_gpu():
     d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["value"] > 0
     assert "REHEARSAL" in d["data"] and d["value_weak"] > 0 and d["value_strong"] == d["value"]
+
+
+RCCL_ONE_RANK = r'''
+import hashlib, importlib, json, os, sys
+import torch
+import torch.distributed as dist
+sys.path.insert(0, sys.argv[1])
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+m = importlib.import_module("cs201_sah-bvh_ray_tracer_amd")
+from importlib import import_module
+shard = import_module("cs201_sah-bvh_ray_tracer_amd.shard")
+g = json.load(open(os.path.join(sys.argv[1], "tests", "golden", "golden.json")))
+want = g["frames"]["1920x1080_render10000_d5_m1_b1_s1_c0_step1"]["sha"]
+s = m.create_random_spheres(10000, 1)
+b = m.build_bvh(s)
+rs = [m.Renderer(0) for _ in range(4)]
+for r in rs:
+    r.upload(s, b)
+sf = shard.ShardedFrame(rs[0], 1920, 1080, renderers=rs)
+cam = m.default_camera()
+ok = []
+for k in range(6):
+    sf.render_local(cam, sf.desc(seed=1))
+    f = sf.gather()
+    torch.cuda.synchronize()
+    ok.append(hashlib.sha256(shard.as_rgba(f).cpu().numpy().tobytes()).hexdigest() == want)
+dist.destroy_process_group()
+print(json.dumps({"backend": "nccl", "frames_ok": ok}))
+sys.exit(0 if all(ok) else 3)
+'''
+
+
+@pytest.mark.gpu
+def test_rccl_gather_one_rank():
+    """The RCCL leg of the N > 1 path on the one-GPU box: a world-1 nccl
+    process group, four contexts rotating frames on their own streams, each
+    frame's slab gathered by dist.gather (RCCL) under its context's stream,
+    every gathered frame equal to the golden 1080p frame. (Two ranks cannot
+    share one device under RCCL; the multi-rank geometry is the gloo
+    rehearsal above and tests/test_shard_gloo.py.)"""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29731", RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, "-c", RCCL_ONE_RANK, ROOT], capture_output=True, text=True, timeout=240,
+                       env=env, cwd=ROOT)
+    assert p.returncode == 0, (p.stdout[-1000:], p.stderr[-3000:])
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["frames_ok"] == [True] * 6
