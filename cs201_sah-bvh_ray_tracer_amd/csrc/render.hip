@@ -304,6 +304,22 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask)
 constexpr uint32_t kHCache = MIRT_HCACHE;
 constexpr int kBounceDiag = 10;  // mirt_bounce_stats words per wave  // HNodes staged in LDS per bounce workgroup (64 B each)
 
+// The bounce queue's control words: {records written} in the first 128-B
+// line, then one read head per queue SEGMENT, each in its own line. The
+// bounce waves read the queue as kQSeg contiguous segments (the primary
+// pass fills it in roughly tile order, so a segment is roughly a band of the
+// image): the waves of workgroup b start on segment b % kQSeg -- the
+// workgroups that share an XCD (dealt round-robin over the 8), so a
+// segment's rays, and the nodes near their origins, stay in one XCD's L2 --
+// and move on to the next segment when theirs runs dry. Eight heads also
+// split the refill atomics that one word would serialise.
+#ifndef MIRT_QSEG
+#define MIRT_QSEG 8
+#endif
+constexpr uint32_t kQSeg = MIRT_QSEG;
+constexpr uint32_t kQLine = 32;                        // dwords per 128-B line
+constexpr size_t kQCtlBytes = 4 * kQLine * (1 + kQSeg);
+
 // First bounce of one pixel, produced by primary_kernel.
 struct BounceRec {
     float ox, oy, oz, dx, dy, dz;
@@ -576,6 +592,7 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
     uint32_t* stk = wstack + (LANE4 ? threadIdx.x : 0);
     Counters cnt{0, 0, 0, 0, 0};
     const uint32_t n = __builtin_amdgcn_readfirstlane(qctl[0]);
+    uint32_t seg = blockIdx.x % kQSeg, segs_left = kQSeg;  // wave-uniform
     bool has = false, exhausted = false;
     Ray ray{0, 0, 0, 0, 0, 0};
     SlabRay sr = slab_ray(ray);
@@ -592,19 +609,25 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
     float best_t = INFINITY;
     uint64_t key = 0;
     for (;;) {
-        // refill lanes that own no chain (one atomic per wave, tile order kept)
+        // refill lanes that own no chain (one atomic per wave, tile order
+        // kept), from the next segment while the current one is dry
         const uint64_t need = __ballot(!has);
-        if (need && !exhausted) {
+        while (need && !exhausted) {
             const int leader = __builtin_ctzll(need);
+            const uint32_t lo = (uint32_t)((uint64_t)n * seg / kQSeg);
+            const uint32_t sz = (uint32_t)((uint64_t)n * (seg + 1) / kQSeg) - lo;
             uint32_t b = 0;
-            if ((threadIdx.x & 63) == leader) b = atomicAdd(&qctl[1], (uint32_t)__popcll(need));
+            if ((threadIdx.x & 63) == leader) b = atomicAdd(&qctl[kQLine * (1 + seg)], (uint32_t)__popcll(need));
             b = __builtin_amdgcn_readlane(b, leader);
-            if (b + (uint32_t)__popcll(need) >= n) exhausted = true;
+            if (b + (uint32_t)__popcll(need) >= sz) {  // this segment is dry: the next one
+                seg = seg + 1 == kQSeg ? 0 : seg + 1;
+                if (--segs_left == 0) exhausted = true;
+            }
             if (!has) {
                 const uint32_t lane0 = threadIdx.x & 63;
                 const uint32_t idx = b + (uint32_t)__popcll(need & ((1ull << lane0) - 1));
-                if (idx < n) {
-                    const BounceRec rec = queue[idx];
+                if (idx < sz) {
+                    const BounceRec rec = queue[lo + idx];
                     ray = Ray{rec.ox, rec.oy, rec.oz, rec.dx, rec.dy, rec.dz};
                     sr = slab_ray(ray);
                     sp = sph_ray(ray);
@@ -621,6 +644,7 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                     has = true;
                 }
             }
+            if (b < sz) break;
         }
         if (!__ballot(has)) break;
         if (DIAG && exhausted && !dg_tx) dg_tx = __builtin_amdgcn_s_memrealtime();
@@ -1578,11 +1602,11 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
     }
     if (wavefront) {
         const size_t pixels = (size_t)f.num_rows * f.width;
-        int rc = ensure(&c->d_queue, &c->queue_cap, sizeof(BounceRec) * pixels + 64);
+        int rc = ensure(&c->d_queue, &c->queue_cap, sizeof(BounceRec) * pixels + kQCtlBytes);
         if (rc) return rc;
-        uint32_t* qctl = (uint32_t*)c->d_queue;                          // {count, head}
-        BounceRec* queue = (BounceRec*)((char*)c->d_queue + 64);
-        HIP_TRY(hipMemsetAsync(qctl, 0, 8, s));
+        uint32_t* qctl = (uint32_t*)c->d_queue;                          // {count}, segment heads
+        BounceRec* queue = (BounceRec*)((char*)c->d_queue + kQCtlBytes);
+        HIP_TRY(hipMemsetAsync(qctl, 0, kQCtlBytes, s));
         // primary_kernel's packets: 8x8 pixel tiles, or 4x4 pixels x 4 frames
         // for an ordered walk over four frames or more
         const int ptiles = c->fast_slab && sc.ordered && f.samples >= 4
