@@ -570,9 +570,15 @@ def main():
     r.set_option(mirt.abi.OPT_BOUNCE_BLOCKS, blocks)
 
     t = torch.tensor([elapsed, kernel_ms, elapsed_d1, elapsed_other or 0.0], dtype=torch.float64, device="cuda")
+    # the whole job's reference-DFS bytes per launch (every
+    # rank's shard), for B / t / (G x 8 TB/s)
+    job_b = torch.tensor([algorithmic_bytes(ref_counts, my_rows * W * SPP * per_launch)], dtype=torch.float64,
+                         device="cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(job_b, op=dist.ReduceOp.SUM)
     elapsed, kernel_ms_max, elapsed_d1, elapsed_other = (float(v) for v in t)
+    job_bytes_per_launch = float(job_b[0])
 
     host = None
     if rank == 0 and world == 1 and not args.no_host:
@@ -650,6 +656,12 @@ def main():
                 "launch_executed_bytes": int(exec_frame_bytes),
                 "frame_period_ms": round(elapsed / args.steps * 1e3, 4),
                 "frame_algorithmic_gbs": round(ref_frame_bytes / batch / (elapsed / args.steps) / 1e9, 1),
+                "job": {"note": "SURVEY 8(e): every rank's reference-DFS bytes over the timed launches / the "
+                                "max-over-ranks timed region, against n_gpus x the HBM peak",
+                        "algorithmic_bytes_per_launch": int(job_bytes_per_launch),
+                        "gbs": round(job_bytes_per_launch * len(timed_plan) / elapsed / 1e9, 1),
+                        "frac": round(job_bytes_per_launch * len(timed_plan) / elapsed / 1e9
+                                      / (world * PEAK_HBM_GBS), 4)},
                 "serial_launch": {
                     "note": "the same launch alone (untimed serial loop, the full persistent bounce grid): not "
                             "the timed configuration",
