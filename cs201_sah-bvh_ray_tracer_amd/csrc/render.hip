@@ -501,8 +501,8 @@ struct BounceWalk<2> {
     WideWalk w;
     lds_uint4* hc = nullptr;  // the top HNodes staged in LDS (bounce_kernel)
     uint32_t hc_n = 0;
-    __device__ void start(const DevScene&) { w = wide_walk_start(true); }
-    __device__ void stop() { w = wide_walk_start(false); }
+    __device__ void start(const DevScene& sc) { w = wide_walk_start(sc, true); }
+    __device__ void stop() { w = WideWalk{kPNone, 0u, 0u}; }
     __device__ bool walking() const { return wide_walking(w); }
     template <bool FAST>
     __device__ void step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr, uint32_t* stk,
@@ -733,7 +733,7 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                                     acc, (lane & 3) == 0)) {
                         sr = slab_ray(ray);
                         sp = sph_ray(ray);
-                        qw = QuadWalk{0u, 0u, 0u};
+                        qw = QuadWalk{sc.wide_root, 0u, 0u};
                         best_t = INFINITY;
                         best_s = -1;
                         pr = prune_off();
@@ -1130,6 +1130,7 @@ struct mirt_ctx {
     HAux* d_haux = nullptr;
     LeafRec* d_leaves = nullptr;
     uint32_t num_hnodes = 0;
+    uint32_t wide_root = 0;     // HNode a four-wide walk starts at (DevScene::wide_root)
     uint8_t* d_ndepth = nullptr;  // depth of every flat node (BVH overlay colours)
     uint32_t* d_overlay = nullptr;  // BVH overlay: per-pixel last line in draw order
     size_t overlay_cap = 0;
@@ -1456,7 +1457,7 @@ DevScene dev_scene(const mirt_ctx* c)
     const bool ordered = prune && c->ordered && c->ordered_ok && c->fast_slab;
     return DevScene{c->d_nodes, c->d_nodes32, c->d_geo, c->d_color, (uint32_t)c->num_nodes, c->num_spheres,
                     prune, c->r_max, c->c_max, c->d_pnodes, ordered, c->d_hnodes, c->d_haux, c->d_leaves, ordered,
-                    ordered ? c->num_hnodes : 0u};
+                    ordered ? c->num_hnodes : 0u, c->wide_root};
 }
 
 AccumShare* accum_new(int device)
@@ -1833,6 +1834,10 @@ try {
     c->num_nodes = nn;
     c->num_spheres = ns;
     c->num_hnodes = (uint32_t)hn.size();
+    {
+        const uint32_t r = hn[0].slot[0].ref;
+        c->wide_root = (r != kPNone && !(r & kPLeaf)) ? r : 0u;
+    }
     c->ordered_ok = ordered;
     c->prune_ok = encloses;
     c->r_max = r_max;

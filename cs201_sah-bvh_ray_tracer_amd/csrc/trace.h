@@ -118,6 +118,10 @@ struct DevScene {
     const LeafRec* leaves;
     int wide;
     uint32_t num_hnodes;  // HNodes, numbered breadth-first: the first ones are the top levels
+    // where a four-wide walk starts: the root's own HNode (1) -- HNode 0's
+    // single slot is the root box, which every ray that can hit a leaf passes
+    // (boxes nest), so its step is skipped -- or 0 when the root is a leaf
+    uint32_t wide_root;
 };
 
 // LDS-resident node data (address space 3: ds_read, never a flat load)
@@ -893,7 +897,10 @@ struct WideWalk {
     uint32_t cur, end, top;
 };
 
-__device__ __forceinline__ WideWalk wide_walk_start(bool active) { return WideWalk{active ? 0u : kPNone, 0u, 0u}; }
+__device__ __forceinline__ WideWalk wide_walk_start(const DevScene& sc, bool active)
+{
+    return WideWalk{active ? sc.wide_root : kPNone, 0u, 0u};
+}
 __device__ __forceinline__ bool wide_walking(const WideWalk& w) { return w.cur != kPNone; }
 
 __device__ __forceinline__ void wide_walk_pop(WideWalk& w, const uint32_t* stk)
@@ -1197,7 +1204,7 @@ __device__ __forceinline__ void closest_hit(const DevScene& sc, const Ray& ray, 
         Prune pr = prune_off();
         best_t = INFINITY;
         best_s = -1;
-        WideWalk w = wide_walk_start(active && !gen);
+        WideWalk w = wide_walk_start(sc, active && !gen);
         while (__ballot(wide_walking(w))) {
             if (!wide_walking(w)) continue;
             wide_lane_step<FAST, COUNT>(sc, sr, sp, pr, w, wstk, best_t, best_s, cnt);
