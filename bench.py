@@ -633,7 +633,9 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
-                "kernel": KERNEL, "kernel_ms": round(bounce_ms, 4),
+                "kernel": (KERNEL.replace("<true, 2,", "<true, 4,")
+                           if r.get_option(mirt.abi.OPT_LEAF_BATCH) else KERNEL),
+                "kernel_ms": round(bounce_ms, 4),
                 "kernel_ms_source": f"mean over the {len(timed_phases)} timed launches ({per_launch} frame(s) each) "
                                     "of HIP events recorded on each launch's own stream around its bounce kernel "
                                     "(mirt_phase_log): the launch's duration UNDER the timed loop's overlap of "

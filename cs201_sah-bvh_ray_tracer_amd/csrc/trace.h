@@ -962,11 +962,30 @@ __device__ __forceinline__ void wide_leaf(const DevScene& sc, const SlabRay& sr,
     }
 }
 
+// The timed gate of wide_leaf with its sphere already loaded: the sphere,
+// then (for a hit that could win) the exact box.
+__device__ __forceinline__ void leaf_gate(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
+                                          uint32_t ref, float4 g, float& best_t, int& best_s)
+{
+    const float t = sphere_t<true>(sp, g, best_t);
+    if (t > 0.0f) {
+        const float4* lp = (const float4*)(sc.leaves + (ref & ~kPLeaf));
+        const float4 l0 = lp[0], l1 = lp[1];
+        const int si = __float_as_int(l1.z);
+        float e;
+        if ((t < best_t || si > best_s) && slab_box<true>(sr, pr, l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, e)) {
+            best_t = t;
+            best_s = si;
+            if (sc.prune) prune_update(pr, sc, sr.ox, sr.oy, sr.oz, sp.a4, t);
+        }
+    }
+}
+
 // hc / hc_n: the first hc_n HNodes (the tree's top levels, visited by
 // every ray) staged in LDS by the caller; a node there is read from LDS
 // instead of through the vector-memory path (the bounce kernel's busiest
 // unit, TD: its cost is the bytes returned per lane, however coalesced).
-template <bool FAST, bool COUNT>
+template <bool FAST, bool COUNT, bool BATCH = false>
 __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
                                                WideWalk& w, uint32_t* stk, float& best_t, int& best_s, Counters& cnt,
                                                lds_uint4* hc = nullptr, uint32_t hc_n = 0)
@@ -1020,6 +1039,25 @@ __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay
     h1 = h1 && !(lm & 2);
     h2 = h2 && !(lm & 4);
     h3 = h3 && !(lm & 8);
+    if constexpr (BATCH && FAST && !COUNT) {
+        // every passing leaf's sphere requested at once (one dependent round
+        // trip for the step instead of one per leaf), then the gates in slot
+        // order against the best so far (least t, a tie to the larger index:
+        // order-free). Pays where the leaf records miss L2 (a 1M-sphere
+        // scene); on an L2-resident tree the extra live registers cost more
+        // than the round trips they save
+        if (__ballot(lm != 0)) {
+            float4 g0, g1, g2, g3;
+            if (lm & 1) g0 = sc.leaves[q3.x & ~kPLeaf].geo;
+            if (lm & 2) g1 = sc.leaves[q3.y & ~kPLeaf].geo;
+            if (lm & 4) g2 = sc.leaves[q3.z & ~kPLeaf].geo;
+            if (lm & 8) g3 = sc.leaves[q3.w & ~kPLeaf].geo;
+            if (lm & 1) leaf_gate(sc, sr, sp, pr, q3.x, g0, best_t, best_s);
+            if (lm & 2) leaf_gate(sc, sr, sp, pr, q3.y, g1, best_t, best_s);
+            if (lm & 4) leaf_gate(sc, sr, sp, pr, q3.z, g2, best_t, best_s);
+            if (lm & 8) leaf_gate(sc, sr, sp, pr, q3.w, g3, best_t, best_s);
+        }
+    } else
     while (__ballot(lm != 0)) {
         if (lm) {
             const uint32_t i = __builtin_ctz(lm);

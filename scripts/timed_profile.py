@@ -14,12 +14,12 @@ import argparse
 import csv
 import json
 
-BOUNCE = "bounce_kernel<true, 2, false>"
+BOUNCE = "bounce_kernel<true, 2, false>"   # <true, 4, false> on trees past the L2 (MIRT_OPT_LEAF_BATCH)
 PRIMARY = "primary_kernel<true, true>"
 
 
 def short(name):
-    for k in (BOUNCE, PRIMARY, "fold_samples_kernel", "mark_deferred_kernel", "render_kernel<true, false>"):
+    for k in (BOUNCE, BOUNCE.replace("<true, 2,", "<true, 4,"), PRIMARY, "fold_samples_kernel", "mark_deferred_kernel", "render_kernel<true, false>"):
         if k in name:
             return k
     return name.split("(")[0][-60:]

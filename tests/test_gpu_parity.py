@@ -897,3 +897,29 @@ def test_bench_launch_plan_displays(gpu, mirt, batch):
     finally:
         for x in rs:
             x.close()
+
+
+@pytest.mark.parametrize("batch", [0, 1])
+def test_leaf_batch_modes_identical(gpu, mirt, golden, small, batch):
+    """The bounce walk with a step's leaf spheres loaded together
+    (MIRT_OPT_LEAF_BATCH 1: bounce_kernel WALK 4, the default on trees past
+    the L2) and without (0) renders every golden depth-5 BVH frame, including
+    the 1M benchmark-sphere frame, byte for byte."""
+    abi = mirt.abi
+    cs = cams(mirt, small)
+    try:
+        n = 0
+        for key in sorted(golden["frames"]):
+            p = parse_frame_key(key)
+            if p["depth"] < 2 or p["mode"] != 1 or not p["use_bvh"]:
+                continue
+            s, b = _scene(mirt, p["kind"], p["n"])
+            gpu.upload(s, b)
+            gpu.set_option(abi.OPT_LEAF_BATCH, batch)
+            assert gpu.get_option(abi.OPT_LEAF_BATCH) == batch
+            img = gpu.render_frame(cs[p["cam"]], p["W"], p["H"], depth=p["depth"], seed=p["seed"])[::p["step"]]
+            assert sha(img) == golden["frames"][key]["sha"], key
+            n += 1
+        assert n >= 8
+    finally:
+        gpu.set_option(abi.OPT_LEAF_BATCH, 2)
