@@ -1086,6 +1086,9 @@ struct AccumShare {
     bool has_fold = false;   // `folded` was recorded at least once
 };
 
+#ifndef MIRT_LEAF_BATCH_DEFAULT
+#define MIRT_LEAF_BATCH_DEFAULT 2
+#endif
 struct mirt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -1143,7 +1146,7 @@ struct mirt_ctx {
     int bounce_blocks = 0;      // wavefront: persistent workgroups (set in mirt_create)
     int bounce_blocks_opt = 0;  // MIRT_OPT_BOUNCE_BLOCKS override (0: occupancy x CUs)
     int quad_drain = 1;         // four-wide bounce walk: finish the drain four lanes per ray
-    int leaf_batch_opt = 2;     // MIRT_OPT_LEAF_BATCH: 0 off, 1 on, 2 auto (leaf_big)
+    int leaf_batch_opt = MIRT_LEAF_BATCH_DEFAULT;  // MIRT_OPT_LEAF_BATCH: 0 off, 1 on, 2 auto (leaf_big)
     bool leaf_big = false;      // the four-wide tree (HNodes + LeafRecs) exceeds the chip's L2
     void* d_queue = nullptr;    // wavefront: {count, head} + bounce records
     size_t queue_cap = 0;

@@ -1030,15 +1030,45 @@ __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay
         h3 = test(s3, e3);
         q3 = make_uint4(s0.w, s1.w, s2.w, s3.w);
     }
-    // 2. passing leaf slots (the node's boxes are dead here): each lane works
-    // through its own list, so the gate code runs max-over-lanes times
-    // instead of once per slot that any lane passes
     uint32_t lm = (uint32_t)(h0 && (q3.x & kPLeaf)) | (uint32_t)(h1 && (q3.y & kPLeaf)) << 1 |
                   (uint32_t)(h2 && (q3.z & kPLeaf)) << 2 | (uint32_t)(h3 && (q3.w & kPLeaf)) << 3;
     h0 = h0 && !(lm & 1);
     h1 = h1 && !(lm & 2);
     h2 = h2 && !(lm & 4);
     h3 = h3 && !(lm & 8);
+    // 2. passing inner slots: nearest next, the others pushed farthest first.
+    // Before the leaf gates, so the slots' keys and flags are dead while the
+    // gates run (the gates' outcome does not depend on the order)
+    const uint32_t n = (uint32_t)h0 + (uint32_t)h1 + (uint32_t)h2 + (uint32_t)h3;
+    if (n == 0) {
+        wide_walk_pop(w, stk);
+    } else if (w.top + n - 1 > (uint32_t)kWideStack) {
+        // the node's whole subtree as a flat DFS segment, its leaf slots included
+        const HAux ax = sc.haux[w.cur];
+        w.cur = ax.flat + 1;
+        w.end = ax.end;
+        lm = 0;
+    } else {
+        // failing slots get +inf keys and passing ones a finite key, so the n
+        // passing slots sort first
+        constexpr float big = 3.0e38f;
+        float k0 = h0 ? fminf(e0, big) : INFINITY, k1 = h1 ? fminf(e1, big) : INFINITY;
+        float k2 = h2 ? fminf(e2, big) : INFINITY, k3 = h3 ? fminf(e3, big) : INFINITY;
+        uint32_t a0 = q3.x, a1 = q3.y, a2 = q3.z, a3 = q3.w;
+        cx(k0, a0, k1, a1);
+        cx(k2, a2, k3, a3);
+        cx(k0, a0, k2, a2);
+        cx(k1, a1, k3, a3);
+        cx(k1, a1, k2, a2);
+        if (n >= 2) stk[(w.top + n - 2) * kWideStride] = a1;
+        if (n >= 3) stk[(w.top + n - 3) * kWideStride] = a2;
+        if (n >= 4) stk[(w.top + n - 4) * kWideStride] = a3;
+        w.top += n - 1;
+        w.cur = a0;
+    }
+    // 3. passing leaf slots (the node's boxes are dead here): each lane works
+    // through its own list, so the gate code runs max-over-lanes times
+    // instead of once per slot that any lane passes
     if constexpr (BATCH && FAST && !COUNT) {
         // every passing leaf's sphere requested at once (one dependent round
         // trip for the step instead of one per leaf), then the gates in slot
@@ -1057,43 +1087,16 @@ __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay
             if (lm & 4) leaf_gate(sc, sr, sp, pr, q3.z, g2, best_t, best_s);
             if (lm & 8) leaf_gate(sc, sr, sp, pr, q3.w, g3, best_t, best_s);
         }
-    } else
-    while (__ballot(lm != 0)) {
-        if (lm) {
-            const uint32_t i = __builtin_ctz(lm);
-            lm &= lm - 1;
-            const uint32_t ref = i == 0 ? q3.x : i == 1 ? q3.y : i == 2 ? q3.z : q3.w;
-            wide_leaf<FAST, COUNT>(sc, sr, sp, pr, ref, best_t, best_s, cnt);
+    } else {
+        while (__ballot(lm != 0)) {
+            if (lm) {
+                const uint32_t i = __builtin_ctz(lm);
+                lm &= lm - 1;
+                const uint32_t ref = i == 0 ? q3.x : i == 1 ? q3.y : i == 2 ? q3.z : q3.w;
+                wide_leaf<FAST, COUNT>(sc, sr, sp, pr, ref, best_t, best_s, cnt);
+            }
         }
     }
-    // 3. passing inner slots: nearest next, the others pushed farthest first
-    const uint32_t n = (uint32_t)h0 + (uint32_t)h1 + (uint32_t)h2 + (uint32_t)h3;
-    if (n == 0) {
-        wide_walk_pop(w, stk);
-        return;
-    }
-    if (w.top + n - 1 > (uint32_t)kWideStack) {
-        const HAux ax = sc.haux[w.cur];
-        w.cur = ax.flat + 1;
-        w.end = ax.end;
-        return;
-    }
-    // failing slots get +inf keys and passing ones a finite key, so the n
-    // passing slots sort first
-    constexpr float big = 3.0e38f;
-    float k0 = h0 ? fminf(e0, big) : INFINITY, k1 = h1 ? fminf(e1, big) : INFINITY;
-    float k2 = h2 ? fminf(e2, big) : INFINITY, k3 = h3 ? fminf(e3, big) : INFINITY;
-    uint32_t a0 = q3.x, a1 = q3.y, a2 = q3.z, a3 = q3.w;
-    cx(k0, a0, k1, a1);
-    cx(k2, a2, k3, a3);
-    cx(k0, a0, k2, a2);
-    cx(k1, a1, k3, a3);
-    cx(k1, a1, k2, a2);
-    if (n >= 2) stk[(w.top + n - 2) * kWideStride] = a1;
-    if (n >= 3) stk[(w.top + n - 3) * kWideStride] = a2;
-    if (n >= 4) stk[(w.top + n - 4) * kWideStride] = a3;
-    w.top += n - 1;
-    w.cur = a0;
 }
 
 // ---------------------------------------------------------------- quad walk
