@@ -462,17 +462,38 @@ __device__ __forceinline__ bool slab_cons(const SlabRay& r, const Prune& p, floa
 }
 
 // Per-ray constants of ray_sphere_intersect: a = d.d, 4a and 2a (hit.c:22-28).
+// MIRT_SPHRAY_LAZY (round 3): recomputed from d at each sphere test (eight
+// VALU) instead of held for the whole walk (four VGPRs fewer in every walk
+// loop: registers, not VALU, limit the walks); the same IEEE expressions, so
+// the same bits; 1/(2a) -- only the estimate's scale -- from v_rcp_f32
+// (1 ulp, well inside sphere_t's 2^-18 margin).
+#ifndef MIRT_SPHRAY_LAZY
+#define MIRT_SPHRAY_LAZY 1
+#endif
 struct SphRay {
     float ox, oy, oz, dx, dy, dz;
-    float a4;     // 4 * a  (hit.c:25: 4 * a * c evaluates (4 * a) * c)
-    float inv2a;  // ~1 / (2a), for the estimate only
-    double a2;    // (double)(2.0f * a)
+#if MIRT_SPHRAY_LAZY
+    __device__ __forceinline__ float a() const { return dot3(dx, dy, dz, dx, dy, dz); }
+    __device__ __forceinline__ float a4() const { return 4.0f * a(); }  // hit.c:25: (4 * a) * c
+    __device__ __forceinline__ float inv2a() const { return __builtin_amdgcn_rcpf(2.0f * a()); }
+    __device__ __forceinline__ double a2() const { return (double)(2.0f * a()); }
+#else
+    float a4_, inv2a_;
+    double a2_;
+    __device__ __forceinline__ float a4() const { return a4_; }
+    __device__ __forceinline__ float inv2a() const { return inv2a_; }
+    __device__ __forceinline__ double a2() const { return a2_; }
+#endif
 };
 
 __device__ __forceinline__ SphRay sph_ray(const Ray& r)
 {
+#if MIRT_SPHRAY_LAZY
+    return {r.ox, r.oy, r.oz, r.dx, r.dy, r.dz};
+#else
     const float a = dot3(r.dx, r.dy, r.dz, r.dx, r.dy, r.dz);
     return {r.ox, r.oy, r.oz, r.dx, r.dy, r.dz, 4.0f * a, 1.0f / (2.0f * a), (double)(2.0f * a)};
+#endif
 }
 
 // hit.c:19-39 without point/normal (computed once for the winner): the t a
@@ -493,17 +514,17 @@ __device__ __forceinline__ float sphere_t(const SphRay& r, float4 s, float best)
     const float ocx = r.ox - s.x, ocy = r.oy - s.y, ocz = r.oz - s.z;
     const float b = 2.0f * dot3(ocx, ocy, ocz, r.dx, r.dy, r.dz);
     const float c = dot3(ocx, ocy, ocz, ocx, ocy, ocz) - s.w * s.w;
-    const float disc = b * b - r.a4 * c;
+    const float disc = b * b - r.a4() * c;
     if (!(disc > 0.0f)) return -1.0f;
     if (FAST) {
         const float sq = __builtin_amdgcn_sqrtf(disc);
-        const float te = (-b - sq) * r.inv2a;
-        const float m = (fabsf(b) + sq) * fabsf(r.inv2a) * 0x1p-18f;
+        const float te = (-b - sq) * r.inv2a();
+        const float m = (fabsf(b) + sq) * fabsf(r.inv2a()) * 0x1p-18f;
         if (te - m > best || te + m <= kEps) return -1.0f;
     }
     // hit.c:28 in double: (-b - sqrt(disc)) / (2a), rounded to float
     const double num = (double)(-b) - __dsqrt_rn((double)disc);
-    const float t = (float)__ddiv_rn(num, r.a2);
+    const float t = (float)__ddiv_rn(num, r.a2());
     return (t > kEps && t <= best) ? t : -1.0f;
 }
 
@@ -534,7 +555,7 @@ __device__ __forceinline__ void lane_step(const DevScene& sc, const SlabRay& sr,
             if (t > 0.0f && (!TIEKEY || t < best_t || nd.sphere > best_s)) {
                 best_t = t;
                 best_s = nd.sphere;
-                if (sc.prune) prune_update(pr, sc, sr.ox, sr.oy, sr.oz, sp.a4, t);
+                if (sc.prune) prune_update(pr, sc, sr.ox, sr.oy, sr.oz, sp.a4(), t);
             }
         }
         next = nd.skip & MIRT_SKIP_MASK;
@@ -597,7 +618,7 @@ __device__ __forceinline__ void closest_bvh(const DevScene& sc, const Ray& ray, 
                         if (t > 0.0f) {
                             best_t = t;
                             best_s = nd.sphere;
-                            if (sc.prune) prune_update(pr, sc, ray.ox, ray.oy, ray.oz, sp.a4, t);
+                            if (sc.prune) prune_update(pr, sc, ray.ox, ray.oy, ray.oz, sp.a4(), t);
                         }
                     }
                 }
@@ -695,7 +716,7 @@ __device__ __forceinline__ void closest_bvh_chunked(const DevScene& sc, const Ra
             const int last = 63 - __builtin_clzll(eq);
             bt = tmin;
             bs = __builtin_amdgcn_readlane(sph, last);
-            if (FAST && sc.prune) prune_update(pr, sc, ray.ox, ray.oy, ray.oz, sp.a4, bt);
+            if (FAST && sc.prune) prune_update(pr, sc, ray.ox, ray.oy, ray.oz, sp.a4(), bt);
         }
         const uint64_t passed_leaves = __ballot(pass && leaf);
         if (COUNT) {  // uniform values: every lane holds the ray's totals
@@ -780,7 +801,7 @@ __device__ __forceinline__ void consider_sphere(const DevScene& sc, const SphRay
     if (t > 0.0f && (t < best_t || si > best_s)) {
         best_t = t;
         best_s = si;
-        if (sc.prune) prune_update(pr, sc, ox, oy, oz, sp.a4, t);
+        if (sc.prune) prune_update(pr, sc, ox, oy, oz, sp.a4(), t);
     }
 }
 
@@ -956,7 +977,7 @@ __device__ __forceinline__ void wide_leaf(const DevScene& sc, const SlabRay& sr,
             if ((t < best_t || si > best_s) && slab_box<FAST>(sr, pr, l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, e)) {
                 best_t = t;
                 best_s = si;
-                if (sc.prune) prune_update(pr, sc, sr.ox, sr.oy, sr.oz, sp.a4, t);
+                if (sc.prune) prune_update(pr, sc, sr.ox, sr.oy, sr.oz, sp.a4(), t);
             }
         }
     }
@@ -976,7 +997,7 @@ __device__ __forceinline__ void leaf_gate(const DevScene& sc, const SlabRay& sr,
         if ((t < best_t || si > best_s) && slab_box<true>(sr, pr, l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, e)) {
             best_t = t;
             best_s = si;
-            if (sc.prune) prune_update(pr, sc, sr.ox, sr.oy, sr.oz, sp.a4, t);
+            if (sc.prune) prune_update(pr, sc, sr.ox, sr.oy, sr.oz, sp.a4(), t);
         }
     }
 }
@@ -1188,7 +1209,7 @@ __device__ __forceinline__ void quad_step(const DevScene& sc, const SlabRay& sr,
     if (cs >= 0 && cand_better(ct, cs, best_t, best_s)) {
         best_t = ct;
         best_s = cs;
-        if (sc.prune) prune_update(pr, sc, sr.ox, sr.oy, sr.oz, sp.a4, ct);
+        if (sc.prune) prune_update(pr, sc, sr.ox, sr.oy, sr.oz, sp.a4(), ct);
     }
     // the passing inner slots: rank by entry (ties by slot), nearest next
     const bool inner = pass && !(q.w & kPLeaf);
