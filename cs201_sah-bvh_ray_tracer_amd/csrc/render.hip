@@ -520,6 +520,15 @@ struct BounceWalk<4> : WideBounceWalk<4> {};
 // over them, the same two after the queue ran dry, start / queue-dry / end
 // time (100 MHz clock), longest chain << 32 | longest walk (in steps)}.
 
+// The RNG key of the pixel a bounce chain belongs to (rng.h: the per-pixel
+// stream of its full-frame index and sample), recomputed where a level is
+// shaded rather than held in two registers for the whole walk.
+__device__ __forceinline__ uint64_t chain_key(const FrameConst& f, uint32_t pixel)
+{
+    const int r = (int)(pixel / (uint32_t)f.width), x = (int)(pixel - (uint32_t)r * (uint32_t)f.width);
+    return pixel_key(f.seed, (uint32_t)(shard_row_to_y(f, r) * f.width + x), row_sample(f, r));
+}
+
 // The shading of one lane whose walk for this level is done (renderer.c:46-77
 // for that level): returns true if the chain goes on (ray re-aimed); else the
 // pixel's colour is folded from the colour stack and stored (if `store`).
@@ -611,7 +620,6 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
     uint32_t pixel = 0, k = 0, base0 = 0;
     int level = 0, best_s = -1;
     float best_t = INFINITY;
-    uint64_t key = 0;
     for (;;) {
         // refill lanes that own no chain (one atomic per wave, tile order
         // kept), from the next segment while the current one is dry
@@ -639,8 +647,6 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                     k = rec.k;
                     base0 = rec.base0;
                     level = 1;
-                    const int r = (int)(pixel / f.width), x = (int)(pixel - r * f.width);
-                    key = pixel_key(f.seed, (uint32_t)(shard_row_to_y(f, r) * f.width + x), row_sample(f, r));
                     w.start(sc);
                     best_t = INFINITY;
                     best_s = -1;
@@ -678,7 +684,8 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                 dg_chain += dg_steps;
                 dg_steps = 0;
             }
-            if (shade_level(sc, f, ray, best_t, best_s, level, k, key, cs, cstride, base0, pixel, out, acc, true)) {
+            if (shade_level(sc, f, ray, best_t, best_s, level, k, chain_key(f, pixel), cs, cstride, base0, pixel, out,
+                            acc, true)) {
                 sr = slab_ray(ray);
                 sp = sph_ray(ray);
                 w.start(sc);
@@ -713,7 +720,6 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
             k = pull(k);
             level = (int)pull((uint32_t)level);
             base0 = pull(base0);
-            key = ((uint64_t)pull((uint32_t)(key >> 32)) << 32) | pull((uint32_t)key);
             best_t = pullf(best_t);
             best_s = (int)pull((uint32_t)best_s);
             pr = Prune{pullf(pr.m), pullf(pr.lim)};
@@ -733,7 +739,7 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                     quad_step<FAST, kWideStride, kWideStack>(sc, sr, sp, pr, qw, qstk, best_t, best_s,
                                                              (lds_uint4*)hcache, hc_n);
                 if (has && qw.cur == kPNone) {
-                    if (shade_level(sc, f, ray, best_t, best_s, level, k, key, qcs, kWideStride, base0, pixel, out,
+                    if (shade_level(sc, f, ray, best_t, best_s, level, k, chain_key(f, pixel), qcs, kWideStride, base0, pixel, out,
                                     acc, (lane & 3) == 0)) {
                         sr = slab_ray(ray);
                         sp = sph_ray(ray);
