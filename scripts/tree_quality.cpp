@@ -361,6 +361,7 @@ float sphere_t(const Ray& r, const mirt_sphere& s)
 struct Stats {
     double visits = 0, gates = 0, rays = 0, pushes = 0;
     double over = 0;  // steps whose pushes would overflow a 20-entry stack (the kernel's kWideStack)
+    double slots = 0;  // live slots of the visited nodes (a visit that loads only those)
     int max_stack = 0;
 };
 
@@ -385,6 +386,7 @@ int walk(const Tree& t, const std::vector<Leaf>& L, const mirt_sphere* sp, const
         st.visits++;
         if (trace) trace->push_back(n);
         const W4& w = t.nodes[n];
+        for (int k = 0; k < w.n; k++) st.slots += w.ref[k] != INT32_MIN;
         std::pair<float, int> in[kMaxWide];
         int m = 0;
         for (int k = 0; k < w.n; k++) {
@@ -749,8 +751,9 @@ int main(int argc, char** argv)
             }
         }
     auto pr = [](const char* name, const Stats& s, size_t nodes) {
-        printf("  %-28s nodes %7zu  rays %8.0f  visits/ray %7.2f  gates/ray %6.2f  pushes/ray %6.2f  max stack %d  overflow/ray %.4f\n",
-               name, nodes, s.rays, s.visits / s.rays, s.gates / s.rays, s.pushes / s.rays, s.max_stack, s.over / s.rays);
+        printf("  %-28s nodes %7zu  rays %8.0f  visits/ray %7.2f  gates/ray %6.2f  pushes/ray %6.2f  max stack %d  overflow/ray %.4f  live slots/visit %.2f\n",
+               name, nodes, s.rays, s.visits / s.rays, s.gates / s.rays, s.pushes / s.rays, s.max_stack, s.over / s.rays,
+               s.slots / s.visits);
     };
     printf("%s %d spheres, %zu live leaves, %d flat nodes, pixel stride %d, SAH bins %d, leaf max %d\n",
            scene.c_str(), n, leaves.size(), nn, stride, g_bins, g_leaf_max);
