@@ -520,6 +520,10 @@ struct BounceWalk<4> : WideBounceWalk<4> {};
 // over them, the same two after the queue ran dry, start / queue-dry / end
 // time (100 MHz clock), longest chain << 32 | longest walk (in steps)}.
 
+// Dynamic LDS of a bounce launch: the colour stack's rows for a frame of
+// `depth` levels (bounce levels 1 .. depth - 1 store a colour each).
+inline size_t bounce_lds_bytes(int depth) { return sizeof(uint32_t) * 256 * (size_t)std::max(depth - 1, 1); }
+
 // The RNG key of the pixel a bounce chain belongs to (rng.h: the per-pixel
 // stream of its full-frame index and sample), recomputed where a level is
 // shaded rather than held in two registers for the whole walk.
@@ -587,7 +591,11 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
     uint32_t dg_steps = 0, dg_chain = 0, dg_walk_max = 0, dg_chain_max = 0;
     constexpr bool LANE4 = WALK == 2 || WALK == 4;  // four-wide, one ray per lane
     constexpr int cstride = 256;
-    __shared__ uint32_t cstack[kMaxDepth * cstride];
+    // the colour stack: one row per bounce level that can store a colour
+    // (levels 1 .. depth - 1), sized at launch (bounce_lds_bytes): a depth-5
+    // frame needs 4 of kMaxDepth's 8 rows, and the 4 KB it leaves free per
+    // workgroup is room for the co-running frames' workgroups
+    extern __shared__ uint32_t cstack[];
     __shared__ uint32_t wstack[LANE4 ? kWideStack * kWideStride : 1];
     __shared__ uint32_t qsrc[LANE4 ? 4 * 16 : 1];  // quad drain: source lane of each quad, per wave
     // the tree's top levels (the first kHCache HNodes, breadth-first) in LDS:
@@ -1639,6 +1647,7 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
                                : tiles;
         const int pblocks = (ptiles + 3) / 4 + dfr.blocks;
         const int bblocks = c->bounce_blocks_opt ? c->bounce_blocks_opt : c->bounce_blocks;
+        const size_t blds = bounce_lds_bytes(f.depth);
         if (c->fast_slab && sc.ordered)
             primary_kernel<true, true><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
         else if (c->fast_slab)
@@ -1648,17 +1657,17 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ph1[ps], s));
         if (d_bdiag && sc.wide)
-            bounce_kernel<true, 2, true><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, d_bdiag);
+            bounce_kernel<true, 2, true><<<bblocks, 256, blds, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, d_bdiag);
         else if (d_bdiag)
-            bounce_kernel<true, 0, true><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, d_bdiag);
+            bounce_kernel<true, 0, true><<<bblocks, 256, blds, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, d_bdiag);
         else if (sc.wide && leaf_batch(c))
-            bounce_kernel<true, 4><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain);
+            bounce_kernel<true, 4><<<bblocks, 256, blds, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain);
         else if (sc.wide)
-            bounce_kernel<true, 2><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain);
+            bounce_kernel<true, 2><<<bblocks, 256, blds, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain);
         else if (c->fast_slab)
-            bounce_kernel<true, 0><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain);
+            bounce_kernel<true, 0><<<bblocks, 256, blds, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain);
         else
-            bounce_kernel<false, 0><<<bblocks, 256, 0, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain);
+            bounce_kernel<false, 0><<<bblocks, 256, blds, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ph2[ps], s));
         if (int rc = fold()) return rc;
@@ -1746,7 +1755,8 @@ int mirt_create(int device, mirt_ctx** out)
         int cus = 0, per_cu = 0;
         e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
         if (e == hipSuccess)
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bounce_kernel<true, 2>, 256, 0);
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bounce_kernel<true, 2>, 256,
+                                                             bounce_lds_bytes(kMaxDepth));
         c->bounce_blocks = std::max(1, cus) * std::max(1, per_cu);
         c->num_cus = cus;
     }
