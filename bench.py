@@ -99,6 +99,18 @@ DEFAULT_BATCH = {1: 1, 2: 1, 4: 4, 8: 4}
 # a gather-sized copy on a fifth stream 11.9 Grays/s, 8 queues 13.2; 8 ctxs on
 # 8 queues without the copy 15.2; profiles/r03f/)
 PIPELINE_MULTI, HW_QUEUES_MULTI = 8, 16
+# the last TAIL_GRID launches of a timed burst run their bounce pass on the
+# full persistent grid: with frames in flight every launch takes 1.5
+# workgroups per CU so the frames share the chip, but the burst's last frame
+# drains alone at that grid (profiles/r03zf: 0.89 ms of the 16 ms region with
+# one 384-workgroup launch on the chip). An application that renders a known
+# sequence (the K timed steps) can give the launches that nothing will follow
+# the whole chip; an interactive loop cannot know its last frame. Measured at
+# K = 20 (profiles/r03zg/summary.txt, rounds interleaved): 1 / 2 last launches
+# 1080p/10k -0.2% / +1.1%, 1080p/100k +1.7% / 0%, 4K/10k +3.1% / +2.6%,
+# 4K/1M 0% / 0%: within the rounds' spread at the metric's config, so the
+# bench keeps one launch plan for the whole burst (0).
+TAIL_GRID = 0
 KERNEL = "bounce_kernel<true, 2, false>"   # dominant kernel of the default (wavefront, four-wide) schedule
 # the PMC-derived bound of the timed launch shape, per workload
 # (scripts/pmc_bench.sh over this script's own command + scripts/pmc_summary.py)
@@ -385,6 +397,9 @@ def main():
                          "flight; weak: N frames per step at N GPUs (reported beside it as value_weak)")
     ap.add_argument("--batch", type=int, default=0,
                     help="steps' frames per launch (frames in flight inside a launch; 0 = DEFAULT_BATCH[N])")
+    ap.add_argument("--tail-grid", type=int, default=TAIL_GRID,
+                    help="the last N launches of a timed burst take the full persistent bounce grid (nothing "
+                         "later will share the chip); 0 = every launch at --bounce-blocks")
     ap.add_argument("--accumulate", action="store_true",
                     help="time the still-camera accumulating display loop (shared accumulation buffer) instead "
                          "of fresh frames")
@@ -500,20 +515,34 @@ def main():
             f += n
         return out
 
-    def launcher(s, depth):
+    def launcher(s, depth, tail=()):
+        """The launch of frames f0 .. f0 + n - 1 on the next context; a launch
+        whose first frame is in `tail` (the burst's last launches) runs its
+        bounce pass on the full persistent grid instead of `blocks`."""
         def run(f0, n):
             acc = args.accumulate and f0 > 0
+            x = s.rs[s.k % len(s.rs)] if f0 in tail else None
+            if x is not None:
+                x.set_option(mirt.abi.OPT_BOUNCE_BLOCKS, 0)
             s.render_local(cam, s.desc(depth=depth, seed=SEED, sample=f0 * SPP, accumulate=acc,
                                        frames=f0 * SPP + 1 if acc else 1, jitter=JITTER, samples=n * SPP))
+            if x is not None:
+                x.set_option(mirt.abi.OPT_BOUNCE_BLOCKS, blocks)
             if world > 1:
                 s.gather(every=SPP)       # every frame's display; N = 1: the slabs are the frames
         return run
 
-    run = launcher(sf, DEPTH)
+    def tail_of(pl):
+        """first frames of the last --tail-grid launches of a pipelined plan"""
+        if len(rs) < 2 or not blocks or args.tail_grid <= 0:
+            return ()
+        return {f0 for f0, _ in pl[-args.tail_grid:]}
+
     warm = plan(0, args.warmup, per_launch)
+    timed_plan = plan(args.warmup * fps, args.steps, per_launch)
+    run = launcher(sf, DEPTH, tail_of(timed_plan))
     for p in warm:
         run(*p)
-    timed_plan = plan(args.warmup * fps, args.steps, per_launch)
     elapsed = timed(world, timed_plan, run)
 
     # the two passes of every timed launch, from the HIP events the library
@@ -529,10 +558,11 @@ def main():
     primary_ms, bounce_ms = (float(v) for v in np.mean(np.array(timed_phases), axis=0))
 
     # depth 1 alongside (camera rays and their shading only)
-    run1 = launcher(sf, 1)
+    plan_d1 = plan(0, args.steps, per_launch)
+    run1 = launcher(sf, 1, tail_of(plan_d1))
     for p in plan(0, 2, per_launch):
         run1(*p)
-    elapsed_d1 = timed(world, plan(0, args.steps, per_launch), run1)
+    elapsed_d1 = timed(world, plan_d1, run1)
 
     # the other scaling mode at N > 1 (same contexts, its own slabs)
     elapsed_other, fps_other = None, None
@@ -542,10 +572,11 @@ def main():
         per_other = fps_other * batch if SPP == 1 or args.accumulate else 1
         sf2 = shard.ShardedFrame(r, W, H, ROW_BLOCK, samples=SPP * per_other, renderers=rs,
                                  share_accum=args.accumulate, accum=SPP > 1 or args.accumulate)
-        run2 = launcher(sf2, DEPTH)
+        plan2 = plan(args.warmup * fps_other, args.steps, per_other)
+        run2 = launcher(sf2, DEPTH, tail_of(plan2))
         for p in plan(0, args.warmup, per_other):
             run2(*p)
-        elapsed_other = timed(world, plan(args.warmup * fps_other, args.steps, per_other), run2)
+        elapsed_other = timed(world, plan2, run2)
         fps = fps_main
 
     # the same launch alone, one context, serial (untimed loop: each launch
@@ -621,7 +652,7 @@ def main():
                        "width": W, "height": H, "spheres": NSPH, "scene": KIND, "max_depth": DEPTH, "spp": SPP,
                        "jitter": JITTER,
                        "frames_per_step": fps, "frames_per_launch": per_launch, "launches": len(timed_plan),
-                       "pipeline": len(rs), "bounce_blocks": blocks, "bvh_nodes": len(bvh),
+                       "pipeline": len(rs), "bounce_blocks": blocks, "tail_grid": len(tail_of(timed_plan)), "bvh_nodes": len(bvh),
                        "row_block": ROW_BLOCK, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                        "step": (f"{fps} frame(s) of the still-camera display loop (main.c:379-408), ctxs sharing "
                                 "one accumulation buffer (mirt_ctx_share_accum)" if args.accumulate else
