@@ -9,10 +9,14 @@ tile edges (W, H not multiples of the 8x8 tile) and over both scene
 generators, so that the camera packets, the deferred zero-component rays, the
 bounce queue and the four-wide walk are all exercised off the tested views.
 """
+import os
+
 import numpy as np
 import pytest
 
-CASES = 16
+# MIRT_FUZZ_CASES raises the count for a longer soak (profiles/r03zh: 512 per
+# scene kind); the default keeps the suite to seconds
+CASES = int(os.environ.get("MIRT_FUZZ_CASES", "16"))
 
 
 def _cameras(mirt, rng):
