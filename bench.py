@@ -523,11 +523,12 @@ def main():
             acc = args.accumulate and f0 > 0
             x = s.rs[s.k % len(s.rs)] if f0 in tail else None
             if x is not None:
+                keep = x.get_option(mirt.abi.OPT_BOUNCE_BLOCKS)
                 x.set_option(mirt.abi.OPT_BOUNCE_BLOCKS, 0)
             s.render_local(cam, s.desc(depth=depth, seed=SEED, sample=f0 * SPP, accumulate=acc,
                                        frames=f0 * SPP + 1 if acc else 1, jitter=JITTER, samples=n * SPP))
             if x is not None:
-                x.set_option(mirt.abi.OPT_BOUNCE_BLOCKS, blocks)
+                x.set_option(mirt.abi.OPT_BOUNCE_BLOCKS, keep)
             if world > 1:
                 s.gather(every=SPP)       # every frame's display; N = 1: the slabs are the frames
         return run
