@@ -978,6 +978,65 @@ __global__ __launch_bounds__(256) void intersect_kernel(DevScene sc, const mirt_
     if (alive) store_hit(ray, t, s, sc, &out[i]);
 }
 
+// ray_bvh_intersect (hit.c:91-109) for a batch too small to fill the chip
+// one ray per lane (benchmark.c's 10,000 rays): one ray per QUAD of lanes,
+// lane j testing slot j of every four-wide node (quad_step, the bounce
+// kernel's drain walk), so each ray's dependent chain of node fetches is
+// walked by four lanes and the batch occupies four times the lanes. The
+// tree's top HNodes are staged in LDS; rays with a zero/tiny direction
+// component take the exact wave-cooperative walk afterwards (closest_hit).
+// ANY: the hit flag (benchmark.c:239-241), else the hit record.
+constexpr int kQuadBatchThreads = 64;  // 16 rays per workgroup: a small batch spreads over the CUs
+template <bool ANY>
+__global__ __launch_bounds__(kQuadBatchThreads) void intersect_quad_kernel(DevScene sc, const mirt_ray* __restrict__ rays,
+                                                                          int n, mirt_hit* __restrict__ out,
+                                                                          int32_t* __restrict__ flags)
+{
+    constexpr int kRays = kQuadBatchThreads / 4;
+    __shared__ uint32_t qstack[kWideStack * kRays];
+    __shared__ uint4 hcache[4 * kHCache];
+    const uint32_t hc_n = min((uint32_t)kHCache, sc.num_hnodes);
+    for (uint32_t i = threadIdx.x; i < 4 * hc_n; i += blockDim.x) hcache[i] = ((const uint4*)sc.hnodes)[i];
+    __syncthreads();
+    const int q = (int)(threadIdx.x >> 2);
+    const int i = (int)blockIdx.x * kRays + q;
+    const bool alive = i < n;
+    const mirt_ray& rr = rays[alive ? i : 0];
+    const Ray ray{rr.origin.x, rr.origin.y, rr.origin.z, rr.direction.x, rr.direction.y, rr.direction.z};
+    const SlabRay sr = slab_ray(ray);
+    const SphRay sp = sph_ray(ray);
+    Prune pr = prune_off();
+    const bool gen = alive && sr.generic;
+    float best_t = INFINITY;
+    int best_s = -1;
+    QuadWalk qw{alive && !gen ? sc.wide_root : kPNone, 0u, 0u};
+    while (__ballot(qw.cur != kPNone)) {
+        if (qw.cur != kPNone)
+            quad_step<true, kRays, kWideStack>(sc, sr, sp, pr, qw, qstack + q, best_t, best_s, (lds_uint4*)hcache, hc_n);
+    }
+    uint64_t gm = __ballot(gen && (threadIdx.x & 3) == 0);
+    while (gm) {  // zero-component rays: the exact chunked walk, one ray per wave pass
+        const int l = __builtin_ctzll(gm);
+        gm &= gm - 1;
+        const Ray g{readlane_f(ray.ox, l), readlane_f(ray.oy, l), readlane_f(ray.oz, l),
+                    readlane_f(ray.dx, l), readlane_f(ray.dy, l), readlane_f(ray.dz, l)};
+        float t;
+        int s2;
+        Counters c2{0, 0, 0, 0, 0};
+        closest_bvh_chunked<true, false>(sc, g, t, s2, c2);
+        if ((int)(threadIdx.x & 63) >> 2 == l >> 2) {
+            best_t = t;
+            best_s = s2;
+        }
+    }
+    if (alive && (threadIdx.x & 3) == 0) {
+        if (ANY)
+            flags[i] = best_s >= 0 ? 1 : 0;
+        else
+            store_hit(ray, best_t, best_s, sc, &out[i]);
+    }
+}
+
 // element-wise ray_sphere_intersect (hit.c:19-39)
 __global__ void sphere_pairs_kernel(const mirt_ray* __restrict__ rays, const mirt_sphere* __restrict__ sph, int n,
                                     mirt_hit* __restrict__ out)
@@ -1160,6 +1219,9 @@ struct AccumShare {
     bool has_fold = false;   // `folded` was recorded at least once
 };
 
+#ifndef MIRT_QUAD_BATCH_DEFAULT
+#define MIRT_QUAD_BATCH_DEFAULT 1
+#endif
 #ifndef MIRT_LEAF_BATCH_DEFAULT
 #define MIRT_LEAF_BATCH_DEFAULT 2
 #endif
@@ -1220,6 +1282,7 @@ struct mirt_ctx {
     int bounce_blocks = 0;      // wavefront: persistent workgroups (set in mirt_create)
     int bounce_blocks_opt = 0;  // MIRT_OPT_BOUNCE_BLOCKS override (0: occupancy x CUs)
     int quad_drain = 1;         // four-wide bounce walk: finish the drain four lanes per ray
+    int quad_batch = MIRT_QUAD_BATCH_DEFAULT;  // small BVH batches one ray per quad (intersect_quad_kernel)
     int leaf_batch_opt = MIRT_LEAF_BATCH_DEFAULT;  // MIRT_OPT_LEAF_BATCH: 0 off, 1 on, 2 auto (leaf_big)
     bool leaf_big = false;      // the four-wide tree (HNodes + LeafRecs) exceeds the chip's L2
     void* d_queue = nullptr;    // wavefront: {count, head} + bounce records
@@ -1752,6 +1815,15 @@ int batch_threads(const mirt_ctx* c, int n)
     return n < 256 * 4 * std::max(1, c->num_cus) ? 64 : 256;
 }
 
+// intersect_quad_kernel for a BVH batch: the four-wide tree, the fast slab
+// filter, and fewer rays than give every CU four waves of one ray per lane
+// (MIRT_OPT_QUAD_BATCH 0 turns it off)
+bool quad_batch(const mirt_ctx* c, int n)
+{
+    const DevScene sc = dev_scene(c);
+    return c->quad_batch && c->fast_slab && sc.wide && n <= 64 * 4 * std::max(1, c->num_cus);
+}
+
 // brute_chunk_kernel over the rays in c->d_in: enough sphere chunks that the
 // grid has ~8 workgroups per CU whatever the ray count.
 int launch_brute(mirt_ctx* c, int n)
@@ -2239,6 +2311,10 @@ int mirt_intersect_rays(mirt_ctx* c, const mirt_ray* rays, int n, int use_bvh, m
         if (rc) return rc;
         brute_finish_kernel<<<(n + 255) / 256, 256, 0, c->stream>>>(dev_scene(c), (const mirt_ray*)c->d_in, n,
                                                                     c->d_keys, (mirt_hit*)c->d_res);
+    } else if (quad_batch(c, n)) {
+        intersect_quad_kernel<false><<<(n + kQuadBatchThreads / 4 - 1) / (kQuadBatchThreads / 4), kQuadBatchThreads, 0,
+                                        c->stream>>>(dev_scene(c), (const mirt_ray*)c->d_in, n, (mirt_hit*)c->d_res,
+                                                     nullptr);
     } else if (c->fast_slab) {
         intersect_kernel<true><<<(n + bt - 1) / bt, bt, 0, c->stream>>>(dev_scene(c), (const mirt_ray*)c->d_in, n,
                                                                       use_bvh, (mirt_hit*)c->d_res);
@@ -2276,6 +2352,10 @@ int mirt_any_hit_rays(mirt_ctx* c, const mirt_ray* rays, int n, int use_bvh, int
         rc = launch_brute(c, n);
         if (rc) return rc;
         keys_to_flags_kernel<<<(n + 255) / 256, 256, 0, c->stream>>>(c->d_keys, n, (int32_t*)c->d_res);
+    } else if (quad_batch(c, n)) {
+        intersect_quad_kernel<true><<<(n + kQuadBatchThreads / 4 - 1) / (kQuadBatchThreads / 4), kQuadBatchThreads, 0,
+                                       c->stream>>>(dev_scene(c), (const mirt_ray*)c->d_in, n, nullptr,
+                                                    (int32_t*)c->d_res);
     } else if (c->fast_slab) {
         bvh_any_kernel<true><<<(n + bt - 1) / bt, bt, 0, c->stream>>>(dev_scene(c), (const mirt_ray*)c->d_in, n,
                                                                     (int32_t*)c->d_res);
@@ -2471,6 +2551,9 @@ int mirt_set_option(mirt_ctx* c, int option, int value)
     case MIRT_OPT_QUAD_DRAIN:
         c->quad_drain = value != 0;
         return MIRT_OK;
+    case MIRT_OPT_QUAD_BATCH:
+        c->quad_batch = value != 0;
+        return MIRT_OK;
     case MIRT_OPT_LEAF_BATCH:
         if (value < 0 || value > 2) break;
         c->leaf_batch_opt = value;
@@ -2498,6 +2581,7 @@ int mirt_get_option(mirt_ctx* c, int option)
     if (option == MIRT_OPT_ORDERED) return c->ordered;
     if (option == MIRT_OPT_BOUNCE_BLOCKS) return c->bounce_blocks_opt;
     if (option == MIRT_OPT_QUAD_DRAIN) return c->quad_drain;
+    if (option == MIRT_OPT_QUAD_BATCH) return c->quad_batch;
     if (option == MIRT_OPT_LEAF_BATCH) return leaf_batch(c) ? 1 : 0;  // in effect for the uploaded scene
     set_error("mirt_get_option: bad option %d", option);
     return MIRT_E_INVALID;

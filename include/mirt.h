@@ -393,10 +393,13 @@ enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3,
                                        keeping frames in flight, ~1.5 per CU (384 on MI355X) */
        MIRT_OPT_QUAD_DRAIN = 11,    /* four-wide bounce walk: 1 (default) = once the queue is dry
                                        and <= 16 lanes of a wave are busy, finish them as quads */
-       MIRT_OPT_LEAF_BATCH = 14     /* four-wide bounce walk: load a step's passing leaf spheres
+       MIRT_OPT_LEAF_BATCH = 14,    /* four-wide bounce walk: load a step's passing leaf spheres
                                        together: 0 never, 1 always, 2 (default) when the tree's
                                        four-wide layout exceeds the chip's 32 MiB of L2;
-                                       mirt_get_option reads back 0/1: in effect for the scene) */ };
+                                       mirt_get_option reads back 0/1: in effect for the scene) */
+       MIRT_OPT_QUAD_BATCH = 15     /* mirt_intersect_rays / mirt_any_hit_rays with the BVH: 1
+                                       (default) = a batch too small to fill the chip one ray per
+                                       lane walks one ray per four lanes (benchmark.c's 10k rays) */ };
 /* Traversal ids keep their first-release values (mirt 0.1: TILE 0, WAVEFRONT 5);
    the retired ids 1-4 (per-lane / chunked / DFS-only schedules of mirt 0.1) and
    the retired option ids 8, 10, 12, 13 return MIRT_E_INVALID. */
