@@ -24,3 +24,5 @@ for wl in 1080p_100k 4k_10k 4k_1m_4spp; do
   step bench_$wl 600 python bench.py --no-cpu --no-host --steps 20 --warmup 5 --workload $wl
 done
 echo done
+step bench_mode 900 python -u scripts/bench_mode_published.py --out "$OUT/r03_bench_mode"
+echo done-all
