@@ -829,9 +829,6 @@ __device__ __forceinline__ void store_hit(const Ray& ray, float t, int s, const 
 // strict `<` does. Any-hit flags are keys != ~0: every sphere is still
 // tested, as benchmark.c:190-199 does (an early exit measured slower: the
 // per-sphere vote costs more than the rare hit saves).
-#ifndef MIRT_BRUTE_PACKED
-#define MIRT_BRUTE_PACKED 1
-#endif
 template <bool FAST>
 __global__ __launch_bounds__(256) void brute_chunk_kernel(DevScene sc, const mirt_ray* __restrict__ rays, int n,
                                                           int chunk, unsigned long long* __restrict__ keys)
@@ -846,62 +843,7 @@ __global__ __launch_bounds__(256) void brute_chunk_kernel(DevScene sc, const mir
     float best_t = INFINITY;
     int best_s = -1;
     if (FAST && MIRT_BRUTE_PACKED && s0 < s1 && __ballot(active)) {
-        // eight spheres per iteration, two per instruction (packed fp32:
-        // v_pk_mul/v_pk_add, the same IEEE roundings as hit.c:22-26's scalar
-        // expressions, no contraction): the discriminants decide nearly every
-        // pair at once, and only a batch with some disc > 0 walks its spheres
-        // through sphere_t (which recomputes that disc) in array order
-        typedef float f2 __attribute__((ext_vector_type(2)));
-        const f2 ox = sp.ox, oy = sp.oy, oz = sp.oz, dx = sp.dx, dy = sp.dy, dz = sp.dz;
-        const f2 a4 = sp.a4();
-        auto disc2 = [&](const float4& p, const float4& q) {
-            const f2 ocx = ox - f2{p.x, q.x}, ocy = oy - f2{p.y, q.y}, ocz = oz - f2{p.z, q.z};
-            const f2 r = f2{p.w, q.w};
-            const f2 b = 2.0f * ((ocx * dx + ocy * dy) + ocz * dz);
-            const f2 c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - r * r;
-            return b * b - a4 * c;
-        };
-        int k = s0;
-        // one base pointer per batch, constant offsets: two s_load_dwordx16;
-        // the next batch is requested before this one is tested
-        auto batch = [&](int k0, float4* g) {
-            const cf32_t* p = (const cf32_t*)sc.geo + 4 * k0;
-#pragma unroll
-            for (int j = 0; j < 8; j++) g[j] = make_float4(p[4 * j], p[4 * j + 1], p[4 * j + 2], p[4 * j + 3]);
-        };
-        float4 g[8], gn[8];
-        if (k + 8 <= s1) batch(k, g);
-        for (; k + 8 <= s1; k += 8) {
-            if (k + 16 <= s1) batch(k + 8, gn);
-            if (active) {
-                const f2 d0 = disc2(g[0], g[1]), d1 = disc2(g[2], g[3]), d2 = disc2(g[4], g[5]), d3 = disc2(g[6], g[7]);
-                const f2 m01 = __builtin_elementwise_max(d0, d1), m23 = __builtin_elementwise_max(d2, d3);
-                const f2 m = __builtin_elementwise_max(m01, m23);
-                // NaN discs (the padding sentinel never enters here) compare false either way
-                if (m.x > 0.0f || m.y > 0.0f || !(m.x == m.x) || !(m.y == m.y)) {
-#pragma unroll
-                    for (int j = 0; j < 8; j++) {
-                        const float t = sphere_t<FAST>(sp, g[j], best_t);
-                        if (t > 0.0f && t < best_t) {
-                            best_t = t;
-                            best_s = k + j;
-                        }
-                    }
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < 8; j++) g[j] = gn[j];
-        }
-        for (; k < s1; k++) {
-            const float4 g = load_geo_uniform(sc.geo, k);
-            if (active) {
-                const float t = sphere_t<FAST>(sp, g, best_t);
-                if (t > 0.0f && t < best_t) {
-                    best_t = t;
-                    best_s = k;
-                }
-            }
-        }
+        brute_range_packed(sc, sp, active, s0, s1, best_t, best_s);
     } else if (s0 < s1 && __ballot(active)) {
         float4 g = load_geo_uniform(sc.geo, s0);
         for (int k = s0; k < s1; k++) {
