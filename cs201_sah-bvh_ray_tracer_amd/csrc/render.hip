@@ -413,6 +413,10 @@ __global__ __launch_bounds__(256) MIRT_PRIMARY_ATTR void primary_kernel(DevScene
     if (alive) {
         if (s < 0) {
             store_pixel(f, out, acc, i, sky_rgba(ray.dy));      // renderer.c:65-70
+        } else if (f.depth < 2) {
+            // depth 1: the bounce would be traced with depth 0 and return
+            // black (renderer.c:23-24), so the pixel is base + 0.5 * black
+            store_pixel(f, out, acc, i, blend_rgba(sc.color[s], 255u << 24));
         } else {
             // renderer.c:49-55: base colour, then the bounce (depth >= 2 here)
             const float4 g = sc.geo[s];
@@ -1161,6 +1165,9 @@ struct AccumShare {
     bool has_fold = false;   // `folded` was recorded at least once
 };
 
+#ifndef MIRT_PRIMARY_DEPTH1
+#define MIRT_PRIMARY_DEPTH1 1
+#endif
 #ifndef MIRT_QUAD_BATCH_DEFAULT
 #define MIRT_QUAD_BATCH_DEFAULT 1
 #endif
@@ -1225,6 +1232,7 @@ struct mirt_ctx {
     int bounce_blocks_opt = 0;  // MIRT_OPT_BOUNCE_BLOCKS override (0: occupancy x CUs)
     int quad_drain = 1;         // four-wide bounce walk: finish the drain four lanes per ray
     int quad_batch = MIRT_QUAD_BATCH_DEFAULT;  // small BVH batches one ray per quad (intersect_quad_kernel)
+    int primary_depth1 = MIRT_PRIMARY_DEPTH1;  // depth-1 frames through the camera-packet kernel alone
     int leaf_batch_opt = MIRT_LEAF_BATCH_DEFAULT;  // MIRT_OPT_LEAF_BATCH: 0 off, 1 on, 2 auto (leaf_big)
     bool leaf_big = false;      // the four-wide tree (HNodes + LeafRecs) exceeds the chip's L2
     void* d_queue = nullptr;    // wavefront: {count, head} + bounce records
@@ -1675,7 +1683,11 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
         return MIRT_OK;
     };
     const bool wavefront = c->trav == kTravWavefront && f.use_bvh && f.depth >= 2 && !d_counts;
-    const int dbw = wavefront ? 4 : bw;  // the wavefront kernels use 256-thread workgroups
+    // depth 1 (camera rays and their shading only): the camera-packet kernel
+    // alone, at its 8 waves per SIMD, where the tree admits the ordered walk
+    const bool primary_only = c->trav == kTravWavefront && f.use_bvh && f.depth == 1 && !d_counts && c->fast_slab &&
+                              c->primary_depth1 && dev_scene(c).ordered;
+    const int dbw = wavefront || primary_only ? 4 : bw;  // the wavefront kernels use 256-thread workgroups
     Deferred dfr{nullptr, nullptr, 0};
     c->phases_valid = wavefront;
     const uint32_t ps = c->ph_next;
@@ -1697,6 +1709,21 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
         // camera; a longer list is strided over the same waves
         const size_t want = std::min(pixels, (size_t)(f.width + f.num_rows + 64));
         dfr = Deferred{c->d_defer + 1, c->d_defer, (int)((want + dbw - 1) / dbw)};
+    }
+    if (primary_only) {
+        // no bounce records: the queue is never written (its control words
+        // are read only by a bounce pass)
+        int rc = ensure(&c->d_queue, &c->queue_cap, sizeof(BounceRec) + kQCtlBytes);
+        if (rc) return rc;
+        uint32_t* qctl = (uint32_t*)c->d_queue;
+        BounceRec* queue = (BounceRec*)((char*)c->d_queue + kQCtlBytes);
+        const int ptiles = f.samples >= 4 ? ((f.width + 3) / 4) * ((f.shard_rows + 3) / 4) * ((f.samples + 3) / 4)
+                                          : tiles;
+        primary_kernel<true, true><<<(ptiles + 3) / 4, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
+        HIP_TRY(hipGetLastError());
+        if (int rc2 = fold()) return rc2;
+        if (timed) HIP_TRY(hipEventRecord(c->ev1, s));
+        return MIRT_OK;
     }
     if (wavefront) {
         const size_t pixels = (size_t)f.num_rows * f.width;
