@@ -266,10 +266,14 @@ def free_port():
         return s.getsockname()[1]
 
 
-def spawn_ranks(n):
+def spawn_ranks(n, deadline_s):
     """Start n copies of this script as ranks 0..n-1 (the torchrun contract's
     environment) and wait; a failing rank ends the others. Runs before any
-    GPU call in this process."""
+    GPU call in this process (the ranks are fresh processes, never a re-exec).
+    A job still running after `deadline_s` seconds (a rank stuck in RCCL init
+    or a gather) is ended: every rank is terminated (killed 5 s later if it
+    ignores that), the stuck ranks are named on stderr and the parent exits
+    124, so the driver records a failure instead of waiting out its limit."""
     port = free_port()
     procs = []
     for r in range(n):
@@ -278,6 +282,7 @@ def spawn_ranks(n):
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
     rc = 0
     live = list(procs)
+    t_end = time.monotonic() + deadline_s
     while live:
         for p in list(live):
             code = p.poll()
@@ -288,8 +293,29 @@ def spawn_ranks(n):
                 rc = code if code > 0 else 128 - code
                 for q in live:
                     q.terminate()
+        if live and time.monotonic() > t_end:
+            stuck = [procs.index(p) for p in live]
+            print(f"bench.py: ranks {stuck} still running after the {deadline_s:.0f} s deadline "
+                  "(--rank-timeout); terminating the job", file=sys.stderr, flush=True)
+            for q in live:
+                q.terminate()
+            t_kill = time.monotonic() + 5.0
+            for q in live:
+                try:
+                    q.wait(timeout=max(0.1, t_kill - time.monotonic()))
+                except subprocess.TimeoutExpired:
+                    q.kill()
+                    q.wait()
+            return 124
         time.sleep(0.05)
     return rc
+
+
+def pg_timeout(args):
+    """The process group's timeout: a collective (or the rendezvous) that
+    waits longer raises in the rank instead of hanging it."""
+    import datetime
+    return datetime.timedelta(seconds=max(10.0, args.rank_timeout - 30.0))
 
 
 def timed(world, launches, body):
@@ -312,9 +338,12 @@ def timed(world, launches, body):
 
 def dry_main(args, world, rank):
     """CPU plumbing check: synthetic slabs through the shard geometry, the
-    gather and the timing of the GPU path (gloo)."""
+    gather and the timing of the GPU path (gloo). MIRT_BENCH_DRY_HANG=r makes
+    rank r ("all": every rank) sleep before joining (the deadline tests)."""
+    if os.environ.get("MIRT_BENCH_DRY_HANG") in (str(rank), "all"):
+        time.sleep(3600)
     if world > 1:
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo", timeout=pg_timeout(args))
     fd = mirt.frame_desc(W, H, depth=DEPTH, row_block=ROW_BLOCK, shard=rank, num_shards=world)
     rows = mirt.shard_rows(fd)
     slab = torch.zeros((shard.slab_rows(H, ROW_BLOCK, world), W), dtype=torch.int32)
@@ -404,6 +433,9 @@ def main():
                     help="time the still-camera accumulating display loop (shared accumulation buffer) instead "
                          "of fresh frames")
     ap.add_argument("--dry", action="store_true", help="CPU plumbing check over gloo (no GPU, no measurement)")
+    ap.add_argument("--rank-timeout", type=float, default=420.0,
+                    help="N > 1 started by this script: seconds before a still-running job is terminated (exit "
+                         "124); each rank's process group times out 30 s earlier")
     ap.add_argument("--opt", action="append", default=[],
                     help="OPTION=VALUE (mirt_set_option on every context; A/B of schedule options), repeatable")
     args = ap.parse_args()
@@ -412,7 +444,7 @@ def main():
     W, H, NSPH, KIND, SPP, JITTER = wl["W"], wl["H"], wl["NSPH"], wl["KIND"], wl["SPP"], wl["JITTER"]
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        return spawn_ranks(args.gpus)
+        return spawn_ranks(args.gpus, args.rank_timeout)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -445,9 +477,9 @@ def main():
     if world > 1:
         torch.cuda.set_device(dev)
         if rehearse:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=pg_timeout(args))
         else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=pg_timeout(args))
     else:
         torch.cuda.set_device(0)
 

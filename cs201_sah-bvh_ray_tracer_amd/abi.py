@@ -172,9 +172,23 @@ SIGNATURES = [
     ("mirt_ray_sphere_intersect", HitRecord, [Ray, P]),
     ("mirt_ray_aabb_intersect", I, [Ray, Aabb]),
     ("mirt_ray_bvh_intersect", HitRecord, [Ray, P]),
+    # include/mirt_multi.h: one frame loop over several GPUs (RCCL gather)
+    ("mirt_multi_create", I, [P, I, I, I, C.POINTER(P)]),
+    ("mirt_multi_destroy", None, [P]),
+    ("mirt_multi_size", I, [P]),
+    ("mirt_multi_lanes", I, [P]),
+    ("mirt_multi_backend", C.c_char_p, [P]),
+    ("mirt_multi_ctx", P, [P, I, I]),
+    ("mirt_multi_set_option", I, [P, I, I]),
+    ("mirt_multi_scene_upload", I, [P, P, I, P]),
+    ("mirt_multi_scene_upload_flat", I, [P, P, I, P, I]),
+    ("mirt_multi_render_frame", I, [P, P, P, P]),
+    ("mirt_multi_render_frame_async", I, [P, P, P, P]),
+    ("mirt_multi_wait", I, [P]),
 ]
 
 OPT_TRAVERSAL, OPT_FAST_SLAB, OPT_BLOCK_WAVES, OPT_DEFER, OPT_BOUNCE_THRESHOLD, OPT_PRUNE, OPT_ORDERED = (
     1, 2, 3, 4, 5, 6, 7)
 OPT_BOUNCE_BLOCKS, OPT_QUAD_DRAIN, OPT_LEAF_BATCH, OPT_QUAD_BATCH = 9, 11, 14, 15
 TRAV_TILE, TRAV_WAVEFRONT = 0, 5
+MULTI_COPY = 1

@@ -29,7 +29,8 @@ struct DropinState {
     const mirt_sphere* spheres = nullptr;
     int num_spheres = -1;
     const mirt_bvh_node* root = nullptr;
-    uint64_t fingerprint = 0;
+    uint64_t fingerprint = 0;       // scene_fingerprint at bind (sphere samples from that call's arguments)
+    uint64_t tree_fp = 0;           // tree_fingerprint at bind (what ray_bvh_intersect re-checks)
     bool bound = false;
     // mirt_dropin_scene: the caller's whole sphere array, for trees built over
     // part of it (benchmark.c:317 builds over [0, n - 1) of n spheres)
@@ -60,13 +61,16 @@ uint64_t fnv(uint64_t h, const void* p, size_t n)
     return h;
 }
 
-// A cheap content fingerprint of a scene, computed on every call: the first
-// 31 nodes of the tree in breadth-first order (bounds, sphere count, and the
-// sphere a non-empty leaf tests) and up to 32 spheres strided over the
-// array. Reading them costs ~60 small loads, against a GPU launch per call.
-uint64_t fingerprint(const mirt_sphere* sp, int ns, const mirt_bvh_node* root)
+// A cheap content fingerprint of a tree, read only through the caller's
+// CURRENT tree pointer: the first 31 nodes in breadth-first order (bounds,
+// sphere count, and the sphere a non-empty leaf tests, read through that
+// leaf's own pointer). Never through a sphere pointer kept from an earlier
+// call: benchmark.c:323-324 frees the previous point's array, and at 10k
+// spheres and up glibc returns it to the kernel (munmap), so a stored pointer
+// may point at unmapped memory. ~60 small loads, against a GPU launch per call.
+uint64_t tree_fingerprint(const mirt_bvh_node* root)
 {
-    uint64_t h = fnv(0xcbf29ce484222325ull, &ns, sizeof ns);
+    uint64_t h = 0xcbf29ce484222325ull;
     const mirt_bvh_node* q[31];
     int head = 0, tail = 0;
     if (root) q[tail++] = root;
@@ -81,6 +85,15 @@ uint64_t fingerprint(const mirt_sphere* sp, int ns, const mirt_bvh_node* root)
         for (const mirt_bvh_node* c : {n->left, n->right})
             if (c && tail < 31) q[tail++] = c;
     }
+    return h;
+}
+
+// The same plus up to 32 spheres strided over the array the caller passes IN
+// THIS CALL (sp, ns are current arguments, so reading them is the caller's
+// own contract, as trace_ray reading spheres[] is).
+uint64_t scene_fingerprint(const mirt_sphere* sp, int ns, const mirt_bvh_node* root)
+{
+    uint64_t h = fnv(tree_fingerprint(root), &ns, sizeof ns);
     if (sp && ns > 0) {
         const int step = ns > 32 ? ns / 32 : 1;
         for (int i = 0; i < ns; i += step) h = fnv(h, &sp[i], sizeof(mirt_sphere));
@@ -91,7 +104,7 @@ uint64_t fingerprint(const mirt_sphere* sp, int ns, const mirt_bvh_node* root)
 
 int bind(DropinState& s, const mirt_sphere* sp, int ns, const mirt_bvh_node* root)
 {
-    const uint64_t fp = fingerprint(sp, ns, root);
+    const uint64_t fp = scene_fingerprint(sp, ns, root);
     if (s.bound && s.spheres == sp && s.num_spheres == ns && s.root == root && s.fingerprint == fp) return MIRT_OK;
     s.bound = false;
     const int rc = mirt_scene_upload(s.ctx, sp, ns, root);
@@ -100,6 +113,7 @@ int bind(DropinState& s, const mirt_sphere* sp, int ns, const mirt_bvh_node* roo
     s.num_spheres = ns;
     s.root = root;
     s.fingerprint = fp;
+    s.tree_fp = tree_fingerprint(root);
     s.bound = true;
     return MIRT_OK;
 }
@@ -296,8 +310,9 @@ mirt_hit_record mirt_ray_bvh_intersect(mirt_ray ray, mirt_bvh_node* node)
             return (int)MIRT_E_INVALID;
         }
         // the scene bound by the last trace_ray (or this call), if the tree
-        // is still the same (pointer and content)
-        if (!(s.bound && s.root == node && s.fingerprint == fingerprint(s.spheres, s.num_spheres, node))) {
+        // is still the same (pointer and content, read through `node` only:
+        // the stored sphere pointer may belong to a freed array)
+        if (!(s.bound && s.root == node && s.tree_fp == tree_fingerprint(node))) {
             // a tree seen without its sphere array: the leaves span it, or
             // the array the caller declared (mirt_dropin_scene) holds them
             const mirt_sphere* lo = nullptr;

@@ -22,4 +22,12 @@ bool frame_desc_valid(const mirt_frame_desc* fd);
 // it. MIRT_OK or MIRT_E_INVALID with the message prefixed by `fn`.
 int validate_flat(const mirt_node* nd, int nn, int num_spheres, int sphere_lo, const char* fn);
 
+// render.hip: the frame of mirt_render_frame up to its D2H copy, enqueued on
+// the ctx's own stream into d_out (fd->samples slabs of the shard; the ctx's
+// own buffer when null) with the ctx's (possibly shared) accumulation buffer;
+// *d_display = the slab holding the display after the last frame.
+int enqueue_frame_device(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, uint32_t* d_out,
+                         uint32_t** d_display, const char* fn);
+int ctx_device(const mirt_ctx* c);
+
 }  // namespace mirt

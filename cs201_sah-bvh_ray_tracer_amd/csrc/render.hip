@@ -2021,13 +2021,15 @@ int mirt_render_frame_device(mirt_ctx* c, const mirt_camera* cam, const mirt_fra
 
 namespace {
 
-// The frame of mirt_render_frame up to and including its D2H copy, enqueued
-// on the ctx's stream.
-int enqueue_host_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, mirt_rgba8* out,
-                       const char* fn)
+// The frame of mirt_render_frame up to its D2H copy, enqueued on the ctx's
+// stream: `samples` slabs into d_out (the ctx's own buffer when null),
+// accumulation in the ctx's (possibly shared) buffer. *d_display = the slab
+// that holds the display after the last frame.
+int enqueue_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, uint32_t* d_out,
+                  uint32_t** d_display, const char* fn)
 {
     if (!ctx_ok(c, true, fn)) return MIRT_E_NOSCENE;
-    if (!cam || !frame_desc_valid(fd) || !out) {
+    if (!cam || !frame_desc_valid(fd)) {
         set_error("%s: invalid arguments", fn);
         return MIRT_E_INVALID;
     }
@@ -2037,19 +2039,46 @@ int enqueue_host_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_des
     }
     const FrameConst f = make_frame_const(cam, fd);
     const size_t pixels = (size_t)f.shard_rows * f.width;  // one frame (several: slab j = display after frame j)
-    int rc = ensure((void**)&c->d_out, &c->out_cap, pixels * f.samples * 4 + 4);
-    if (rc) return rc;
+    if (!d_out) {
+        int rc = ensure((void**)&c->d_out, &c->out_cap, pixels * f.samples * 4 + 4);
+        if (rc) return rc;
+        d_out = c->d_out;
+    }
     // a new frame geometry starts a fresh accumulation buffer
-    rc = accum_prepare(c->acc, pixels, c->stream);
+    int rc = accum_prepare(c->acc, pixels, c->stream);
     if (rc) return rc;
-    rc = launch_render(c, f, c->d_out, c->acc->d_acc, c->stream, true, nullptr);
+    rc = launch_render(c, f, d_out, c->acc->d_acc, c->stream, true, nullptr);
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(out, c->d_out + (size_t)(f.samples - 1) * pixels, pixels * 4, hipMemcpyDeviceToHost,
-                           c->stream));
+    *d_display = d_out + (size_t)(f.samples - 1) * pixels;
+    return MIRT_OK;
+}
+
+// The frame of mirt_render_frame up to and including its D2H copy, enqueued
+// on the ctx's stream.
+int enqueue_host_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, mirt_rgba8* out,
+                       const char* fn)
+{
+    if (!out) {
+        set_error("%s: invalid arguments", fn);
+        return MIRT_E_INVALID;
+    }
+    uint32_t* disp = nullptr;
+    if (int rc = enqueue_frame(c, cam, fd, nullptr, &disp, fn)) return rc;
+    const size_t pixels = (size_t)shard_row_count(fd) * fd->width;
+    HIP_TRY(hipMemcpyAsync(out, disp, pixels * 4, hipMemcpyDeviceToHost, c->stream));
     return MIRT_OK;
 }
 
 }  // namespace
+
+namespace mirt {
+int enqueue_frame_device(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, uint32_t* d_out,
+                         uint32_t** d_display, const char* fn)
+{
+    return enqueue_frame(c, cam, fd, d_out, d_display, fn);
+}
+int ctx_device(const mirt_ctx* c) { return c->device; }
+}  // namespace mirt
 
 extern "C" {
 
@@ -2118,6 +2147,14 @@ int mirt_ctx_share_accum(mirt_ctx* c, mirt_ctx* owner)
             return MIRT_E_NOMEM;
         }
     } else {
+        if (next->refs == 1) {
+            // the owner's frames enqueued while its buffer was private wrote
+            // it directly (store_pixel) and recorded no fold event: from now
+            // on every fold, on any stream, must follow them
+            if (next->has_fold) HIP_TRY(hipStreamWaitEvent(owner->stream, next->folded, 0));
+            HIP_TRY(hipEventRecord(next->folded, owner->stream));
+            next->has_fold = true;
+        }
         next->refs++;
     }
     // c's frames enqueued so far still use its old buffer
@@ -2494,6 +2531,9 @@ int mirt_set_option(mirt_ctx* c, int option, int value)
     if (!c) return MIRT_E_INVALID;
     switch (option) {
     case MIRT_OPT_TRAVERSAL:
+        // mirt 0.2 numbered WAVEFRONT 1 (0.1 and 0.3+: 5); 1 stays a
+        // deprecated alias so binaries built against the 0.2 header keep working
+        if (value == MIRT_TRAV_WAVEFRONT_V02) value = MIRT_TRAV_WAVEFRONT;
         if (value != MIRT_TRAV_TILE && value != MIRT_TRAV_WAVEFRONT) break;
         c->trav = value;
         return MIRT_OK;

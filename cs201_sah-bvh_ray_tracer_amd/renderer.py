@@ -403,3 +403,77 @@ class Renderer:
         out = np.zeros(len(rays), np.int32)
         check(self.L.mirt_aabb_pairs(self.h, ptr(rays), ptr(boxes), len(rays), ptr(out)), "mirt_aabb_pairs")
         return out
+
+
+class MultiRenderer:
+    """One frame loop over several GPUs from this process (include/mirt_multi.h,
+    SURVEY §8(b) mirt_init(num_gpus)): interleaved row blocks per rank, the
+    slabs gathered to rank 0 over RCCL (distinct devices) or by device copies
+    ("copy": forced, or a device listed twice -- n shards on one GPU), `lanes`
+    frames in flight. Frames equal Renderer.render_frame's on one GPU."""
+
+    def __init__(self, devices, lanes=1, copy=False):
+        self.L = load()
+        devs = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        check(self.L.mirt_multi_create(devs, len(devices), lanes, abi.MULTI_COPY if copy else 0, C.byref(h)),
+              "mirt_multi_create")
+        self.h = h
+        self.devices = list(devices)
+
+    def close(self):
+        if self.h:
+            self.L.mirt_multi_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def backend(self):
+        return self.L.mirt_multi_backend(self.h).decode()
+
+    @property
+    def size(self):
+        return self.L.mirt_multi_size(self.h)
+
+    def upload(self, spheres, bvh):
+        spheres = np.ascontiguousarray(spheres, abi.SPHERE)
+        if isinstance(bvh, Bvh):
+            check(self.L.mirt_multi_scene_upload_flat(self.h, ptr(spheres), len(spheres), ptr(bvh.nodes),
+                                                      len(bvh.nodes)), "mirt_multi_scene_upload_flat")
+        else:
+            check(self.L.mirt_multi_scene_upload(self.h, ptr(spheres), len(spheres), bvh), "mirt_multi_scene_upload")
+
+    def set_option(self, option, value):
+        check(self.L.mirt_multi_set_option(self.h, option, value), "mirt_multi_set_option")
+
+    def render_frame(self, cam, width, height, depth=5, use_bvh=True, seed=1, sample=0, accumulate=False, frames=1,
+                     row_block=8, samples=1, jitter=False):
+        """The whole frame (height, width, 4) uint8, blocking."""
+        fd = frame_desc(width, height, depth, use_bvh, seed, sample, accumulate, frames, row_block, 0, 1, samples,
+                        jitter)
+        out = np.zeros((height, width, 4), np.uint8)
+        check(self.L.mirt_multi_render_frame(self.h, C.byref(cam), C.byref(fd), ptr(out)), "mirt_multi_render_frame")
+        return out
+
+    def render_frame_async(self, cam, fd, out):
+        """Enqueue a whole frame into `out` (HostBuffer or uint8 array of
+        height x width x 4) on the next lane; complete after wait()."""
+        arr = out.array if isinstance(out, HostBuffer) else out
+        if arr.nbytes < fd.width * fd.height * 4 or not arr.flags["C_CONTIGUOUS"]:
+            raise MirtError("render_frame_async: output too small")
+        check(self.L.mirt_multi_render_frame_async(self.h, C.byref(cam), C.byref(fd), ptr(arr)),
+              "mirt_multi_render_frame_async")
+
+    def wait(self):
+        check(self.L.mirt_multi_wait(self.h), "mirt_multi_wait")

@@ -400,10 +400,12 @@ enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3,
        MIRT_OPT_QUAD_BATCH = 15     /* mirt_intersect_rays / mirt_any_hit_rays with the BVH: 1
                                        (default) = a batch too small to fill the chip one ray per
                                        lane walks one ray per four lanes (benchmark.c's 10k rays) */ };
-/* Traversal ids keep their first-release values (mirt 0.1: TILE 0, WAVEFRONT 5);
-   the retired ids 1-4 (per-lane / chunked / DFS-only schedules of mirt 0.1) and
-   the retired option ids 8, 10, 12, 13 return MIRT_E_INVALID. */
-enum { MIRT_TRAV_TILE = 0, MIRT_TRAV_WAVEFRONT = 5 };
+/* Traversal ids keep their first-release values (mirt 0.1: TILE 0, WAVEFRONT 5).
+   ABI note: the mirt 0.2 header numbered WAVEFRONT 1; mirt_set_option accepts
+   1 as a deprecated alias of MIRT_TRAV_WAVEFRONT (mirt_get_option reads back
+   5), to be dropped in 1.0. The retired ids 2-4 (chunked / DFS-only schedules
+   of mirt 0.1) and the retired option ids 8, 10, 12, 13 return MIRT_E_INVALID. */
+enum { MIRT_TRAV_TILE = 0, MIRT_TRAV_WAVEFRONT = 5, MIRT_TRAV_WAVEFRONT_V02 = 1 /* deprecated alias */ };
 int mirt_set_option(mirt_ctx *ctx, int option, int value);
 int mirt_get_option(mirt_ctx *ctx, int option);
 

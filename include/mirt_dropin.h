@@ -26,7 +26,10 @@
  * Scenes: trace_ray / ray_bvh_intersect upload the caller's spheres and
  * pointer tree on first sight and reuse them while the key -- sphere
  * pointer, count, root pointer AND a content fingerprint (the tree's top 31
- * nodes, 32 strided spheres) -- is unchanged, so benchmark.c's free /
+ * nodes, 32 strided spheres of the array passed in that call; ray_bvh_intersect
+ * re-checks the tree part only, read through the tree it is given, never
+ * through a sphere pointer kept from an earlier call) -- is unchanged, so
+ * benchmark.c's free /
  * malloc / rebuild loop (benchmark.c:306-324), whose new tree and array
  * usually land at the old addresses, re-uploads without being told;
  * mirt_dropin_invalidate() forces it (e.g. after changing a sphere in place
@@ -36,7 +39,12 @@
  * range -- or the whole array declared with mirt_dropin_scene, which a caller
  * whose tree covers part of its array (benchmark.c:317 builds over
  * [0, n - 1)) passes so that a 0-sphere leaf pointing at spheres[n - 1]
- * tests it as hit.c:96-97 does.
+ * tests it as hit.c:96-97 does. Without the declaration such a leaf's
+ * spheres[n - 1] lies past the leaves' span and becomes the never-hit
+ * sentinel: the one case where the per-ray call can differ from hit.c without
+ * the declaration (benchmark.c migration). A declaration is
+ * read when the next tree is bound, so re-declare per array (benchmark.c:306)
+ * and clear it (mirt_dropin_scene(NULL, 0)) before freeing the array.
  *
  * RNG: trace_ray's bounces draw from the per-pixel RNG contract
  * with seed/sample from mirt_dropin_rng and pixel index = the number of
@@ -66,7 +74,9 @@ void mirt_dropin_release(void);
 /* RNG contract of trace_ray's bounces; restarts the pixel counter at 0. */
 void mirt_dropin_rng(uint64_t seed, uint32_t sample);
 /* The caller's whole sphere array for ray_bvh_intersect calls whose tree lies
-   inside it (NULL / 0: none). Optional; see "Scenes" above. */
+   inside it (NULL / 0: none). Optional; see "Scenes" above. The library reads
+   the array when it binds a tree inside it, so the declaration must name
+   live memory: clear it before freeing the array. */
 int mirt_dropin_scene(const mirt_sphere *spheres, int num_spheres);
 /* Forget the uploaded scene (after changing sphere contents in place). */
 void mirt_dropin_invalidate(void);

@@ -17,6 +17,12 @@
  * --per-ray K: the first K rays of both loops again through the per-ray
  * surface (mirt_ray_sphere_intersect over every sphere / mirt_ray_bvh_intersect
  * on the pointer tree, the calls benchmark.c:196 and :242 make) -- must agree.
+ * --per-ray-bvh K: the BVH loop's first K rays only (one launch per ray, so it
+ * runs at every point of the reference sweep, whose arrays of 10k spheres and
+ * up glibc munmaps on free: the drop-in must never read a freed array).
+ * Each point declares its whole array (mirt_dropin_scene: the tree covers
+ * [0, n - 1) of it, benchmark.c:317) and clears the declaration before
+ * freeing it -- the documented recipe for benchmark.c.
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -41,10 +47,11 @@ int main(int argc, char **argv)
     const unsigned seed = (unsigned)strtoul(argv[1], NULL, 10);
     const int num_rays = atoi(argv[2]);
     const char *out = argv[3];
-    int per_ray = 0, npts = 0;
+    int per_ray = 0, per_ray_bvh = 0, npts = 0;
     int counts[64];
     for (int i = 4; i < argc; i++) {
         if (!strcmp(argv[i], "--per-ray") && i + 1 < argc) per_ray = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--per-ray-bvh") && i + 1 < argc) per_ray_bvh = atoi(argv[++i]);
         else if (npts < 64) counts[npts++] = atoi(argv[i]);
     }
     const float world_size = 1000.0f; /* benchmark.c:299 */
@@ -81,6 +88,7 @@ int main(int argc, char **argv)
         if ((rc = mirt_bench_rays(&st, rays_a, num_rays))) return fail("mirt_bench_rays", rc);
         if ((rc = mirt_bench_rays(&st, rays_b, num_rays))) return fail("mirt_bench_rays", rc);
         if ((rc = mirt_scene_upload(ctx, spheres, n, root))) return fail("mirt_scene_upload", rc);
+        if ((rc = mirt_dropin_scene(spheres, n))) return fail("mirt_dropin_scene", rc);
 
         if ((rc = mirt_any_hit_rays(ctx, rays_a, num_rays, 0, hit_a))) return fail("mirt_any_hit_rays", rc);
         const double t_no = mirt_last_kernel_ms(ctx) / 1e3;
@@ -112,6 +120,19 @@ int main(int argc, char **argv)
             }
             printf("per-ray surface, first %d rays of both loops: %d mismatches\n", K, mismatches);
         }
+        if (per_ray_bvh > 0) {
+            const int K = per_ray_bvh < num_rays ? per_ray_bvh : num_rays;
+            int bad = 0;
+            for (int k = 0; k < K; k++) {
+                mirt_hit_record h = mirt_ray_bvh_intersect(rays_b[k], root);
+                if (mirt_dropin_status()) return fail("mirt_ray_bvh_intersect", mirt_dropin_status());
+                if (h.hit_something != hit_b[k] ||
+                    (h.hit_something && (h.object != &spheres[rec_b[k].sphere] || h.t != rec_b[k].t)))
+                    bad++;
+            }
+            mismatches += bad;
+            printf("per-ray BVH surface, first %d rays: %d mismatches\n", K, bad);
+        }
 
         fprintf(fdat, "%d %f %f\n", n, t_no, t_bvh); /* save_benchmark_data */
         fwrite(hit_a, sizeof(int32_t), (size_t)num_rays, fbin);
@@ -120,6 +141,7 @@ int main(int argc, char **argv)
            and array usually come back at these addresses, and the drop-in's
            content fingerprint has to notice (the per-ray check above runs at
            every sweep point) */
+        mirt_dropin_scene(NULL, 0);
         mirt_free_bvh(root);
         free(spheres);
         printf("----------------------------------------\n");

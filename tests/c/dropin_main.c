@@ -6,7 +6,7 @@
  * motion, 'b' toggles the BVH) driven by a script instead of SDL, each frame
  * ONE mirt_render_frame call in place of the per-pixel loop of main.c:356-407.
  *
- *   dropin_main W H NSPH SEED SCRIPT OUT [--ref-build LIBREF] [--per-ray]
+ *   dropin_main W H NSPH SEED SCRIPT OUT [--ref-build LIBREF] [--per-ray] [--gpus N [--same-device]]
  *
  * SCRIPT: frames separated by ',', each listing the events polled before it:
  *   w s a d   move along forward / right (main.c:291-310)
@@ -24,6 +24,10 @@
  * (mirt_get_camera_ray + mirt_trace_ray per pixel, the loop of
  * main.c:358-374; two launches per pixel, so for small frames) and check it
  * against mirt_render_frame's.
+ * --gpus N: the same loop over N GPUs from this one thread (include/mirt_multi.h:
+ * interleaved 8-row blocks per GPU, the slabs gathered to GPU 0 over RCCL, one
+ * mirt_multi_render_frame per frame); --same-device puts the N ranks on GPU 0
+ * (copy-mode gather: the N-GPU frame geometry on a one-GPU box).
  * Exit status 0 = ran (and the per-ray check matched).
  */
 #include <dlfcn.h>
@@ -36,6 +40,7 @@
 
 #include "mirt.h"
 #include "mirt_dropin.h"
+#include "mirt_multi.h"
 
 #define MOVE_SPEED 0.5f      /* constants.h:3 */
 #define ROTATE_SPEED 0.002f  /* constants.h:4 */
@@ -68,10 +73,12 @@ int main(int argc, char **argv)
     const unsigned seed = (unsigned)strtoul(argv[4], NULL, 10);
     const char *script = argv[5], *out = argv[6];
     const char *libref = NULL;
-    int per_ray = 0;
+    int per_ray = 0, gpus = 0, same_device = 0;
     for (int i = 7; i < argc; i++) {
         if (!strcmp(argv[i], "--ref-build") && i + 1 < argc) libref = argv[++i];
         else if (!strcmp(argv[i], "--per-ray")) per_ray = 1;
+        else if (!strcmp(argv[i], "--gpus") && i + 1 < argc) gpus = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--same-device")) same_device = 1;
     }
 
     /* main.c:203-221: camera, srand, N x create_random_sphere */
@@ -105,10 +112,22 @@ int main(int argc, char **argv)
     if (!root) return fail("build_bvh_node", -1);
     printf("BVH built in %f seconds (%d nodes)\n", now() - t0, mirt_bvh_count(root));
 
-    mirt_ctx *ctx;
-    if ((rc = mirt_create(0, &ctx))) return fail("mirt_create", rc);
-    /* the reference's pointer tree and the (reordered) spheres, copied once */
-    if ((rc = mirt_scene_upload(ctx, spheres, N, root))) return fail("mirt_scene_upload", rc);
+    mirt_ctx *ctx = NULL;
+    mirt_multi *multi = NULL;
+    if (gpus > 0) {
+        /* mirt_init(num_gpus) of SURVEY 8(b): one renderer over the node's GPUs */
+        int devs[64];
+        if (gpus > 64) return fail("--gpus", -1);
+        for (int g = 0; g < gpus; g++) devs[g] = same_device ? 0 : g;
+        if ((rc = mirt_multi_create(devs, gpus, 1, 0, &multi))) return fail("mirt_multi_create", rc);
+        printf("%d ranks, gather over %s\n", mirt_multi_size(multi), mirt_multi_backend(multi));
+        if ((rc = mirt_multi_scene_upload(multi, spheres, N, root))) return fail("mirt_multi_scene_upload", rc);
+        ctx = mirt_multi_ctx(multi, 0, 0);
+    } else {
+        if ((rc = mirt_create(0, &ctx))) return fail("mirt_create", rc);
+        /* the reference's pointer tree and the (reordered) spheres, copied once */
+        if ((rc = mirt_scene_upload(ctx, spheres, N, root))) return fail("mirt_scene_upload", rc);
+    }
 
     char path[4096];
     snprintf(path, sizeof path, "%s.rgba", out);
@@ -170,7 +189,12 @@ int main(int argc, char **argv)
             fd.accumulate = 1;
             fd.frames = accumulated_frames;
         }
-        if ((rc = mirt_render_frame(ctx, &camera, &fd, frame))) return fail("mirt_render_frame", rc);
+        if (multi) {
+            fd.num_shards = 1; /* the whole frame: mirt_multi shards it */
+            if ((rc = mirt_multi_render_frame(multi, &camera, &fd, frame))) return fail("mirt_multi_render_frame", rc);
+        } else if ((rc = mirt_render_frame(ctx, &camera, &fd, frame))) {
+            return fail("mirt_render_frame", rc);
+        }
         fwrite(frame, sizeof(mirt_rgba8), (size_t)W * H, fimg);
         uint32_t cw[16];
         memcpy(cw, &camera, sizeof cw);
@@ -216,7 +240,8 @@ int main(int argc, char **argv)
            total_render_time / frame_count * 1e3, mirt_last_kernel_ms(ctx));
     fclose(fimg);
     fclose(flog);
-    mirt_destroy(ctx);
+    if (multi) mirt_multi_destroy(multi);
+    else mirt_destroy(ctx);
     mirt_free_bvh(root);
     free(frame);
     free(spheres);

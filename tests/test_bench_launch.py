@@ -38,6 +38,28 @@ def test_failing_rank_fails_the_launch():
     assert p.returncode != 0
 
 
+@pytest.mark.parametrize("hang,want_rc", [("1", None), ("all", 124)])
+def test_stuck_rank_hits_the_deadline(hang, want_rc):
+    """A rank that never joins must not hold the launch. MIRT_BENCH_DRY_HANG=1:
+    rank 1 sleeps before init_process_group, so rank 0's rendezvous times out
+    (the process group's timeout) and the parent ends the job. "all": no rank
+    joins, nothing raises inside the ranks, and the parent's own deadline
+    (--rank-timeout) terminates them: exit 124. Either way the parent exits
+    non-zero within the deadline + 10 s."""
+    import time
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["MIRT_BENCH_DRY_HANG"] = hang
+    deadline = 20.0
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry", "--steps", "2",
+                        "--warmup", "1", "--rank-timeout", str(deadline)], capture_output=True, text=True,
+                       timeout=120, env=env, cwd=ROOT)
+    dt = time.monotonic() - t0
+    assert p.returncode != 0 and dt < deadline + 10, (p.returncode, dt, p.stderr[-2000:])
+    if want_rc is not None:
+        assert p.returncode == want_rc and "deadline" in p.stderr and "[0, 1]" in p.stderr, p.stderr[-2000:]
+
+
 @pytest.mark.gpu
 def test_multi_rank_bench_rehearsal_on_one_gpu():
     """The N > 1 bench path on a one-GPU box (MIRT_BENCH_SHARE_GPU=1: both

@@ -156,6 +156,29 @@ def test_c_main_loop_matches_oracle(tmp_path, mirt, oracle):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("gpus,same", [(1, False), (3, True), (8, True)])
+def test_c_main_loop_multi_gpu(tmp_path, golden, gpus, same):
+    """main.c's loop driving N GPUs from C with no Python between
+    (mirt_multi_render_frame per frame): --gpus 1 gathers through RCCL, 3 and
+    8 ranks on the one GPU through the copy gather; the first frame is the
+    golden 1080p frame and the accumulating frames equal the one-ctx run's."""
+    exe = build(tmp_path, "dropin_main")
+    one = str(tmp_path / "one")
+    rc, so, se = run([exe, "1920", "1080", "10000", "1", "R,,", one])
+    assert rc == 0, se
+    out = str(tmp_path / "multi")
+    cmd = [exe, "1920", "1080", "10000", "1", "R,,", out, "--gpus", str(gpus)] + (["--same-device"] if same else [])
+    rc, so, se = run(cmd)
+    assert rc == 0, so + se
+    assert f"{gpus} ranks, gather over {'copy' if same else 'rccl'}" in so
+    raw, log = _frames(out, 1920, 1080)
+    ref, log1 = _frames(one, 1920, 1080)
+    assert log == log1 and len(raw) == 3
+    assert hashlib.sha256(raw[0].tobytes()).hexdigest() == golden["frames"]["1920x1080_render10000_d5_m1_b1_s1_c0_step1"]["sha"]
+    assert (raw == ref).all()
+
+
+@pytest.mark.gpu
 def test_c_per_pixel_loop_through_per_ray_surface(tmp_path):
     """main.c:358-374 verbatim in structure: mirt_get_camera_ray +
     mirt_trace_ray per pixel reproduce mirt_render_frame's fresh frame."""
@@ -182,11 +205,14 @@ def test_c_reference_built_pointer_tree(tmp_path, golden):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,per_ray", [("small", 32), ("reference", 0)])
+@pytest.mark.parametrize("name,per_ray", [("small", ["--per-ray", "32"]), ("reference", ["--per-ray-bvh", "16"])])
 def test_c_benchmark_mode(tmp_path, name, per_ray):
     """benchmark.c's sweep from C: per-ray hit flags of both loops equal the
     reference's (tests/golden/bench_mode.json); on the small sweep the first
-    32 rays also go through the per-ray surface one call at a time."""
+    32 rays also go through the per-ray surface one call at a time, on the
+    reference sweep (5k-50k spheres: arrays past glibc's mmap threshold, freed
+    and reallocated between points with no invalidate call) the BVH loop's
+    first 16 rays go through mirt_ray_bvh_intersect."""
     with open(os.path.join(GOLDEN, "bench_mode.json")) as f:
         sw = json.load(f)["sweeps"][name]
     pts = sw["points"]
@@ -194,8 +220,7 @@ def test_c_benchmark_mode(tmp_path, name, per_ray):
     exe = build(tmp_path, "dropin_bench")
     out = str(tmp_path / "b")
     cmd = [exe, str(sw["seed"]), str(nr), out] + [str(p["spheres"]) for p in pts]
-    if per_ray:
-        cmd += ["--per-ray", str(per_ray)]
+    cmd += per_ray
     rc, so, se = run(cmd)
     assert rc == 0, so[-2000:] + se
     flags = np.fromfile(out + ".bin", np.int32).reshape(len(pts), 2, nr)
@@ -205,3 +230,17 @@ def test_c_benchmark_mode(tmp_path, name, per_ray):
         assert int(f[0].sum()) == p["hits_no_bvh"] and int(f[1].sum()) == p["hits_bvh"]
     lines = open(out + ".txt").read().split("\n")
     assert [int(ln.split()[0]) for ln in lines if ln] == [p["spheres"] for p in pts]
+
+
+@pytest.mark.gpu
+def test_c_benchmark_mode_large_arrays_freed(tmp_path):
+    """benchmark.c:306-324's free / malloc / rebuild with arrays of several MB
+    (150k and 200k spheres: 3-4 MB, munmapped by free), the tree and array
+    usually returning at the same addresses and no invalidate call: every
+    per-ray mirt_ray_bvh_intersect agrees with the batch call on the live
+    scene (a drop-in that read the freed array would fault or disagree)."""
+    exe = build(tmp_path, "dropin_bench")
+    out = str(tmp_path / "big")
+    rc, so, se = run([exe, "3", "512", out, "150000", "150000", "200000", "200000", "--per-ray-bvh", "8"])
+    assert rc == 0, so[-2000:] + se
+    assert so.count("per-ray BVH surface, first 8 rays: 0 mismatches") == 4

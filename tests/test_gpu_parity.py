@@ -351,6 +351,40 @@ def test_shared_accumulation_frames_in_flight(gpu, mirt, oracle, small, W, H, n)
             x.close()
 
 
+def test_share_after_private_async_frames(gpu, mirt):
+    """A ctx that starts sharing a buffer whose owner still has frames in
+    flight that wrote it privately (no fold event): the sharer's first fold
+    must follow them. Owner: three async accumulating frames, no
+    wait; then the share and the sharer's frame 4: equals four blocking
+    frames on one ctx."""
+    W, H = 640, 360
+    s, b = _scene(mirt, "render", 10000)
+    cam = mirt.default_camera()
+    rs = [mirt.Renderer(0) for _ in range(2)]
+    bufs = [mirt.HostBuffer((H, W, 4)) for _ in rs]
+    try:
+        for x in rs:
+            x.upload(s, b)
+        for k in range(3):
+            fd = mirt.frame_desc(W, H, depth=5, seed=4, sample=k, accumulate=k > 0, frames=k + 1)
+            rs[0].render_frame_async(cam, fd, bufs[0])
+        rs[1].share_accum(rs[0])
+        fd = mirt.frame_desc(W, H, depth=5, seed=4, sample=3, accumulate=True, frames=4)
+        rs[1].render_frame_async(cam, fd, bufs[1])
+        rs[1].wait()
+        rs[0].wait()
+        got = bufs[1].array.copy()
+        gpu.upload(s, b)
+        for k in range(4):
+            seq = gpu.render_frame(cam, W, H, depth=5, seed=4, sample=k, accumulate=k > 0, frames=k + 1)
+        assert (got == seq).all()
+    finally:
+        for x in bufs:
+            x.close()
+        for x in rs:
+            x.close()
+
+
 def test_counts_match_oracle(gpu, mirt, oracle):
     s, b = _scene(mirt, "render", 10000)
     gpu.upload(s, b)
@@ -629,6 +663,21 @@ def test_bounce_modes_identical(gpu, mirt, golden, drain, threshold, blocks):
         gpu.set_option(abi.OPT_BOUNCE_BLOCKS, 0)
     key = "1920x1080_render10000_d5_m1_b1_s1_c0_step1"
     assert sha(img) == golden["frames"][key]["sha"]
+
+
+def test_traversal_v02_alias(gpu, mirt):
+    """the mirt 0.2 header's MIRT_TRAV_WAVEFRONT (1) is accepted as
+    a deprecated alias and reads back as 5; the retired ids stay errors."""
+    abi = mirt.abi
+    try:
+        gpu.set_option(abi.OPT_TRAVERSAL, abi.TRAV_TILE)
+        gpu.set_option(abi.OPT_TRAVERSAL, 1)
+        assert gpu.get_option(abi.OPT_TRAVERSAL) == abi.TRAV_WAVEFRONT
+        for bad in (2, 3, 4, 6):
+            with pytest.raises(mirt.MirtError):
+                gpu.set_option(abi.OPT_TRAVERSAL, bad)
+    finally:
+        gpu.set_option(abi.OPT_TRAVERSAL, abi.TRAV_WAVEFRONT)
 
 
 def test_cached_tree_renders_golden_frame(gpu, mirt, golden, tmp_path):

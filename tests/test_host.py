@@ -126,7 +126,7 @@ def test_abi_exports_every_declared_symbol(mirt):
     """libmirt.so loads and exports every function include/*.h declares
     (and abi.SIGNATURES covers exactly those)."""
     declared = set()
-    for h in ("mirt.h", "mirt_dropin.h"):
+    for h in ("mirt.h", "mirt_dropin.h", "mirt_multi.h"):
         hdr = open(os.path.join(ROOT, "include", h)).read()
         hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
         declared |= set(re.findall(r"\b(mirt_[a-z0-9_]+)\s*\(", hdr))

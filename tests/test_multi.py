@@ -1,0 +1,112 @@
+"""include/mirt_multi.h: one frame loop over several GPUs from one process
+(SURVEY §8(b) mirt_init(num_gpus); §8(e) interleaved row-block shards, the
+slabs gathered to rank 0 over RCCL, de-interleaved there).
+
+The frame of n ranks must equal the one-GPU frame byte for byte (the RNG
+contract keys on the full-frame pixel index). On the one-GPU box: n = 1 runs
+the real RCCL path (ncclCommInitAll over one device, every slab through an
+ncclSend/ncclRecv group), and n = 2 / 3 / 8 ranks on the same device run the
+copy-mode gather (RCCL refuses two ranks on one device) -- the same shard
+geometry, slab strides and de-interleave as n GPUs. CPU: the entry points
+fail loudly without a GPU."""
+import hashlib
+
+import numpy as np
+import pytest
+
+GOLD = "1920x1080_render10000_d5_m1_b1_s1_c0_step1"
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def test_multi_fails_loudly_without_gpu(mirt):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(mirt.MirtError):
+        mirt.MultiRenderer([0])
+
+
+@pytest.fixture(scope="module")
+def scene10k(mirt):
+    s = mirt.create_random_spheres(10000, 1)
+    return s, mirt.build_bvh(s)
+
+
+@pytest.mark.gpu
+def test_multi_rccl_one_gpu_golden(mirt, golden, scene10k):
+    """n = 1 through RCCL: the golden 1080p / 10k depth-5 frame."""
+    s, b = scene10k
+    with mirt.MultiRenderer([0]) as m:
+        assert m.backend == "rccl" and m.size == 1
+        m.upload(s, b)
+        img = m.render_frame(mirt.default_camera(), 1920, 1080, depth=5, seed=1)
+        assert sha(img) == golden["frames"][GOLD]["sha"]
+        img2 = m.render_frame(mirt.default_camera(), 1920, 1080, depth=5, seed=1)
+        assert sha(img2) == golden["frames"][GOLD]["sha"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_multi_same_device_golden(mirt, golden, scene10k, n):
+    """n shards on one GPU, copy-mode gather + de-interleave: the golden frame."""
+    s, b = scene10k
+    with mirt.MultiRenderer([0] * n) as m:
+        assert m.backend == "copy" and m.size == n
+        m.upload(s, b)
+        img = m.render_frame(mirt.default_camera(), 1920, 1080, depth=5, seed=1)
+        assert sha(img) == golden["frames"][GOLD]["sha"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,rb", [(3, 8), (5, 16), (4, 1)])
+def test_multi_ragged_frames_equal_one_gpu(gpu, mirt, n, rb):
+    """Ragged sizes (77 x 45: the last block short, some ranks one block
+    fewer) and other interleave blocks equal one ctx's frame, depth 1 and 5,
+    brute force too."""
+    s = mirt.create_random_spheres(1000, 2)
+    b = mirt.build_bvh(s)
+    gpu.upload(s, b)
+    cam = mirt.default_camera()
+    with mirt.MultiRenderer([0] * n) as m:
+        m.upload(s, b)
+        for depth, bvh in ((1, True), (5, True), (5, False)):
+            want = gpu.render_frame(cam, 77, 45, depth=depth, use_bvh=bvh, seed=3)
+            got = m.render_frame(cam, 77, 45, depth=depth, use_bvh=bvh, seed=3, row_block=rb)
+            assert (got == want).all(), (depth, bvh)
+
+
+@pytest.mark.gpu
+def test_multi_lanes_accumulating_loop(gpu, mirt, scene10k):
+    """main.c:349-408's loop with frames in flight: 3 lanes x 2 shards, a
+    fresh frame, accumulating frames, a camera move, more accumulation; every
+    host frame equals the same sequence of blocking one-ctx frames."""
+    s, b = scene10k
+    W, H = 320, 180
+    cam0 = mirt.default_camera()
+    cam1 = mirt.default_camera()
+    cam1.position.x += 0.5
+    seq = [(cam0, False, 1), (cam0, True, 2), (cam0, True, 3), (cam1, False, 1), (cam1, True, 2), (cam1, True, 3),
+           (cam1, True, 4)]
+    gpu.upload(s, b)
+    want = [gpu.render_frame(c, W, H, depth=5, seed=2, sample=k, accumulate=a, frames=f)
+            for k, (c, a, f) in enumerate(seq)]
+    with mirt.MultiRenderer([0, 0], lanes=3) as m:
+        m.upload(s, b)
+        bufs = [mirt.HostBuffer((H, W, 4)) for _ in range(3)]
+        got = []
+        try:
+            # three frames in flight between waits (frame k on lane k % 3)
+            for k, (c, a, f) in enumerate(seq):
+                fd = mirt.frame_desc(W, H, depth=5, seed=2, sample=k, accumulate=a, frames=f)
+                m.render_frame_async(c, fd, bufs[k % 3])
+                if k % 3 == 2 or k == len(seq) - 1:
+                    m.wait()
+                    got += [bufs[j % 3].array.copy() for j in range(len(got), k + 1)]
+        finally:
+            for x in bufs:
+                x.close()
+    for k in range(len(seq)):
+        assert (got[k] == want[k]).all(), k
