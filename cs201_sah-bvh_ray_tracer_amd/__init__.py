@@ -16,11 +16,11 @@ Layout:
 """
 from . import abi
 from .lib import LIB_PATH, MirtError, build, load
-from .renderer import (Bvh, HostBuffer, MultiRenderer, RandState, Renderer, build_bvh, build_bvh_cached, build_bvh_node, camera_update,
+from .renderer import (Bvh, HostBuffer, MultiRenderer, host_register, host_unregister, RandState, Renderer, build_bvh, build_bvh_cached, build_bvh_node, camera_update,
                        create_bench_rays, create_benchmark_spheres, create_random_spheres, default_camera,
                        flatten_bvh,
                        frame_desc, free_bvh, shard_rows, validate_bvh)
 
-__all__ = ["abi", "LIB_PATH", "MirtError", "build", "load", "Bvh", "HostBuffer", "MultiRenderer", "RandState", "Renderer", "build_bvh", "build_bvh_cached",
+__all__ = ["abi", "LIB_PATH", "MirtError", "build", "load", "Bvh", "HostBuffer", "MultiRenderer", "host_register", "host_unregister", "RandState", "Renderer", "build_bvh", "build_bvh_cached",
            "build_bvh_node", "camera_update", "create_bench_rays", "create_benchmark_spheres", "create_random_spheres",
            "default_camera", "flatten_bvh", "frame_desc", "free_bvh", "shard_rows", "validate_bvh"]

@@ -140,6 +140,8 @@ SIGNATURES = [
     ("mirt_ctx_wait", I, [P]),
     ("mirt_host_alloc", I, [C.c_size_t, C.POINTER(P)]),
     ("mirt_host_free", None, [P]),
+    ("mirt_host_register", I, [P, C.c_size_t]),
+    ("mirt_host_unregister", I, [P]),
     ("mirt_accum_download", I, [P, P, C.c_size_t]),
     ("mirt_ctx_share_accum", I, [P, P]),
     ("mirt_trace_rays", I, [P, P, I, I, I, C.c_uint64, C.c_uint32, P]),

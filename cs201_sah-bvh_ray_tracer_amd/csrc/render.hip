@@ -2116,6 +2116,26 @@ void mirt_host_free(void* p)
     if (p) (void)hipHostFree(p);
 }
 
+int mirt_host_register(void* p, size_t bytes)
+{
+    if (!p || !bytes) {
+        set_error("mirt_host_register: invalid arguments");
+        return MIRT_E_INVALID;
+    }
+    HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterDefault));
+    return MIRT_OK;
+}
+
+int mirt_host_unregister(void* p)
+{
+    if (!p) {
+        set_error("mirt_host_unregister: null pointer");
+        return MIRT_E_INVALID;
+    }
+    HIP_TRY(hipHostUnregister(p));
+    return MIRT_OK;
+}
+
 int mirt_accum_download(mirt_ctx* c, float* out, size_t count)
 {
     if (!ctx_ok(c, false, "mirt_accum_download") || !out) return MIRT_E_INVALID;

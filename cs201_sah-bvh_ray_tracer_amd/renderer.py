@@ -177,6 +177,18 @@ def shard_rows(fd):
     return rows
 
 
+def host_register(arr):
+    """Page-lock a C-contiguous numpy array in place (mirt_host_register):
+    blocking frames copied into it become one DMA. host_unregister before the
+    array is released."""
+    assert arr.flags["C_CONTIGUOUS"]
+    check(load().mirt_host_register(ptr(arr), arr.nbytes), "mirt_host_register")
+
+
+def host_unregister(arr):
+    check(load().mirt_host_unregister(ptr(arr)), "mirt_host_unregister")
+
+
 class HostBuffer:
     """Page-locked host memory (mirt_host_alloc) viewed as a numpy array."""
 
@@ -254,6 +266,15 @@ class Renderer:
                         num_shards, samples, jitter)
         n = check(self.L.mirt_shard_rows(C.byref(fd), None), "mirt_shard_rows")
         out = np.zeros((n, width, 4), np.uint8)
+        check(self.L.mirt_render_frame(self.h, C.byref(cam), C.byref(fd), ptr(out)), "mirt_render_frame")
+        return out
+
+    def render_frame_into(self, cam, width, height, out, depth=5, use_bvh=True, seed=1, sample=0, accumulate=False,
+                          frames=1, samples=1, jitter=False):
+        """render_frame into a caller-given C-contiguous uint8 array (pageable,
+        registered or page-locked) of height x width x 4."""
+        fd = frame_desc(width, height, depth, use_bvh, seed, sample, accumulate, frames, 8, 0, 1, samples, jitter)
+        assert out.flags["C_CONTIGUOUS"] and out.nbytes >= width * height * 4
         check(self.L.mirt_render_frame(self.h, C.byref(cam), C.byref(fd), ptr(out)), "mirt_render_frame")
         return out
 

@@ -261,6 +261,13 @@ int mirt_ctx_wait(mirt_ctx *ctx);
    releases it (NULL is ignored). */
 int mirt_host_alloc(size_t bytes, void **out);
 void mirt_host_free(void *p);
+/* Page-lock a caller-owned buffer in place (hipHostRegister) -- the frame
+   buffer main.c:241-273's loop mallocs once and reuses every frame: the
+   blocking mirt_render_frame's D2H into it is then one DMA instead of the
+   runtime's staged pageable copy. The registration pins the pages until
+   mirt_host_unregister, which must come before the buffer is freed. */
+int mirt_host_register(void *p, size_t bytes);
+int mirt_host_unregister(void *p);
 
 /* Download the ctx's accumulation buffer (row-major float3 of the shard),
    after every fold enqueued into it so far. */

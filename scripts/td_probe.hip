@@ -1,63 +1,88 @@
-// Texture-path probe (not part of the library): cost of per-lane 16-B loads
-// from an L1/L2-resident table as a function of how many 64-B nodes the
-// lanes of one wave touch per instruction -- the bounce walk's node loads
-// are four dwordx4 per lane-visit.
+// Vector-memory gather probe (not part of the library): the chip's peak rate
+// of wave-level 16-B-per-lane loads (global_load_dwordx4) from an
+// L2-resident table, as a function of how many distinct 64-B nodes one
+// instruction touches -- the denominator of bench.py's `roofline` (the
+// bounce walk's node, leaf and sphere loads are per-lane dwordx4 gathers over
+// an L2-resident tree).
 //   hipcc -O3 --offload-arch=gfx950 scripts/td_probe.hip -o scripts/td_probe
-//   ./td_probe   (prints ns per wave-instruction for each lane grouping)
+//   ./scripts/td_probe > profiles/r04_td_probe.json   (one JSON object)
+// Shapes:
+//   lines L (1..64): L lanes of each wave active, each reading its own
+//     64-B node as four dwordx4 (the bounce walk's HNode visit) -> L distinct
+//     nodes per load instruction. The walk's waves run with a varying number
+//     of active lanes (queue refill at 20, quad drain below 16), so its mean
+//     distinct lines per instruction (TCP accesses / VMEM instructions in
+//     the counter pass) selects the peak it is priced against.
+//   shared G: all 64 lanes active, G lanes per node (quads, whole wave).
+// Every case: 8 waves per SIMD (2048 workgroups x 256), 256 independent
+// node visits per lane, timed after a warm-up launch; chip rate = wave-load
+// instructions / s.
 #include <hip/hip_runtime.h>
-#include <cstdio>
-#include <cstdint>
-#include <vector>
 
-// group: lanes per node (1 = every lane its own node, 4 = a quad shares one
-// node, each lane its own 16 B of it, 64 = the wave shares one node).
-// words: 4 loads per lane-visit (the whole 64-B node per lane) when
-// `whole`, else 1 (the lane's 16-B piece).
-__global__ void probe(const uint4* __restrict__ tab, uint32_t mask, int group, int whole, int iters,
-                      uint32_t* __restrict__ out)
+#include <cstdint>
+#include <cstdio>
+
+__global__ void __launch_bounds__(256) probe(const uint4* __restrict__ tab, uint32_t mask, int active, int group,
+                                             int iters, uint32_t* __restrict__ out)
 {
     const uint32_t lane = threadIdx.x & 63;
+    if ((int)lane >= active) return;
     const uint32_t seed = blockIdx.x * 977u + (threadIdx.x / group) * 131u;
     uint32_t acc = 0;
     for (int i = 0; i < iters; i++) {
-        const uint32_t node = ((seed + (uint32_t)i * 7919u) * 2654435761u >> 8) & mask;  // independent loads
+        const uint32_t node = ((seed + (uint32_t)i * 7919u) * 2654435761u >> 8) & mask;  // independent visits
         const uint4* p = tab + 4 * node;
-        if (whole) {
-            const uint4 a = p[0], b = p[1], c = p[2], d = p[3];
-            acc += a.x ^ b.y ^ c.z ^ d.w;
-        } else {
-            const uint4 a = p[lane & 3];
-            acc += a.x ^ a.w;
-        }
+        const uint4 a = p[0], b = p[1], c = p[2], d = p[3];
+        // every word used, so each load stays one global_load_dwordx4
+        acc += (a.x ^ a.y ^ a.z ^ a.w) + (b.x ^ b.y ^ b.z ^ b.w) + (c.x ^ c.y ^ c.z ^ c.w) + (d.x ^ d.y ^ d.z ^ d.w);
     }
-    if (acc == 0x12345678u) out[0] = acc;
+    if (acc == 0x12345678u) out[0] = acc;   // keeps the loads; never true for the table's contents
 }
 
 int main()
 {
-    const uint32_t nodes = 1u << 14;  // 1 MB: L2-resident
-    uint4* tab;
-    uint32_t* out;
-    (void)hipMalloc(&tab, sizeof(uint4) * 4 * nodes);
-    (void)hipMalloc(&out, 4);
+    const uint32_t nodes = 1u << 14;  // 16k x 64 B = 1 MB: L2-resident (the 10k scene's four-wide tree: 0.7 MB)
+    uint4* tab = nullptr;
+    uint32_t* out = nullptr;
+    if (hipMalloc(&tab, sizeof(uint4) * 4 * nodes) != hipSuccess || hipMalloc(&out, 4) != hipSuccess) return 1;
     (void)hipMemset(tab, 1, sizeof(uint4) * 4 * nodes);
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
-    const int blocks = 256 * 8, threads = 256, iters = 256;
-    for (int whole = 1; whole >= 0; whole--)
-        for (int group : {1, 4, 16, 64}) {
-            probe<<<blocks, threads>>>(tab, nodes - 1, group, whole, iters, out);
+    int cus = 0, clk_khz = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    (void)hipDeviceGetAttribute(&clk_khz, hipDeviceAttributeClockRate, 0);
+    const int blocks = 2048, threads = 256, iters = 256;
+    printf("{\"probe\": \"scripts/td_probe.hip\", \"cus\": %d, \"clock_khz\": %d, \"table_bytes\": %u, "
+           "\"waves\": %d, \"visits_per_lane\": %d, \"loads_per_visit\": 4, \"cases\": [",
+           cus, clk_khz, (unsigned)(64u * nodes), blocks * threads / 64, iters);
+    const int lines[] = {64, 48, 32, 24, 20, 16, 12, 8, 4, 1};
+    const int shared[] = {4, 16, 64};
+    bool first = true;
+    for (int k = 0; k < (int)(sizeof lines / sizeof lines[0]) + (int)(sizeof shared / sizeof shared[0]); k++) {
+        const bool sh = k >= (int)(sizeof lines / sizeof lines[0]);
+        const int active = sh ? 64 : lines[k];
+        const int group = sh ? shared[k - sizeof lines / sizeof lines[0]] : 1;
+        float best = 1e30f;
+        for (int rep = 0; rep < 3; rep++) {
+            probe<<<blocks, threads>>>(tab, nodes - 1, active, group, iters, out);   // warm
             (void)hipEventRecord(e0);
-            probe<<<blocks, threads>>>(tab, nodes - 1, group, whole, iters, out);
+            probe<<<blocks, threads>>>(tab, nodes - 1, active, group, iters, out);
             (void)hipEventRecord(e1);
             (void)hipEventSynchronize(e1);
             float ms = 0;
             (void)hipEventElapsedTime(&ms, e0, e1);
-            const double inst = (double)blocks * (threads / 64) * iters * (whole ? 4 : 1);
-            printf("whole=%d lanes_per_node=%2d  %.3f ms  %.3f ns per wave-load-instruction (chip)\n", whole, group,
-                   ms, ms * 1e6 / inst);
+            if (ms < best) best = ms;
         }
+        const double inst = (double)blocks * (threads / 64) * iters * 4;   // wave-level load instructions
+        const int distinct = sh ? 64 / group : active;
+        printf("%s\n  {\"active_lanes\": %d, \"lanes_per_node\": %d, \"nodes_per_instruction\": %d, \"ms\": %.4f, "
+               "\"wave_load_instructions\": %.0f, \"ginst_per_s\": %.3f, \"cycles_per_instruction_per_cu\": %.2f}",
+               first ? "" : ",", active, group, distinct, best, inst, inst / (best * 1e-3) / 1e9,
+               (best * 1e-3) * clk_khz * 1e3 * cus / inst);
+        first = false;
+    }
+    printf("\n]}\n");
     (void)hipFree(tab);
     (void)hipFree(out);
     return 0;

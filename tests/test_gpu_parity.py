@@ -680,6 +680,23 @@ def test_traversal_v02_alias(gpu, mirt):
         gpu.set_option(abi.OPT_TRAVERSAL, abi.TRAV_WAVEFRONT)
 
 
+def test_blocking_frame_into_registered_buffer(gpu, mirt, golden):
+    """mirt_render_frame into the caller's own malloc'd buffer after
+    mirt_host_register (main.c's frame buffer, page-locked in place): the
+    golden frame, twice; unregistered afterwards."""
+    s, b = _scene(mirt, "render", 10000)
+    gpu.upload(s, b)
+    page = np.zeros((1080, 1920, 4), np.uint8)
+    mirt.host_register(page)
+    try:
+        for _ in range(2):
+            page[:] = 0
+            gpu.render_frame_into(mirt.default_camera(), 1920, 1080, page, depth=5, seed=1)
+            assert sha(page) == golden["frames"]["1920x1080_render10000_d5_m1_b1_s1_c0_step1"]["sha"]
+    finally:
+        mirt.host_unregister(page)
+
+
 def test_cached_tree_renders_golden_frame(gpu, mirt, golden, tmp_path):
     """A scene uploaded from the tree cache file (mirt_bvh_build_flat_cached,
     second call = a load) renders the golden 1080p depth-5 frame."""
