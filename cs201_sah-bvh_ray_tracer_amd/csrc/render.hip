@@ -302,7 +302,7 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask)
 #define MIRT_HCACHE 16
 #endif
 constexpr uint32_t kHCache = MIRT_HCACHE;
-constexpr int kBounceDiag = 10;  // mirt_bounce_stats words per wave  // HNodes staged in LDS per bounce workgroup (64 B each)
+constexpr int kBounceDiag = 12;  // mirt_bounce_stats words per wave  // HNodes staged in LDS per bounce workgroup (64 B each)
 
 // The bounce queue's control words: {records written} in the first 128-B
 // line, then one read head per queue SEGMENT, each in its own line. The
@@ -593,6 +593,7 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
     uint64_t dg_it = 0, dg_lanes = 0, dg_it_x = 0, dg_lanes_x = 0, dg_tx = 0, dg_qit = 0, dg_tq = 0;
     const uint64_t dg_t0 = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
     uint32_t dg_steps = 0, dg_chain = 0, dg_walk_max = 0, dg_chain_max = 0;
+    uint64_t dg_seg = 0, dg_fb = 0;
     constexpr bool LANE4 = WALK == 2 || WALK == 4;  // four-wide, one ray per lane
     constexpr int cstride = 256;
     // the colour stack: one row per bounce level that can store a colour
@@ -687,7 +688,16 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                 }
                 if (has && w.walking()) dg_steps++;
             }
-            if (has && w.walking()) w.template step<FAST>(sc, sr, sp, pr, stk, best_t, best_s, cnt);
+            if constexpr (DIAG && LANE4) {
+                // lane-steps spent in a DFS-segment fallback (the lane stack
+                // would have overflowed), and the fallbacks entered
+                const bool seg0 = has && w.walking() && w.w.end != 0;
+                if (has && w.walking()) w.template step<FAST>(sc, sr, sp, pr, stk, best_t, best_s, cnt);
+                dg_seg += seg0 ? 1u : 0u;
+                dg_fb += (!seg0 && has && w.w.end != 0) ? 1u : 0u;
+            } else {
+                if (has && w.walking()) w.template step<FAST>(sc, sr, sp, pr, stk, best_t, best_s, cnt);
+            }
         }
         // shade every lane whose ray is done
         if (has && !w.walking()) {
@@ -783,6 +793,16 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
             d[7] = ((uint64_t)dg_chain_max << 32) | dg_walk_max;
             d[8] = dg_qit;
             d[9] = dg_tq;
+        }
+        // per-lane sums reduced over the wave
+        for (int o = 32; o; o >>= 1) {
+            dg_seg += (uint64_t)__shfl_xor((long long)dg_seg, o);
+            dg_fb += (uint64_t)__shfl_xor((long long)dg_fb, o);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            uint64_t* d = diag + kBounceDiag * (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+            d[10] = dg_seg;
+            d[11] = dg_fb;
         }
     }
 }
@@ -2237,7 +2257,7 @@ int mirt_bounce_stats(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc
     }
     const int waves = (c->bounce_blocks_opt ? c->bounce_blocks_opt : c->bounce_blocks) * 4;
     if (!out || cap < waves) return -waves;
-    static_assert(kBounceDiag == 10, "mirt.h documents 10 words per wave");
+    static_assert(kBounceDiag == 12, "mirt.h documents 12 words per wave");
     FrameConst f = make_frame_const(cam, fd);
     f.accumulate = 0;
     const size_t pixels = (size_t)f.num_rows * f.width;

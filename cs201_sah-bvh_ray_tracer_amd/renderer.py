@@ -329,12 +329,13 @@ class Renderer:
         """Per-wave diagnostic of the bounce kernel: uint64 array of (iterations,
         walking lanes summed, iterations after the queue ran dry, their lanes,
         t_start, t_dry, t_end [10 ns ticks], longest chain << 32 | longest walk,
-        quad-drain iterations, t_quad_start)."""
+        quad-drain iterations, t_quad_start, DFS-segment fallback lane-steps,
+        fallbacks entered)."""
         fd = frame_desc(width, height, depth, True, seed, sample, False, 1, 8, shard, num_shards)
         n = -self.L.mirt_bounce_stats(self.h, C.byref(cam), C.byref(fd), None, 0)
         if n <= 0:
             check(-n, "mirt_bounce_stats")
-        out = np.zeros((n, 10), np.uint64)
+        out = np.zeros((n, 12), np.uint64)
         check(self.L.mirt_bounce_stats(self.h, C.byref(cam), C.byref(fd), ptr(out), n), "mirt_bounce_stats")
         return out
 

@@ -341,12 +341,15 @@ int mirt_count_frame(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_des
 int mirt_wave_stats(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_desc *fd, uint32_t *out, int cap);
 
 /* Diagnostic: renders the frame (depth >= 2, BVH, wavefront schedule) with the
-   instrumented bounce kernel and writes 10 uint64 per bounce wave: loop
+   instrumented bounce kernel and writes 12 uint64 per bounce wave: loop
    iterations, walking lanes summed over them, the same two after the bounce
    queue ran dry, start / queue-dry / end time (100 MHz clock), longest
    chain << 32 | longest walk (steps) of the lane loop, quad-drain loop
-   iterations and the time the quad drain began (0: none). Returns the
-   number of waves (or -waves if cap is too small). */
+   iterations, the time the quad drain began (0: none), lane-steps of the
+   lane loop spent in DFS-segment fallbacks (a four-wide step whose pushes
+   would overflow the LDS lane stack walks the node's subtree in DFS order)
+   and the fallbacks entered. Returns the number of waves (or -waves if cap
+   is too small). */
 int mirt_bounce_stats(mirt_ctx *ctx, const mirt_camera *cam, const mirt_frame_desc *fd, uint64_t *out, int cap);
 
 /* The ctx's own stream (a hipStream_t, non-blocking): the blocking calls run

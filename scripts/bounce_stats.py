@@ -58,6 +58,9 @@ def report(r, cam, ns, a):
         "lanes_per_iter_before_dry": round(float((d[:, 1] - d[:, 3]).sum() / (d[:, 0] - d[:, 2]).sum()), 2),
         "lanes_per_iter_after_dry": round(float(d[:, 3].sum() / max(1.0, d[:, 2].sum())), 2),
         "iters_after_dry_frac": round(float(d[:, 2].sum() / d[:, 0].sum()), 3),
+        "lane_steps": int(d[:, 1].sum()),
+        "fallback_lane_steps": int(d[:, 10].sum()), "fallbacks": int(d[:, 11].sum()),
+        "fallback_share_of_lane_steps": round(float(d[:, 10].sum() / max(1.0, d[:, 1].sum())), 4),
         "longest_walk_p50": int(np.median(walk)), "longest_walk_max": int(walk.max()),
         "longest_chain_p50": int(np.median(chain)), "longest_chain_max": int(chain.max())}), flush=True)
 
