@@ -113,8 +113,13 @@ PIPELINE_MULTI, HW_QUEUES_MULTI = 8, 16
 TAIL_GRID = 0
 KERNEL = "bounce_kernel<true, 2, false>"   # dominant kernel of the default (wavefront, four-wide) schedule
 # the PMC-derived bound of the timed launch shape, per workload
-# (scripts/pmc_bench.sh over this script's own command + scripts/pmc_summary.py)
-PMC_BOUND = {wl: os.path.join(ROOT, "profiles", f"r03_pmc_bound_{wl}.json") for wl in WORKLOADS}
+# (scripts/pmc_bench.sh over this script's own command + scripts/pmc_summary.py);
+# the newest round's file wins
+PMC_BOUND = {wl: [os.path.join(ROOT, "profiles", f"r0{r}_pmc_bound_{wl}.json") for r in (4, 3)] for wl in WORKLOADS}
+# the chip's gather peak by access shape (scripts/td_probe.hip + its counter
+# passes, scripts/td_probe_summary.py): the roofline's denominator
+TD_PROBE = os.path.join(ROOT, "profiles", "r04_td_probe.json")
+WAVE_SLOTS = 256 * 4 * 5   # CUs x SIMDs x the bounce kernel's 5 waves per SIMD (amdgpu_waves_per_eu)
 
 
 def algorithmic_bytes(c, pixels):
@@ -379,14 +384,88 @@ def dry_main(args, world, rank):
 
 def load_pmc_bound(name):
     """The PMC-derived bound of the frame kernels of workload `name` in the
-    timed launch shape (profiles/r03_pmc_bound_<name>.json: scripts/pmc_bench.sh
+    timed launch shape (profiles/r0N_pmc_bound_<name>.json: scripts/pmc_bench.sh
     over `bench.py --workload name` + scripts/pmc_summary.py), or None."""
-    path = PMC_BOUND.get(name)
-    if not path or not os.path.exists(path):
+    for path in PMC_BOUND.get(name, []):
+        if os.path.exists(path):
+            with open(path) as f:
+                d = json.load(f)
+            if d.get("workload") == [W, H, NSPH, DEPTH]:
+                return d, path
+    return None, None
+
+
+def gather_peak(probe, tcp_per_inst):
+    """The chip's peak rate (G wave-load instructions/s) of dwordx4 gathers
+    whose instructions touch as many L1 lines as the kernel's do: linear
+    interpolation, in cycles per instruction, over the probe's one-node-per-
+    lane cases keyed by their measured TCP accesses per instruction."""
+    pts = sorted((c["tcp_accesses_per_instruction"], 1.0 / c["ginst_per_s"]) for c in probe["cases"]
+                 if c["lanes_per_node"] == 1 and "tcp_accesses_per_instruction" in c)
+    if not pts:
         return None, None
-    with open(path) as f:
-        d = json.load(f)
-    return (d, path) if d.get("workload") == [W, H, NSPH, DEPTH] else (None, None)
+    x = min(max(tcp_per_inst, pts[0][0]), pts[-1][0])
+    for (x0, y0), (x1, y1) in zip(pts, pts[1:]):
+        if x0 <= x <= x1:
+            y = y0 + (y1 - y0) * (x - x0) / max(x1 - x0, 1e-12)
+            return 1.0 / y, [(x0, round(1 / y0, 3)), (x1, round(1 / y1, 3))]
+    return 1.0 / pts[-1][1], [pts[-1]]
+
+
+def vmem_roofline(pmc, pmc_path, ms_per_step, frames_per_launch):
+    """roofline of the dominant kernel on the unit that binds it (VERDICT r3
+    item 1): the bounce kernel's vector-memory gather path. achieved = its
+    wave-level load instructions (SQ_INSTS_VMEM_RD) / its exclusive time
+    (GRBM_GUI_ACTIVE of the same counter pass, the timed launch shape);
+    peak = scripts/td_probe's chip rate for gathers of the same shape (TCP
+    accesses per load instruction). Recompute: counters and derived values
+    in the PMC file, the probe table in profiles/r04_td_probe.json."""
+    if not pmc or not os.path.exists(TD_PROBE):
+        return None
+    with open(TD_PROBE) as f:
+        probe = json.load(f)
+    kb = pmc["kernels"].get("timed/bounce", {})
+    kp = pmc["kernels"].get("timed/primary", {})
+    cb, db = kb.get("counters", {}), kb.get("derived", {})
+    cp, dp = kp.get("counters", {}), kp.get("derived", {})
+    if "SQ_INSTS_VMEM_RD" not in cb or "TCP_TOTAL_CACHE_ACCESSES_sum" not in cb or "kernel_ms_at_2400MHz" not in db:
+        return None
+    vmem, ms = cb["SQ_INSTS_VMEM_RD"], db["kernel_ms_at_2400MHz"]
+    tcp_per_inst = cb["TCP_TOTAL_CACHE_ACCESSES_sum"] / vmem
+    peak, bracket = gather_peak(probe, tcp_per_inst)
+    if not peak:
+        return None
+    achieved = vmem / (ms * 1e-3) / 1e9
+    share = min(1.0, cb.get("SQ_WAVES", WAVE_SLOTS) / WAVE_SLOTS)
+    vmem_step = (vmem + cp.get("SQ_INSTS_VMEM_RD", 0.0)) / frames_per_launch
+    step_rate = vmem_step / (ms_per_step * 1e-3) / 1e9
+    return {
+        "bound": "vmem", "achieved": round(achieved, 3), "peak": round(peak, 3), "unit": "Ginst/s",
+        "frac": round(achieved / peak, 4),
+        "traffic": db.get("hbm_bytes"),
+        "kernel_ms": ms,
+        "kernel_ms_source": "exclusive time of one bounce launch of the timed shape (GRBM_GUI_ACTIVE / 8 XCDs at "
+                            "2.4 GHz, median over the launches of the counter pass; rocprofv3 serialises the "
+                            "dispatches it counts)",
+        "kernel_ms_per_step_share": round(ms * share, 4),
+        "kernel_wave_slot_share": round(share, 4),
+        "definition": "the bounce kernel (hit.c:91-109's walk for the bounce rays) on its binding unit, the "
+                      "vector-memory gather path (TA/TD: per-lane dwordx4 loads of nodes, leaf records, spheres "
+                      "from an L2-resident tree): its wave-level load instructions per second of its own time, "
+                      "against the chip's peak rate for gathers touching the same number of L1 lines per "
+                      "instruction (scripts/td_probe.hip). kernel_ms_per_step_share = kernel_ms x the launch's "
+                      "waves / the chip's wave slots at 5 per SIMD: the frames in flight share the chip.",
+        "vmem_rd_per_launch": vmem, "tcp_accesses_per_instruction": round(tcp_per_inst, 3),
+        "peak_bracket": bracket, "td_busy": db.get("td_busy"), "ta_busy": db.get("ta_busy"),
+        "valu_busy": db.get("valu_busy"), "wait_any_per_wave_cycle": db.get("wait_any_per_wave_cycle"),
+        "primary_valu_busy": dp.get("valu_busy"), "primary_kernel_ms": dp.get("kernel_ms_at_2400MHz"),
+        "timed_loop": {"note": "the frame loop's gather path per step: both kernels' load instructions per frame "
+                               "/ ms_per_step, against the same peak (frames in flight hide the walk's latency "
+                               "that one launch alone cannot)",
+                       "vmem_rd_per_frame": vmem_step, "ginst_per_s": round(step_rate, 3),
+                       "frac": round(step_rate / peak, 4)},
+        "source": os.path.relpath(pmc_path, ROOT) + " + " + os.path.relpath(TD_PROBE, ROOT),
+    }
 
 
 def bound_line(pb, exec_b, ref_b, ms):
@@ -662,7 +741,16 @@ def main():
         pb = pmc["kernels"].get("timed/bounce", {}).get("derived", {}) if pmc else {}
         pp = pmc["kernels"].get("timed/primary", {}).get("derived", {}) if pmc else {}
         traffic = pb.get("hbm_bytes")
-        bm = bound_line(pb, exec_b, ref_b, bounce_ms)
+        bm = bound_line(pb, exec_b, ref_b, pb.get("kernel_ms_at_2400MHz") or bounce_ms)
+        kname = KERNEL.replace("<true, 2,", "<true, 4,") if r.get_option(mirt.abi.OPT_LEAF_BATCH) else KERNEL
+        roof = vmem_roofline(pmc, pmc_path, elapsed / args.steps * 1e3, per_launch)
+        if roof is None:
+            # no counter file for this workload: the roofline is not measured here (never priced against
+            # the HBM peak with the reference's bytes: VERDICT r3)
+            roof = {"bound": "vmem", "achieved": None, "peak": None, "unit": "Ginst/s", "frac": None,
+                    "traffic": traffic, "note": "no profiles/r0N_pmc_bound_<workload>.json or td_probe table for "
+                                                "this workload"}
+        roof["kernel"] = kname
         if bm:
             bm["source"] = (os.path.relpath(pmc_path, ROOT) + " (medians over the dispatches of the timed launch "
                             "shape, one rocprofv3 --pmc pass of this command per counter set; rocprofv3 serialises "
@@ -694,46 +782,47 @@ def main():
                                  "display in its own slab, launches rotating over `pipeline` ctxs",
                        "parallelism": f"row-block shard x{world}" + (" + RCCL gather of every frame" if world > 1
                                                                      else "")},
-            "roofline": {
-                "bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
-                "kernel": (KERNEL.replace("<true, 2,", "<true, 4,")
-                           if r.get_option(mirt.abi.OPT_LEAF_BATCH) else KERNEL),
-                "kernel_ms": round(bounce_ms, 4),
-                "kernel_ms_source": f"mean over the {len(timed_phases)} timed launches ({per_launch} frame(s) each) "
-                                    "of HIP events recorded on each launch's own stream around its bounce kernel "
-                                    "(mirt_phase_log): the launch's duration UNDER the timed loop's overlap of "
-                                    "`pipeline` launches",
-                "algorithmic_bytes_per_launch": int(ref_b),
-                "definition": "SURVEY 8(d): bytes of the REFERENCE's exhaustive DFS (hit.c:91-109, no pruning) "
-                              "for the bounce levels at 32 B/node test + 16 B/sphere test + 4 B/hit colour + "
-                              "4 B/pixel, / the bounce kernel's HIP-event time in the timed loop. The tree is "
-                              "L2/MALL-resident, so this effective rate is not HBM use. Measured HBM use and the "
-                              "unit that does bound the kernel: hbm_measured, bound_measured.",
+            "roofline": roof,
+            # SURVEY 8(d)'s figure, kept beside the roofline under its own name: the REFERENCE's work per
+            # second, not a use of any unit (it exceeds HBM peak because the walk skips most
+            # of it and the tree is cache-resident)
+            "reference_work": {
+                "definition": "SURVEY 8(d): bytes of the REFERENCE's exhaustive DFS (hit.c:91-109, no pruning) at "
+                              "32 B/node test + 16 B/sphere test + 4 B/hit colour + 4 B/pixel, per second. The "
+                              "walk executes a fraction of them (executed_vs_reference) from an L2/MALL-resident "
+                              "tree, so this is the reference's work replaced per second, not HBM use.",
+                "bounce_bytes_per_launch": int(ref_b),
+                "bounce_launch_ms_under_overlap": round(bounce_ms, 4),
+                "bounce_launch_ms_source": f"mean over the {len(timed_phases)} timed launches of HIP events on each "
+                                           "launch's own stream around its bounce kernel (mirt_phase_log): "
+                                           "durations UNDER the overlap of `pipeline` launches, so longer than "
+                                           "the kernel's share of a step",
+                "reference_work_gbs": round(achieved, 1),
+                "reference_work_vs_hbm_peak": round(achieved / PEAK_HBM_GBS, 4),
+                "executed_vs_reference_bytes": round(exec_b / max(ref_b, 1), 4),
                 "hbm_measured": None if traffic is None else {
-                    "bytes_per_launch": traffic, "gbs": round(traffic / (bounce_ms / 1e3) / 1e9, 2),
-                    "frac": round(traffic / (bounce_ms / 1e3) / 1e9 / PEAK_HBM_GBS, 5)},
+                    "bytes_per_launch": traffic,
+                    "gbs_over_exclusive_time": round(traffic / (pb["kernel_ms_at_2400MHz"] / 1e3) / 1e9, 2),
+                    "frac": round(traffic / (pb["kernel_ms_at_2400MHz"] / 1e3) / 1e9 / PEAK_HBM_GBS, 5)},
                 "bound_measured": bm,
-                "primary_kernel_ms": round(primary_ms, 4),
-                "primary_algorithmic_bytes": int(ref_frame_bytes - ref_b),
+                "primary_launch_ms_under_overlap": round(primary_ms, 4),
+                "primary_bytes_per_launch": int(ref_frame_bytes - ref_b),
                 "primary_bound_measured": bound_line(pp, exec_frame_bytes - exec_b, ref_frame_bytes - ref_b,
-                                                     primary_ms),
-                "launch_algorithmic_bytes": int(ref_frame_bytes),
+                                                     pp.get("kernel_ms_at_2400MHz") or primary_ms),
+                "launch_bytes": int(ref_frame_bytes),
                 "launch_executed_bytes": int(exec_frame_bytes),
                 "frame_period_ms": round(elapsed / args.steps * 1e3, 4),
-                "frame_algorithmic_gbs": round(ref_frame_bytes / batch / (elapsed / args.steps) / 1e9, 1),
+                "frame_reference_gbs": round(ref_frame_bytes / batch / (elapsed / args.steps) / 1e9, 1),
                 "job": {"note": "SURVEY 8(e): every rank's reference-DFS bytes over the timed launches / the "
-                                "max-over-ranks timed region, against n_gpus x the HBM peak",
-                        "algorithmic_bytes_per_launch": int(job_bytes_per_launch),
-                        "gbs": round(job_bytes_per_launch * len(timed_plan) / elapsed / 1e9, 1),
-                        "frac": round(job_bytes_per_launch * len(timed_plan) / elapsed / 1e9
-                                      / (world * PEAK_HBM_GBS), 4)},
+                                "max-over-ranks timed region",
+                        "bytes_per_launch": int(job_bytes_per_launch),
+                        "gbs": round(job_bytes_per_launch * len(timed_plan) / elapsed / 1e9, 1)},
                 "serial_launch": {
                     "note": "the same launch alone (untimed serial loop, the full persistent bounce grid): not "
                             "the timed configuration",
                     "frame_ms": round(kernel_ms, 4), "primary_ms": round(serial_primary_ms, 4),
                     "bounce_ms": round(serial_bounce_ms, 4),
-                    "bounce_achieved_gbs": round(ref_b / (serial_bounce_ms / 1e3) / 1e9, 1)}},
+                    "bounce_reference_gbs": round(ref_b / (serial_bounce_ms / 1e3) / 1e9, 1)}},
             "work": {k: int(v) for k, v in counts.items()},
             "work_reference_dfs": {k: int(v) for k, v in ref_counts.items() if k != "lane_steps"},
             "traced_rays_per_s_M": round(counts["rays"] * world / (elapsed / args.steps) / 1e6, 3),

@@ -50,11 +50,14 @@ def main():
                 print(lib, "bench failed", p.stderr[-1000:])
                 sys.exit(p.returncode)
             d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
-            rl = d["roofline"]
+            # round 4: the timed launches' HIP-event times live under reference_work
+            rl = d.get("reference_work") or d["roofline"]
             sl = rl.get("serial_launch", rl)      # bench.py before round 3 kept these at the top level
-            res[lib].append((d["value"], rl["kernel_ms"], rl["primary_kernel_ms"], sl["frame_ms"], d["depth1_mrays_s"]))
-            print(json.dumps({"lib": lib, "value": d["value"], "bounce_ms": rl["kernel_ms"],
-                              "primary_ms": rl["primary_kernel_ms"], "frame_ms": sl["frame_ms"],
+            b_ms = rl.get("bounce_launch_ms_under_overlap", rl.get("kernel_ms"))
+            p_ms = rl.get("primary_launch_ms_under_overlap", rl.get("primary_kernel_ms"))
+            res[lib].append((d["value"], b_ms, p_ms, sl["frame_ms"], d["depth1_mrays_s"]))
+            print(json.dumps({"lib": lib, "value": d["value"], "bounce_ms": b_ms,
+                              "primary_ms": p_ms, "frame_ms": sl["frame_ms"],
                               "serial_bounce_ms": sl.get("bounce_ms"), "serial_primary_ms": sl.get("primary_ms"),
                               "depth1": d["depth1_mrays_s"]}), flush=True)
     for lib, v in res.items():
