@@ -426,12 +426,14 @@ def vmem_roofline(pmc, pmc_path, ms_per_step, frames_per_launch):
         probe = json.load(f)
     kb = pmc["kernels"].get("timed/bounce", {})
     kp = pmc["kernels"].get("timed/primary", {})
-    cb, db = kb.get("counters", {}), kb.get("derived", {})
-    cp, dp = kp.get("counters", {}), kp.get("derived", {})
-    if "SQ_INSTS_VMEM_RD" not in cb or "TCP_TOTAL_CACHE_ACCESSES_sum" not in cb or "kernel_ms_at_2400MHz" not in db:
+    vb, db = kb.get("vmem_pass"), kb.get("derived", {})
+    vp, dp = kp.get("vmem_pass") or {}, kp.get("derived", {})
+    if not vb or not vb.get("tcp_accesses_per_instruction"):
         return None
-    vmem, ms = cb["SQ_INSTS_VMEM_RD"], db["kernel_ms_at_2400MHz"]
-    tcp_per_inst = cb["TCP_TOTAL_CACHE_ACCESSES_sum"] / vmem
+    # instructions, time and access shape from ONE counter pass
+    vmem, ms, tcp_per_inst = vb["SQ_INSTS_VMEM_RD"], vb["kernel_ms_at_2400MHz"], vb["tcp_accesses_per_instruction"]
+    cb = {"SQ_WAVES": vb.get("SQ_WAVES") or WAVE_SLOTS}
+    cp = {"SQ_INSTS_VMEM_RD": vp.get("SQ_INSTS_VMEM_RD", 0.0)}
     peak, bracket = gather_peak(probe, tcp_per_inst)
     if not peak:
         return None

@@ -4,7 +4,9 @@
 # per dispatch, so it serialises the dispatches it counts -- the counters
 # describe each kernel of the timed launch shape, not the overlap itself).
 # One small counter set per pass, each under its own kill timeout, within
-# 8 SQ / 4 TCC / 4 TCP / 2 TA / 2 TD / 2 GRBM counters:
+# 8 SQ / 4 TCC / 4 TCP / 2 TA / 2 TD / 2 GRBM counters. Set 1 carries the
+# roofline's numerator, its time and its access shape in ONE pass
+# (SQ_INSTS_VMEM_RD, GRBM_GUI_ACTIVE, TCP_TOTAL_CACHE_ACCESSES_sum):
 #   scripts/pmc_bench.sh <tag> [bench.py arguments]
 # Summarise: scripts/pmc_summary.py gpurun_out/<tag> --pattern 'bench.*' --bounce-grid 98304 --json ...
 set -u
@@ -13,7 +15,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/$1; shift
 mkdir -p "$OUT"
 SETS=(
- "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU"
+ "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU GRBM_GUI_ACTIVE TCP_TOTAL_CACHE_ACCESSES_sum"
  "TA_TA_BUSY_sum GRBM_GUI_ACTIVE"
  "TD_TD_BUSY_sum GRBM_GUI_ACTIVE"
  "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum"

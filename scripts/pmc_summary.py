@@ -17,6 +17,11 @@ the utilisations derived from them (MI355X_MICROARCH.md for the units):
   HBM bytes         FETCH_SIZE x 2 (gfx950 tallies a wide read at half) +
                     WRITE_SIZE, both KiB
   mean L2 latency   TCP_TCC_READ_REQ_LATENCY / TCP_TCC_READ_REQ (cycles)
+  vmem_pass         from the ONE pass holding SQ_INSTS_VMEM_RD, GRBM_GUI_ACTIVE and
+                    TCP_TOTAL_CACHE_ACCESSES_sum: the kernel's wave-level load
+                    instructions, its exclusive time and its L1 accesses per load
+                    instruction (bench.py's roofline: / the gather peak of the same
+                    access shape, profiles/r04_td_probe.json)
 """
 import argparse
 import collections
@@ -118,12 +123,30 @@ def main():
                 names[kern] = r["Kernel_Name"]
         for (kern, k), v in acc.items():
             e = cfgs[cfg + "/" + kern]
-            e.setdefault("counters", {})[k] = statistics.median(v)
-            e.setdefault("launches", {})[k] = len(v)
+            e.setdefault("_all", collections.defaultdict(list))[k] += v
+            # each pass on its own too: values that must come from ONE pass
+            # (the vmem roofline: instructions, time and access shape) are
+            # read from the pass that holds SQ_INSTS_VMEM_RD
+            e.setdefault("passes", {}).setdefault(os.path.basename(d), {})[k] = statistics.median(v)
             e["kernel"] = names[kern]
+    for e in cfgs.values():
+        allv = e.pop("_all")
+        e["counters"] = {k: statistics.median(v) for k, v in allv.items()}
+        e["launches"] = {k: len(v) for k, v in allv.items()}
     out = {}
     for cfg, e in sorted(cfgs.items()):
         e["derived"] = derive(e["counters"])
+        vp = [p for p in e.get("passes", {}).values() if "SQ_INSTS_VMEM_RD" in p and "GRBM_GUI_ACTIVE" in p]
+        if vp:
+            p = vp[0]
+            g = p["GRBM_GUI_ACTIVE"] / XCDS
+            e["vmem_pass"] = {
+                "SQ_INSTS_VMEM_RD": p["SQ_INSTS_VMEM_RD"], "GRBM_GUI_ACTIVE": p["GRBM_GUI_ACTIVE"],
+                "TCP_TOTAL_CACHE_ACCESSES_sum": p.get("TCP_TOTAL_CACHE_ACCESSES_sum"), "SQ_WAVES": p.get("SQ_WAVES"),
+                "kernel_ms_at_2400MHz": round(g / CLOCK_HZ * 1e3, 4),
+                "vmem_ginst_per_s": round(p["SQ_INSTS_VMEM_RD"] / (g / CLOCK_HZ) / 1e9, 3),
+                "tcp_accesses_per_instruction": round(p["TCP_TOTAL_CACHE_ACCESSES_sum"] / p["SQ_INSTS_VMEM_RD"], 3)
+                if p.get("TCP_TOTAL_CACHE_ACCESSES_sum") else None}
         out[cfg] = e
         print(cfg, e["kernel"][:80])
         for k, v in sorted(e["derived"].items()):
