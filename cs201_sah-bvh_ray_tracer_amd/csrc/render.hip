@@ -494,12 +494,17 @@ struct BounceWalk<0> {
     __device__ bool walking() const { return w.cur != kPNone; }
     template <bool FAST>
     __device__ void step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr, uint32_t*, float& bt,
-                         int& bs, Counters& cnt)
+                         int& bs, Counters& cnt, NodePf* = nullptr)
     {
         lane_step<FAST, false>(sc, sr, sp, pr, w.cur, bt, bs, cnt);
         if (w.cur >= w.end) w.cur = kPNone;
     }
 };
+// MIRT_NODE_PREFETCH (WALK 2): request the next step's node before the
+// step's leaf gates (trace.h NodePf); A/B in DESIGN §8 (round 4)
+#ifndef MIRT_NODE_PREFETCH
+#define MIRT_NODE_PREFETCH 1
+#endif
 template <int WALK>
 struct WideBounceWalk {  // WALK 2: four-wide; 4: four-wide, a step's leaf spheres loaded together
     WideWalk w;
@@ -510,9 +515,10 @@ struct WideBounceWalk {  // WALK 2: four-wide; 4: four-wide, a step's leaf spher
     __device__ bool walking() const { return wide_walking(w); }
     template <bool FAST>
     __device__ void step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr, uint32_t* stk,
-                         float& bt, int& bs, Counters& cnt)
+                         float& bt, int& bs, Counters& cnt, NodePf* pf = nullptr)
     {
-        wide_lane_step<FAST, false, WALK == 4>(sc, sr, sp, pr, w, stk, bt, bs, cnt, hc, hc_n);
+        wide_lane_step<FAST, false, WALK == 4>(sc, sr, sp, pr, w, stk, bt, bs, cnt, hc, hc_n,
+                                               (MIRT_NODE_PREFETCH && WALK == 2) ? pf : nullptr);
     }
 };
 template <>
@@ -673,6 +679,9 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
         if (DIAG && exhausted && !dg_tx) dg_tx = __builtin_amdgcn_s_memrealtime();
         if (LANE4 && quad_drain && exhausted && __popcll(__ballot(has)) <= 16) break;  // -> quad drain
         // walk until few lanes are still walking and the others can make progress
+        // (pf: the node the last step requested for the next; lives in this loop only)
+        NodePf pf;
+        pf.valid = false;
         for (;;) {
             const uint64_t walking = __ballot(has && w.walking());
             if (!walking) break;
@@ -692,11 +701,11 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                 // lane-steps spent in a DFS-segment fallback (the lane stack
                 // would have overflowed), and the fallbacks entered
                 const bool seg0 = has && w.walking() && w.w.end != 0;
-                if (has && w.walking()) w.template step<FAST>(sc, sr, sp, pr, stk, best_t, best_s, cnt);
+                if (has && w.walking()) w.template step<FAST>(sc, sr, sp, pr, stk, best_t, best_s, cnt, &pf);
                 dg_seg += seg0 ? 1u : 0u;
                 dg_fb += (!seg0 && has && w.w.end != 0) ? 1u : 0u;
             } else {
-                if (has && w.walking()) w.template step<FAST>(sc, sr, sp, pr, stk, best_t, best_s, cnt);
+                if (has && w.walking()) w.template step<FAST>(sc, sr, sp, pr, stk, best_t, best_s, cnt, &pf);
             }
         }
         // shade every lane whose ray is done

@@ -15,8 +15,11 @@ while [ $# -ge 2 ]; do
     for f in host_scene bvh_build bvh_cache dropin; do
         /opt/rocm/bin/hipcc $common -c "$CSRC/$f.cpp" -o "$obj/$f.o" &
     done
-    /opt/rocm/bin/hipcc $common --offload-arch=gfx950 -c "$CSRC/render.hip" -o "$obj/render.o" &
+    for f in render multi; do
+        /opt/rocm/bin/hipcc $common --offload-arch=gfx950 -c "$CSRC/$f.hip" -o "$obj/$f.o" &
+    done
     wait
-    /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$ROOT/ab/libmirt_$name.so" "$obj"/*.o
+    /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$ROOT/ab/libmirt_$name.so" "$obj"/*.o \
+        -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
     echo "ab/libmirt_$name.so ($flags)"
 done
