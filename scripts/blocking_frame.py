@@ -6,7 +6,9 @@ SDL_RenderPresent) through the blocking call, by destination (VERDICT r3
   registered    the same numpy array after mirt_host_register (page-locked in
                 place: the D2H is one DMA into the caller's own buffer)
   pinned        mirt_render_frame into mirt_host_alloc memory
-  kernels       the frame's kernels alone into device memory (the floor)
+  kernels       the frame's kernels alone into device memory (one launch)
+  bands         MIRT_OPT_BANDS 1..8 (default 4): the blocking frame as contiguous
+                row bands traced at once, each band's copy behind its own kernels
 
 1080p / 10k depth 5 (bench.py's workload), median of 21 calls each, every
 frame checked against the first. Prints one JSON line.
@@ -47,11 +49,24 @@ def main():
             dts.append(time.perf_counter() - t0)
         return sorted(dts)[len(dts) // 2] * 1e3
 
+    r.set_option(m.abi.OPT_BANDS, 1)
     ref = r.render_frame(cam, W, H, depth=5, seed=1)
     out = {"workload": "1920x1080, 10000 spheres, depth 5 (blocking mirt_render_frame per frame)"}
+    # MIRT_OPT_BANDS: the frame as contiguous row bands traced at once, each copied when done
+    bands = {}
     page = np.zeros((H, W, 4), np.uint8)
+    hb = m.HostBuffer((H, W, 4))
+    ok = True
+    for nb in (1, 2, 3, 4, 6, 8):
+        r.set_option(m.abi.OPT_BANDS, nb)
+        bands[nb] = {"pageable_ms": round(med(lambda: r.render_frame_into(cam, W, H, page, depth=5, seed=1)), 4),
+                     "pinned_ms": round(med(lambda: r.render_frame_into(cam, W, H, hb.array, depth=5, seed=1)), 4)}
+        ok = ok and bool((page == ref).all()) and bool((hb.array == ref).all())
+    hb.close()
+    out["bands"] = bands
+    r.set_option(m.abi.OPT_BANDS, 4)
     out["pageable_ms"] = med(lambda: r.render_frame_into(cam, W, H, page, depth=5, seed=1))
-    ok = bool((page == ref).all())
+    ok = ok and bool((page == ref).all())
     m.host_register(page)
     try:
         out["registered_ms"] = med(lambda: r.render_frame_into(cam, W, H, page, depth=5, seed=1))
