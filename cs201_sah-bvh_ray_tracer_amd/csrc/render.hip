@@ -494,17 +494,12 @@ struct BounceWalk<0> {
     __device__ bool walking() const { return w.cur != kPNone; }
     template <bool FAST>
     __device__ void step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr, uint32_t*, float& bt,
-                         int& bs, Counters& cnt, NodePf* = nullptr)
+                         int& bs, Counters& cnt)
     {
         lane_step<FAST, false>(sc, sr, sp, pr, w.cur, bt, bs, cnt);
         if (w.cur >= w.end) w.cur = kPNone;
     }
 };
-// MIRT_NODE_PREFETCH (WALK 2): request the next step's node before the
-// step's leaf gates (trace.h NodePf); A/B in DESIGN §8 (round 4)
-#ifndef MIRT_NODE_PREFETCH
-#define MIRT_NODE_PREFETCH 1
-#endif
 template <int WALK>
 struct WideBounceWalk {  // WALK 2: four-wide; 4: four-wide, a step's leaf spheres loaded together
     WideWalk w;
@@ -515,10 +510,9 @@ struct WideBounceWalk {  // WALK 2: four-wide; 4: four-wide, a step's leaf spher
     __device__ bool walking() const { return wide_walking(w); }
     template <bool FAST>
     __device__ void step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr, uint32_t* stk,
-                         float& bt, int& bs, Counters& cnt, NodePf* pf = nullptr)
+                         float& bt, int& bs, Counters& cnt)
     {
-        wide_lane_step<FAST, false, WALK == 4>(sc, sr, sp, pr, w, stk, bt, bs, cnt, hc, hc_n,
-                                               (MIRT_NODE_PREFETCH && WALK == 2) ? pf : nullptr);
+        wide_lane_step<FAST, false, WALK == 4>(sc, sr, sp, pr, w, stk, bt, bs, cnt, hc, hc_n);
     }
 };
 template <>
@@ -679,9 +673,6 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
         if (DIAG && exhausted && !dg_tx) dg_tx = __builtin_amdgcn_s_memrealtime();
         if (LANE4 && quad_drain && exhausted && __popcll(__ballot(has)) <= 16) break;  // -> quad drain
         // walk until few lanes are still walking and the others can make progress
-        // (pf: the node the last step requested for the next; lives in this loop only)
-        NodePf pf;
-        pf.valid = false;
         for (;;) {
             const uint64_t walking = __ballot(has && w.walking());
             if (!walking) break;
@@ -701,11 +692,11 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                 // lane-steps spent in a DFS-segment fallback (the lane stack
                 // would have overflowed), and the fallbacks entered
                 const bool seg0 = has && w.walking() && w.w.end != 0;
-                if (has && w.walking()) w.template step<FAST>(sc, sr, sp, pr, stk, best_t, best_s, cnt, &pf);
+                if (has && w.walking()) w.template step<FAST>(sc, sr, sp, pr, stk, best_t, best_s, cnt);
                 dg_seg += seg0 ? 1u : 0u;
                 dg_fb += (!seg0 && has && w.w.end != 0) ? 1u : 0u;
             } else {
-                if (has && w.walking()) w.template step<FAST>(sc, sr, sp, pr, stk, best_t, best_s, cnt, &pf);
+                if (has && w.walking()) w.template step<FAST>(sc, sr, sp, pr, stk, best_t, best_s, cnt);
             }
         }
         // shade every lane whose ray is done
@@ -2228,15 +2219,18 @@ int render_banded(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd
         }
         alias_scene(c->band[sb - 1], c);
     }
+    // the bands share the chip: together about one full persistent bounce grid
     const int keep = c->bounce_blocks_opt;
-    const int blocks = (3 * std::max(1, c->num_cus)) / 2;
+    const int blocks = std::max(c->num_cus, (keep ? keep : c->bounce_blocks) / nb);
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
     c->timed_recorded = true;
     HIP_TRY(hipEventRecord(c->band_start, c->stream));   // after the accumulation buffer's (re)start
+    // every band's kernels first, then the copies: a copy into pageable
+    // memory can hold the host thread until it is done, which would
+    // otherwise delay the next band's launch
     for (int sb = 0; sb < nb; sb++) {
         mirt_ctx* x = sb ? c->band[sb - 1] : c;
-        const hipStream_t st = x->stream;
-        if (sb) HIP_TRY(hipStreamWaitEvent(st, c->band_start, 0));
+        if (sb) HIP_TRY(hipStreamWaitEvent(x->stream, c->band_start, 0));
         mirt_frame_desc bd = *fd;
         bd.row_block = rb;
         bd.shard = sb;
@@ -2244,14 +2238,19 @@ int render_banded(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd
         bd.samples = 1;
         const FrameConst f = make_frame_const(cam, &bd);
         const size_t off = (size_t)sb * rb * W;
-        x->bounce_blocks_opt = keep ? keep : blocks;
-        rc = launch_render(x, f, c->d_out + off, c->acc->d_acc ? c->acc->d_acc + 3 * off : nullptr, st, false,
+        x->bounce_blocks_opt = blocks;
+        rc = launch_render(x, f, c->d_out + off, c->acc->d_acc ? c->acc->d_acc + 3 * off : nullptr, x->stream, false,
                            nullptr);
-        x->bounce_blocks_opt = sb ? x->bounce_blocks_opt : keep;
+        c->bounce_blocks_opt = keep;
         if (rc) return rc;
-        HIP_TRY(hipMemcpyAsync(out + off, c->d_out + off, (size_t)f.shard_rows * W * 4, hipMemcpyDeviceToHost, st));
+    }
+    for (int sb = 0; sb < nb; sb++) {
+        mirt_ctx* x = sb ? c->band[sb - 1] : c;
+        const size_t off = (size_t)sb * rb * W;
+        const int rows = std::min(rb, H - sb * rb);
+        HIP_TRY(hipMemcpyAsync(out + off, c->d_out + off, (size_t)rows * W * 4, hipMemcpyDeviceToHost, x->stream));
         if (sb) {
-            HIP_TRY(hipEventRecord(c->band_done[sb], st));
+            HIP_TRY(hipEventRecord(c->band_done[sb], x->stream));
             HIP_TRY(hipStreamWaitEvent(c->stream, c->band_done[sb], 0));
         }
     }

@@ -1002,34 +1002,17 @@ __device__ __forceinline__ void leaf_gate(const DevScene& sc, const SlabRay& sr,
     }
 }
 
-// The next step's node, requested before this step's leaf gates (NodePf):
-// the walk is a chain of dependent round trips (node -> slot tests -> leaf
-// sphere -> gate -> next node), so a step with leaf gates paid two in a row;
-// with the next node in flight while the gates' spheres come back it pays
-// about one. Pure data movement: the next step still tests the node against
-// the prune state the gates leave.
-#ifndef MIRT_PF_WORDS
-#define MIRT_PF_WORDS 4   // dwordx4 of the next node requested early: 4 (all) or 2 (the first two slots)
-#endif
-struct NodePf {
-    uint4 a, b, c, d;
-    bool valid;
-};
-
 // hc / hc_n: the first hc_n HNodes (the tree's top levels, visited by
 // every ray) staged in LDS by the caller; a node there is read from LDS
 // instead of through the vector-memory path (the bounce kernel's busiest
 // unit, TD: its cost is the bytes returned per lane, however coalesced).
-// pf (non-null): the node prefetched by the previous step, and this step's
-// prefetch of the next one (not for nodes in LDS, nor in a DFS segment).
 template <bool FAST, bool COUNT, bool BATCH = false>
 __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
                                                WideWalk& w, uint32_t* stk, float& best_t, int& best_s, Counters& cnt,
-                                               lds_uint4* hc = nullptr, uint32_t hc_n = 0, NodePf* pf = nullptr)
+                                               lds_uint4* hc = nullptr, uint32_t hc_n = 0)
 {
     if (COUNT) cnt.steps++;
     if (w.end) {
-        if (pf) pf->valid = false;
         lane_step<FAST, COUNT, true>(sc, sr, sp, pr, w.cur, best_t, best_s, cnt);
         if (w.cur >= w.end) {
             w.end = 0;
@@ -1044,18 +1027,7 @@ __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay
     uint4 q3;  // the slots' references
     {
         uint4 s0, s1, s2, s3;
-        if (pf && pf->valid && MIRT_PF_WORDS >= 4) {
-            s0 = pf->a;
-            s1 = pf->b;
-            s2 = pf->c;
-            s3 = pf->d;
-        } else if (pf && pf->valid && MIRT_PF_WORDS == 2) {
-            const uint4* p = (const uint4*)(sc.hnodes + w.cur);
-            s0 = pf->a;
-            s1 = pf->b;
-            s2 = p[2];
-            s3 = p[3];
-        } else if (w.cur < hc_n) {
+        if (w.cur < hc_n) {
             lds_uint4* p = hc + 4 * w.cur;
             s0 = lds_load(p);
             s1 = lds_load(p + 1);
@@ -1114,19 +1086,6 @@ __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay
         if (n >= 4) stk[(w.top + n - 4) * kWideStride] = a3;
         w.top += n - 1;
         w.cur = a0;
-    }
-    if (pf) {
-        // the next node requested now, so its round trip overlaps the gates'
-        pf->valid = w.cur != kPNone && !w.end && w.cur >= hc_n;
-        if (pf->valid) {
-            const uint4* p = (const uint4*)(sc.hnodes + w.cur);
-            pf->a = p[0];
-            pf->b = p[1];
-            if (MIRT_PF_WORDS >= 4) {
-                pf->c = p[2];
-                pf->d = p[3];
-            }
-        }
     }
     // 3. passing leaf slots (the node's boxes are dead here): each lane works
     // through its own list, so the gate code runs max-over-lanes times
