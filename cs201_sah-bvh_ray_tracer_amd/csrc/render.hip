@@ -1194,10 +1194,7 @@ struct AccumShare {
 #ifndef MIRT_LEAF_BATCH_DEFAULT
 #define MIRT_LEAF_BATCH_DEFAULT 2
 #endif
-#ifndef MIRT_BANDS_DEFAULT
-#define MIRT_BANDS_DEFAULT 4
-#endif
-constexpr int kMaxBands = 8;
+
 struct mirt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -1266,14 +1263,6 @@ struct mirt_ctx {
     unsigned long long* d_keys = nullptr;  // chunked brute force: per-ray (t, index) keys
     size_t keys_cap = 0;
     int num_cus = 0;
-    // banded blocking frames (MIRT_OPT_BANDS): the frame split into contiguous
-    // row bands traced at once on this ctx and band contexts (their own
-    // stream and frame scratch, THIS ctx's scene), each band copied to the
-    // host as soon as it is done
-    int bands = MIRT_BANDS_DEFAULT;
-    mirt_ctx* band[kMaxBands - 1] = {};
-    hipEvent_t band_start = nullptr, band_done[kMaxBands] = {};
-    bool alias = false;         // the scene buffers belong to another ctx (a band ctx): not freed here
 };
 
 namespace {
@@ -1906,26 +1895,6 @@ void mirt_destroy(mirt_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (mirt_ctx*& b : c->band) {
-        mirt_destroy(b);
-        b = nullptr;
-    }
-    (void)hipSetDevice(c->device);
-    if (c->band_start) (void)hipEventDestroy(c->band_start);
-    for (hipEvent_t ev : c->band_done)
-        if (ev) (void)hipEventDestroy(ev);
-    if (c->alias) {
-        // the parent's scene: not ours to free
-        c->d_nodes = nullptr;
-        c->d_nodes32 = nullptr;
-        c->d_geo = nullptr;
-        c->d_color = nullptr;
-        c->d_pnodes = nullptr;
-        c->d_hnodes = nullptr;
-        c->d_haux = nullptr;
-        c->d_leaves = nullptr;
-        c->d_ndepth = nullptr;
-    }
     accum_release(c->acc);
     for (void* p : {(void*)c->d_nodes, (void*)c->d_nodes32, (void*)c->d_geo, (void*)c->d_color, (void*)c->d_out,
                     c->d_in, c->d_res, (void*)c->d_counts, (void*)c->d_defer, c->d_queue, (void*)c->d_keys, (void*)c->d_pnodes,
@@ -2134,138 +2103,8 @@ int ctx_device(const mirt_ctx* c) { return c->device; }
 
 extern "C" {
 
-namespace {
-
-// A band ctx sees the parent's scene and schedule (re-aliased before every
-// banded frame, so a new upload or option on the parent carries over).
-void alias_scene(mirt_ctx* b, const mirt_ctx* c)
-{
-    b->alias = true;
-    b->d_nodes = c->d_nodes;
-    b->d_nodes32 = c->d_nodes32;
-    b->d_geo = c->d_geo;
-    b->d_color = c->d_color;
-    b->num_nodes = c->num_nodes;
-    b->num_spheres = c->num_spheres;
-    b->d_pnodes = c->d_pnodes;
-    b->d_hnodes = c->d_hnodes;
-    b->d_haux = c->d_haux;
-    b->d_leaves = c->d_leaves;
-    b->d_ndepth = c->d_ndepth;
-    b->num_hnodes = c->num_hnodes;
-    b->wide_root = c->wide_root;
-    b->prune_ok = c->prune_ok;
-    b->ordered_ok = c->ordered_ok;
-    b->r_max = c->r_max;
-    b->c_max = c->c_max;
-    b->leaf_big = c->leaf_big;
-    b->trav = c->trav;
-    b->fast_slab = c->fast_slab;
-    b->block_waves = c->block_waves;
-    b->defer = c->defer;
-    b->prune = c->prune;
-    b->ordered = c->ordered;
-    b->bounce_threshold = c->bounce_threshold;
-    b->quad_drain = c->quad_drain;
-    b->primary_depth1 = c->primary_depth1;
-    b->leaf_batch_opt = c->leaf_batch_opt;
-}
-
-// Whether mirt_render_frame splits this frame into bands: a whole frame
-// (not a shard, one sample) of at least 512k pixels, on a ctx whose
-// accumulation is its own, with >= 8 rows per band.
-bool banded(const mirt_ctx* c, const mirt_frame_desc* fd)
-{
-    return c && c->bands > 1 && frame_desc_valid(fd) && fd->num_shards == 1 && fd->samples <= 1 && !accum_chain(c) &&
-           (size_t)fd->width * fd->height >= ((size_t)1 << 19) && fd->height >= 8 * c->bands && c->num_spheres >= 0;
-}
-
-// The blocking frame as `bands` contiguous row bands traced at once: band s
-// is shard s of num_shards = bands with row_block = the band height, so its
-// compact rows ARE image rows s * rb .. and its pixels, accumulation and RNG
-// keys sit at the full frame's offsets (a band renders exactly the frame's
-// bytes for its rows). Each band's kernels run on its own stream (band 0 on
-// the ctx's) with 1.5 persistent bounce workgroups per CU, as frames in
-// flight do, and its D2H copy follows on the same stream, so the copies of
-// finished bands overlap the last band's tail (the reference's
-// one-frame-at-a-time loop, main.c:350-421, pays render + copy per frame).
-int render_banded(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, mirt_rgba8* out)
-{
-    if (!ctx_ok(c, true, "mirt_render_frame")) return MIRT_E_NOSCENE;
-    if (!cam || !out) {
-        set_error("mirt_render_frame: invalid arguments");
-        return MIRT_E_INVALID;
-    }
-    if (fd->use_bvh && c->num_nodes == 0) {
-        set_error("mirt_render_frame: use_bvh set but no tree uploaded");
-        return MIRT_E_NOSCENE;
-    }
-    const int W = fd->width, H = fd->height;
-    const int rb = ((H + c->bands - 1) / c->bands + 7) / 8 * 8;
-    const int nb = (H + rb - 1) / rb;
-    const size_t pixels = (size_t)W * H;
-    int rc = ensure((void**)&c->d_out, &c->out_cap, pixels * 4 + 4);
-    if (rc) return rc;
-    rc = accum_prepare(c->acc, pixels, c->stream);
-    if (rc) return rc;
-    if (!c->band_start) HIP_TRY(hipEventCreateWithFlags(&c->band_start, hipEventDisableTiming));
-    for (int sb = 0; sb < nb; sb++)
-        if (!c->band_done[sb]) HIP_TRY(hipEventCreateWithFlags(&c->band_done[sb], hipEventDisableTiming));
-    for (int sb = 1; sb < nb; sb++) {
-        if (!c->band[sb - 1]) {
-            rc = mirt_create(c->device, &c->band[sb - 1]);
-            if (rc) return rc;
-            (void)hipSetDevice(c->device);
-        }
-        alias_scene(c->band[sb - 1], c);
-    }
-    // the bands share the chip: together about one full persistent bounce grid
-    const int keep = c->bounce_blocks_opt;
-    const int blocks = std::max(c->num_cus, (keep ? keep : c->bounce_blocks) / nb);
-    HIP_TRY(hipEventRecord(c->ev0, c->stream));
-    c->timed_recorded = true;
-    HIP_TRY(hipEventRecord(c->band_start, c->stream));   // after the accumulation buffer's (re)start
-    // every band's kernels first, then the copies: a copy into pageable
-    // memory can hold the host thread until it is done, which would
-    // otherwise delay the next band's launch
-    for (int sb = 0; sb < nb; sb++) {
-        mirt_ctx* x = sb ? c->band[sb - 1] : c;
-        if (sb) HIP_TRY(hipStreamWaitEvent(x->stream, c->band_start, 0));
-        mirt_frame_desc bd = *fd;
-        bd.row_block = rb;
-        bd.shard = sb;
-        bd.num_shards = nb;
-        bd.samples = 1;
-        const FrameConst f = make_frame_const(cam, &bd);
-        const size_t off = (size_t)sb * rb * W;
-        x->bounce_blocks_opt = blocks;
-        rc = launch_render(x, f, c->d_out + off, c->acc->d_acc ? c->acc->d_acc + 3 * off : nullptr, x->stream, false,
-                           nullptr);
-        c->bounce_blocks_opt = keep;
-        if (rc) return rc;
-    }
-    for (int sb = 0; sb < nb; sb++) {
-        mirt_ctx* x = sb ? c->band[sb - 1] : c;
-        const size_t off = (size_t)sb * rb * W;
-        const int rows = std::min(rb, H - sb * rb);
-        HIP_TRY(hipMemcpyAsync(out + off, c->d_out + off, (size_t)rows * W * 4, hipMemcpyDeviceToHost, x->stream));
-        if (sb) {
-            HIP_TRY(hipEventRecord(c->band_done[sb], x->stream));
-            HIP_TRY(hipStreamWaitEvent(c->stream, c->band_done[sb], 0));
-        }
-    }
-    c->bounce_blocks_opt = keep;
-    HIP_TRY(hipEventRecord(c->ev1, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    HIP_TRY(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
-    return MIRT_OK;
-}
-
-}  // namespace
-
 int mirt_render_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, mirt_rgba8* out)
 {
-    if (banded(c, fd)) return render_banded(c, cam, fd, out);
     if (int rc = enqueue_host_frame(c, cam, fd, out, "mirt_render_frame")) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));
     HIP_TRY(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
@@ -2773,10 +2612,6 @@ int mirt_set_option(mirt_ctx* c, int option, int value)
         if (value != 1 && value != 2 && value != 4 && value != 8) break;
         c->block_waves = value;
         return MIRT_OK;
-    case MIRT_OPT_BANDS:
-        if (value < 1 || value > kMaxBands) break;
-        c->bands = value;
-        return MIRT_OK;
     default:
         break;
     }
@@ -2797,7 +2632,6 @@ int mirt_get_option(mirt_ctx* c, int option)
     if (option == MIRT_OPT_BOUNCE_BLOCKS) return c->bounce_blocks_opt;
     if (option == MIRT_OPT_QUAD_DRAIN) return c->quad_drain;
     if (option == MIRT_OPT_QUAD_BATCH) return c->quad_batch;
-    if (option == MIRT_OPT_BANDS) return c->bands;
     if (option == MIRT_OPT_LEAF_BATCH) return leaf_batch(c) ? 1 : 0;  // in effect for the uploaded scene
     set_error("mirt_get_option: bad option %d", option);
     return MIRT_E_INVALID;

@@ -407,14 +407,9 @@ enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3,
                                        together: 0 never, 1 always, 2 (default) when the tree's
                                        four-wide layout exceeds the chip's 32 MiB of L2;
                                        mirt_get_option reads back 0/1: in effect for the scene) */
-       MIRT_OPT_QUAD_BATCH = 15,    /* mirt_intersect_rays / mirt_any_hit_rays with the BVH: 1
+       MIRT_OPT_QUAD_BATCH = 15     /* mirt_intersect_rays / mirt_any_hit_rays with the BVH: 1
                                        (default) = a batch too small to fill the chip one ray per
-                                       lane walks one ray per four lanes (benchmark.c's 10k rays) */
-       MIRT_OPT_BANDS = 16          /* blocking mirt_render_frame of a whole frame (>= 512k pixels,
-                                       the ctx's own accumulation): traced as this many contiguous
-                                       row bands at once (1..8, default 4; 1 = one launch), each
-                                       band copied to the host as soon as it is done, so the copy
-                                       overlaps the other bands' tails. Same bytes either way. */ };
+                                       lane walks one ray per four lanes (benchmark.c's 10k rays) */ };
 /* Traversal ids keep their first-release values (mirt 0.1: TILE 0, WAVEFRONT 5).
    ABI note: the mirt 0.2 header numbered WAVEFRONT 1; mirt_set_option accepts
    1 as a deprecated alias of MIRT_TRAV_WAVEFRONT (mirt_get_option reads back

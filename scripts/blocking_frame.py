@@ -7,8 +7,8 @@ SDL_RenderPresent) through the blocking call, by destination (VERDICT r3
                 place: the D2H is one DMA into the caller's own buffer)
   pinned        mirt_render_frame into mirt_host_alloc memory
   kernels       the frame's kernels alone into device memory (one launch)
-  bands         MIRT_OPT_BANDS 1..8 (default 4): the blocking frame as contiguous
-                row bands traced at once, each band's copy behind its own kernels
+  zero_copy     the kernels write the frame straight into page-locked host
+                memory (mirt_render_frame_device with a host pointer): no copy
 
 1080p / 10k depth 5 (bench.py's workload), median of 21 calls each, every
 frame checked against the first. Prints one JSON line.
@@ -49,22 +49,10 @@ def main():
             dts.append(time.perf_counter() - t0)
         return sorted(dts)[len(dts) // 2] * 1e3
 
-    r.set_option(m.abi.OPT_BANDS, 1)
     ref = r.render_frame(cam, W, H, depth=5, seed=1)
     out = {"workload": "1920x1080, 10000 spheres, depth 5 (blocking mirt_render_frame per frame)"}
-    # MIRT_OPT_BANDS: the frame as contiguous row bands traced at once, each copied when done
-    bands = {}
     page = np.zeros((H, W, 4), np.uint8)
-    hb = m.HostBuffer((H, W, 4))
     ok = True
-    for nb in (1, 2, 3, 4, 6, 8):
-        r.set_option(m.abi.OPT_BANDS, nb)
-        bands[nb] = {"pageable_ms": round(med(lambda: r.render_frame_into(cam, W, H, page, depth=5, seed=1)), 4),
-                     "pinned_ms": round(med(lambda: r.render_frame_into(cam, W, H, hb.array, depth=5, seed=1)), 4)}
-        ok = ok and bool((page == ref).all()) and bool((hb.array == ref).all())
-    hb.close()
-    out["bands"] = bands
-    r.set_option(m.abi.OPT_BANDS, 4)
     out["pageable_ms"] = med(lambda: r.render_frame_into(cam, W, H, page, depth=5, seed=1))
     ok = ok and bool((page == ref).all())
     m.host_register(page)
@@ -77,6 +65,16 @@ def main():
     out["pinned_ms"] = med(lambda: r.render_frame_into(cam, W, H, hb.array, depth=5, seed=1))
     ok = ok and bool((hb.array == ref).all())
     hb.close()
+    hz = m.HostBuffer((H, W, 4))
+    fdz = m.frame_desc(W, H, depth=5, seed=1)
+    stz = torch.cuda.Stream()
+
+    def zero_copy():
+        r.render_frame_device(cam, fdz, hz.array.ctypes.data, None, stz.cuda_stream)
+        stz.synchronize()
+    out["zero_copy_ms"] = med(zero_copy)
+    ok = ok and bool((hz.array == ref).all())
+    hz.close()
     d = torch.zeros((H, W), dtype=torch.int32, device="cuda")
     fd = m.frame_desc(W, H, depth=5, seed=1)
     st = torch.cuda.Stream()
@@ -85,7 +83,7 @@ def main():
         r.render_frame_device(cam, fd, d.data_ptr(), None, st.cuda_stream)
         st.synchronize()
     out["kernels_ms"] = med(kern)
-    for k in ("pageable", "registered", "pinned", "kernels"):
+    for k in ("pageable", "registered", "pinned", "zero_copy", "kernels"):
         out[k + "_mrays_s"] = round(W * H / out[k + "_ms"] / 1e3, 1)
         out[k + "_ms"] = round(out[k + "_ms"], 4)
     out["frames_equal"] = ok

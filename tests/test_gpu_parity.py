@@ -697,33 +697,6 @@ def test_blocking_frame_into_registered_buffer(gpu, mirt, golden):
         mirt.host_unregister(page)
 
 
-@pytest.mark.parametrize("bands", [2, 3, 5, 8])
-def test_banded_blocking_frames(gpu, mirt, bands):
-    """MIRT_OPT_BANDS: the blocking call traces a whole frame as contiguous
-    row bands at once (band ctxs over the same scene) -- the same bytes as
-    one launch for fresh and accumulating frames, depth 1 and 5, brute
-    force, and a ragged height whose last band is short."""
-    abi = mirt.abi
-    s, b = _scene(mirt, "render", 10000)
-    gpu.upload(s, b)
-    cam = mirt.default_camera()
-    W, H = 1000, 701
-    cases = [dict(depth=5), dict(depth=1), dict(depth=5, use_bvh=False)]
-    try:
-        for kw in cases:
-            gpu.set_option(abi.OPT_BANDS, 1)
-            want = [gpu.render_frame(cam, W, H, seed=3, sample=k, accumulate=k > 0, frames=k + 1, **kw)
-                    for k in range(3)]
-            gpu.set_option(abi.OPT_BANDS, bands)
-            assert gpu.get_option(abi.OPT_BANDS) == bands
-            got = [gpu.render_frame(cam, W, H, seed=3, sample=k, accumulate=k > 0, frames=k + 1, **kw)
-                   for k in range(3)]
-            for k in range(3):
-                assert (got[k] == want[k]).all(), (kw, k)
-    finally:
-        gpu.set_option(abi.OPT_BANDS, 4)
-
-
 def test_cached_tree_renders_golden_frame(gpu, mirt, golden, tmp_path):
     """A scene uploaded from the tree cache file (mirt_bvh_build_flat_cached,
     second call = a load) renders the golden 1080p depth-5 frame."""
