@@ -878,15 +878,31 @@ def host_inclusive(rs, cam, steps):
     run(0, steps_h)
     el = time.perf_counter() - t0
     last = bufs[(steps_h - 1) % n].array.copy()
-    # the blocking call (pageable destination, one frame at a time: the full
-    # persistent grid); median: page faults make single calls noisy
+    # the blocking call, one frame at a time (the full persistent grid), into
+    # the caller's own frame buffer registered in place (INTEGRATION.md's
+    # recipe for main.c's malloc'd buffer: the kernels write the pixels
+    # straight into it) and into plain pageable memory; medians: page faults
+    # make single calls noisy
     rs[0].set_option(mirt.abi.OPT_BOUNCE_BLOCKS, 0)
     img = rs[0].render_frame(cam, W, H, depth=DEPTH, seed=SEED, samples=SPP, jitter=JITTER)
-    dts = []
-    for _ in range(11):
-        t1 = time.perf_counter()
-        img = rs[0].render_frame(cam, W, H, depth=DEPTH, seed=SEED, samples=SPP, jitter=JITTER)
-        dts.append(time.perf_counter() - t1)
+
+    def blocking(dst, n=11):
+        rs[0].render_frame_into(cam, W, H, dst, depth=DEPTH, seed=SEED, samples=SPP, jitter=JITTER)
+        dts = []
+        for _ in range(n):
+            t1 = time.perf_counter()
+            rs[0].render_frame_into(cam, W, H, dst, depth=DEPTH, seed=SEED, samples=SPP, jitter=JITTER)
+            dts.append(time.perf_counter() - t1)
+        return sorted(dts)[len(dts) // 2]
+    page = np.zeros((H, W, 4), np.uint8)
+    dt_page = blocking(page)
+    same = bool((page == img).all())
+    mirt.host_register(page)
+    try:
+        dt_reg = blocking(page)
+        same = same and bool((page == img).all())
+    finally:
+        mirt.host_unregister(page)
     for b in bufs:
         b.close()
     return {"host_inclusive_mrays_s": round(W * H * SPP * steps_h / el / 1e6, 3),
@@ -894,8 +910,13 @@ def host_inclusive(rs, cam, steps):
             "host_inclusive_frames": steps_h,
             "host_inclusive_method": f"{n} ctxs, kernels + async D2H into page-locked buffers "
                                      "(mirt_render_frame_async), frame k waits for frame k - n",
-            "host_frame_equals_blocking_call": bool((last == img).all()),
-            "host_blocking_mrays_s": round(W * H * SPP / sorted(dts)[len(dts) // 2] / 1e6, 3)}
+            "host_frame_equals_blocking_call": bool((last == img).all()) and same,
+            "host_blocking_mrays_s": round(W * H * SPP / dt_reg / 1e6, 3),
+            "host_blocking_ms": round(dt_reg * 1e3, 4),
+            "host_blocking_method": "one blocking mirt_render_frame per frame into a malloc'd (numpy) frame buffer "
+                                    "registered once with mirt_host_register: the kernels write the pixels straight "
+                                    "into it (MIRT_OPT_ZERO_COPY), median of 11",
+            "host_blocking_pageable_mrays_s": round(W * H * SPP / dt_page / 1e6, 3)}
 
 
 if __name__ == "__main__":

@@ -1255,6 +1255,7 @@ struct mirt_ctx {
     int quad_batch = MIRT_QUAD_BATCH_DEFAULT;  // small BVH batches one ray per quad (intersect_quad_kernel)
     int primary_depth1 = MIRT_PRIMARY_DEPTH1;  // depth-1 frames through the camera-packet kernel alone
     int leaf_batch_opt = MIRT_LEAF_BATCH_DEFAULT;  // MIRT_OPT_LEAF_BATCH: 0 off, 1 on, 2 auto (leaf_big)
+    int zero_copy = 1;          // MIRT_OPT_ZERO_COPY: blocking frames into page-locked memory written in place
     bool leaf_big = false;      // the four-wide tree (HNodes + LeafRecs) exceeds the chip's L2
     void* d_queue = nullptr;    // wavefront: {count, head} + bounce records
     size_t queue_cap = 0;
@@ -2103,8 +2104,38 @@ int ctx_device(const mirt_ctx* c) { return c->device; }
 
 extern "C" {
 
+namespace {
+
+// The device-visible address of a page-locked host range (mirt_host_alloc /
+// mirt_host_register memory), or null for pageable memory.
+uint32_t* host_mapped(const void* p, size_t bytes)
+{
+    hipPointerAttribute_t a, b;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeHost || !a.devicePointer ||
+        hipPointerGetAttributes(&b, (const char*)p + bytes - 1) != hipSuccess || b.type != hipMemoryTypeHost) {
+        (void)hipGetLastError();   // a pageable pointer is an error to the query, not to the caller
+        return nullptr;
+    }
+    return (uint32_t*)a.devicePointer;
+}
+
+}  // namespace
+
 int mirt_render_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, mirt_rgba8* out)
 {
+    // a page-locked destination (the recipe for main.c's reused frame buffer:
+    // mirt_host_register): the frame kernels store each pixel straight into
+    // it, so the frame is in host memory when they end -- no copy after them
+    // (one frame, the ctx's own accumulation: nothing reads the output back)
+    if (c && c->zero_copy && out && frame_desc_valid(fd) && fd->samples <= 1 && !accum_chain(c)) {
+        if (uint32_t* d = host_mapped(out, (size_t)shard_row_count(fd) * fd->width * 4)) {
+            uint32_t* disp = nullptr;
+            if (int rc = enqueue_frame(c, cam, fd, d, &disp, "mirt_render_frame")) return rc;
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            HIP_TRY(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+            return MIRT_OK;
+        }
+    }
     if (int rc = enqueue_host_frame(c, cam, fd, out, "mirt_render_frame")) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));
     HIP_TRY(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
@@ -2604,6 +2635,9 @@ int mirt_set_option(mirt_ctx* c, int option, int value)
     case MIRT_OPT_QUAD_BATCH:
         c->quad_batch = value != 0;
         return MIRT_OK;
+    case MIRT_OPT_ZERO_COPY:
+        c->zero_copy = value != 0;
+        return MIRT_OK;
     case MIRT_OPT_LEAF_BATCH:
         if (value < 0 || value > 2) break;
         c->leaf_batch_opt = value;
@@ -2632,6 +2666,7 @@ int mirt_get_option(mirt_ctx* c, int option)
     if (option == MIRT_OPT_BOUNCE_BLOCKS) return c->bounce_blocks_opt;
     if (option == MIRT_OPT_QUAD_DRAIN) return c->quad_drain;
     if (option == MIRT_OPT_QUAD_BATCH) return c->quad_batch;
+    if (option == MIRT_OPT_ZERO_COPY) return c->zero_copy;
     if (option == MIRT_OPT_LEAF_BATCH) return leaf_batch(c) ? 1 : 0;  // in effect for the uploaded scene
     set_error("mirt_get_option: bad option %d", option);
     return MIRT_E_INVALID;

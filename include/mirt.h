@@ -264,8 +264,10 @@ void mirt_host_free(void *p);
 /* Page-lock a caller-owned buffer in place (hipHostRegister) -- the frame
    buffer main.c:241-273's loop mallocs once and reuses every frame: the
    blocking mirt_render_frame's D2H into it is then one DMA instead of the
-   runtime's staged pageable copy. The registration pins the pages until
-   mirt_host_unregister, which must come before the buffer is freed. */
+   runtime's staged pageable copy -- or none at all: with MIRT_OPT_ZERO_COPY
+   (default) the frame kernels write the pixels straight into it. The
+   registration pins the pages until mirt_host_unregister, which must come
+   before the buffer is freed. */
 int mirt_host_register(void *p, size_t bytes);
 int mirt_host_unregister(void *p);
 
@@ -407,9 +409,14 @@ enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3,
                                        together: 0 never, 1 always, 2 (default) when the tree's
                                        four-wide layout exceeds the chip's 32 MiB of L2;
                                        mirt_get_option reads back 0/1: in effect for the scene) */
-       MIRT_OPT_QUAD_BATCH = 15     /* mirt_intersect_rays / mirt_any_hit_rays with the BVH: 1
+       MIRT_OPT_QUAD_BATCH = 15,    /* mirt_intersect_rays / mirt_any_hit_rays with the BVH: 1
                                        (default) = a batch too small to fill the chip one ray per
-                                       lane walks one ray per four lanes (benchmark.c's 10k rays) */ };
+                                       lane walks one ray per four lanes (benchmark.c's 10k rays) */
+       MIRT_OPT_ZERO_COPY = 17      /* blocking mirt_render_frame of one frame into PAGE-LOCKED
+                                       memory (mirt_host_alloc / mirt_host_register; the ctx's
+                                       own accumulation): 1 (default) = the frame kernels store
+                                       every pixel straight into it (no copy after them); 0 = a
+                                       DMA copy after the kernels. Pageable memory: a copy. */ };
 /* Traversal ids keep their first-release values (mirt 0.1: TILE 0, WAVEFRONT 5).
    ABI note: the mirt 0.2 header numbered WAVEFRONT 1; mirt_set_option accepts
    1 as a deprecated alias of MIRT_TRAV_WAVEFRONT (mirt_get_option reads back

@@ -4,11 +4,10 @@ SDL_RenderPresent) through the blocking call, by destination (VERDICT r3
 
   pageable      mirt_render_frame into a numpy array (the runtime stages the D2H)
   registered    the same numpy array after mirt_host_register (page-locked in
-                place: the D2H is one DMA into the caller's own buffer)
-  pinned        mirt_render_frame into mirt_host_alloc memory
+                place: the kernels write the pixels straight into it,
+                MIRT_OPT_ZERO_COPY; registered_copy: one DMA after the kernels)
+  pinned        mirt_render_frame into mirt_host_alloc memory (pinned_copy: DMA)
   kernels       the frame's kernels alone into device memory (one launch)
-  zero_copy     the kernels write the frame straight into page-locked host
-                memory (mirt_render_frame_device with a host pointer): no copy
 
 1080p / 10k depth 5 (bench.py's workload), median of 21 calls each, every
 frame checked against the first. Prints one JSON line.
@@ -56,25 +55,20 @@ def main():
     out["pageable_ms"] = med(lambda: r.render_frame_into(cam, W, H, page, depth=5, seed=1))
     ok = ok and bool((page == ref).all())
     m.host_register(page)
-    try:
-        out["registered_ms"] = med(lambda: r.render_frame_into(cam, W, H, page, depth=5, seed=1))
-        ok = ok and bool((page == ref).all())
-    finally:
-        m.host_unregister(page)
     hb = m.HostBuffer((H, W, 4))
-    out["pinned_ms"] = med(lambda: r.render_frame_into(cam, W, H, hb.array, depth=5, seed=1))
-    ok = ok and bool((hb.array == ref).all())
-    hb.close()
-    hz = m.HostBuffer((H, W, 4))
-    fdz = m.frame_desc(W, H, depth=5, seed=1)
-    stz = torch.cuda.Stream()
-
-    def zero_copy():
-        r.render_frame_device(cam, fdz, hz.array.ctypes.data, None, stz.cuda_stream)
-        stz.synchronize()
-    out["zero_copy_ms"] = med(zero_copy)
-    ok = ok and bool((hz.array == ref).all())
-    hz.close()
+    try:
+        for zc, sfx in ((1, ""), (0, "_copy")):
+            r.set_option(m.abi.OPT_ZERO_COPY, zc)
+            page[:] = 0
+            out["registered" + sfx + "_ms"] = med(lambda: r.render_frame_into(cam, W, H, page, depth=5, seed=1))
+            ok = ok and bool((page == ref).all())
+            hb.array[:] = 0
+            out["pinned" + sfx + "_ms"] = med(lambda: r.render_frame_into(cam, W, H, hb.array, depth=5, seed=1))
+            ok = ok and bool((hb.array == ref).all())
+    finally:
+        r.set_option(m.abi.OPT_ZERO_COPY, 1)
+        m.host_unregister(page)
+        hb.close()
     d = torch.zeros((H, W), dtype=torch.int32, device="cuda")
     fd = m.frame_desc(W, H, depth=5, seed=1)
     st = torch.cuda.Stream()
@@ -83,7 +77,7 @@ def main():
         r.render_frame_device(cam, fd, d.data_ptr(), None, st.cuda_stream)
         st.synchronize()
     out["kernels_ms"] = med(kern)
-    for k in ("pageable", "registered", "pinned", "zero_copy", "kernels"):
+    for k in ("pageable", "registered", "registered_copy", "pinned", "pinned_copy", "kernels"):
         out[k + "_mrays_s"] = round(W * H / out[k + "_ms"] / 1e3, 1)
         out[k + "_ms"] = round(out[k + "_ms"], 4)
     out["frames_equal"] = ok

@@ -682,19 +682,43 @@ def test_traversal_v02_alias(gpu, mirt):
 
 def test_blocking_frame_into_registered_buffer(gpu, mirt, golden):
     """mirt_render_frame into the caller's own malloc'd buffer after
-    mirt_host_register (main.c's frame buffer, page-locked in place): the
-    golden frame, twice; unregistered afterwards."""
+    mirt_host_register (main.c's frame buffer, page-locked in place) -- the
+    kernels write the pixels straight into it (MIRT_OPT_ZERO_COPY) -- and
+    into mirt_host_alloc memory: the golden frame; fresh and accumulating
+    frames, depth 1 and 5, brute force, equal the copy path's and pageable
+    memory's."""
+    abi = mirt.abi
     s, b = _scene(mirt, "render", 10000)
     gpu.upload(s, b)
+    cam = mirt.default_camera()
     page = np.zeros((1080, 1920, 4), np.uint8)
+    hb = mirt.HostBuffer((1080, 1920, 4))
     mirt.host_register(page)
     try:
-        for _ in range(2):
-            page[:] = 0
-            gpu.render_frame_into(mirt.default_camera(), 1920, 1080, page, depth=5, seed=1)
-            assert sha(page) == golden["frames"]["1920x1080_render10000_d5_m1_b1_s1_c0_step1"]["sha"]
+        assert gpu.get_option(abi.OPT_ZERO_COPY) == 1
+        for dst in (page, hb.array):
+            for _ in range(2):
+                dst[:] = 0
+                gpu.render_frame_into(cam, 1920, 1080, dst, depth=5, seed=1)
+                assert sha(dst) == golden["frames"]["1920x1080_render10000_d5_m1_b1_s1_c0_step1"]["sha"]
+        W, H = 640, 360
+        small_page = np.zeros((H, W, 4), np.uint8)
+        for kw in (dict(depth=5), dict(depth=1), dict(depth=5, use_bvh=False)):
+            want = [gpu.render_frame(cam, W, H, seed=2, sample=k, accumulate=k > 0, frames=k + 1, **kw)
+                    for k in range(3)]
+            for zc in (1, 0):
+                gpu.set_option(abi.OPT_ZERO_COPY, zc)
+                for k in range(3):
+                    out = hb.array.reshape(-1)[:H * W * 4].reshape(H, W, 4)
+                    gpu.render_frame_into(cam, W, H, out, seed=2, sample=k, accumulate=k > 0, frames=k + 1, **kw)
+                    assert (out == want[k]).all(), (kw, zc, k)
+                    gpu.render_frame_into(cam, W, H, small_page, seed=2, sample=k, accumulate=k > 0, frames=k + 1,
+                                          **kw)
+                    assert (small_page == want[k]).all(), (kw, zc, k)
     finally:
+        gpu.set_option(abi.OPT_ZERO_COPY, 1)
         mirt.host_unregister(page)
+        hb.close()
 
 
 def test_cached_tree_renders_golden_frame(gpu, mirt, golden, tmp_path):
