@@ -903,6 +903,8 @@ def host_inclusive(rs, cam, steps):
         same = same and bool((page == img).all())
     finally:
         mirt.host_unregister(page)
+    dt_pin = blocking(bufs[0].array)
+    same = same and bool((bufs[0].array == img).all())
     for b in bufs:
         b.close()
     return {"host_inclusive_mrays_s": round(W * H * SPP * steps_h / el / 1e6, 3),
@@ -911,11 +913,12 @@ def host_inclusive(rs, cam, steps):
             "host_inclusive_method": f"{n} ctxs, kernels + async D2H into page-locked buffers "
                                      "(mirt_render_frame_async), frame k waits for frame k - n",
             "host_frame_equals_blocking_call": bool((last == img).all()) and same,
-            "host_blocking_mrays_s": round(W * H * SPP / dt_reg / 1e6, 3),
-            "host_blocking_ms": round(dt_reg * 1e3, 4),
-            "host_blocking_method": "one blocking mirt_render_frame per frame into a malloc'd (numpy) frame buffer "
-                                    "registered once with mirt_host_register: the kernels write the pixels straight "
-                                    "into it (MIRT_OPT_ZERO_COPY), median of 11",
+            "host_blocking_mrays_s": round(W * H * SPP / dt_pin / 1e6, 3),
+            "host_blocking_ms": round(dt_pin * 1e3, 4),
+            "host_blocking_method": "one blocking mirt_render_frame per frame (main.c:350-421's loop) into a frame "
+                                    "buffer from mirt_host_alloc: the kernels write the pixels straight into it "
+                                    "(MIRT_OPT_ZERO_COPY), median of 11",
+            "host_blocking_registered_mrays_s": round(W * H * SPP / dt_reg / 1e6, 3),
             "host_blocking_pageable_mrays_s": round(W * H * SPP / dt_page / 1e6, 3)}
 
 

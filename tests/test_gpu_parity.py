@@ -706,15 +706,13 @@ def test_blocking_frame_into_registered_buffer(gpu, mirt, golden):
         for kw in (dict(depth=5), dict(depth=1), dict(depth=5, use_bvh=False)):
             want = [gpu.render_frame(cam, W, H, seed=2, sample=k, accumulate=k > 0, frames=k + 1, **kw)
                     for k in range(3)]
+            pinned = hb.array.reshape(-1)[:H * W * 4].reshape(H, W, 4)
             for zc in (1, 0):
                 gpu.set_option(abi.OPT_ZERO_COPY, zc)
-                for k in range(3):
-                    out = hb.array.reshape(-1)[:H * W * 4].reshape(H, W, 4)
-                    gpu.render_frame_into(cam, W, H, out, seed=2, sample=k, accumulate=k > 0, frames=k + 1, **kw)
-                    assert (out == want[k]).all(), (kw, zc, k)
-                    gpu.render_frame_into(cam, W, H, small_page, seed=2, sample=k, accumulate=k > 0, frames=k + 1,
-                                          **kw)
-                    assert (small_page == want[k]).all(), (kw, zc, k)
+                for dst in (pinned, small_page):   # each a whole accumulation run from a fresh frame
+                    for k in range(3):
+                        gpu.render_frame_into(cam, W, H, dst, seed=2, sample=k, accumulate=k > 0, frames=k + 1, **kw)
+                        assert (dst == want[k]).all(), (kw, zc, k)
     finally:
         gpu.set_option(abi.OPT_ZERO_COPY, 1)
         mirt.host_unregister(page)
