@@ -49,6 +49,9 @@ def main():
     ap.add_argument("--spp", type=int, default=1, help="jittered samples per frame (BASELINE configs[4]: 4)")
     ap.add_argument("--batch", type=int, default=1,
                     help="with --pipeline: consecutive frames per launch (each frame's display its own slab)")
+    ap.add_argument("--tail-grid", type=int, default=0,
+                    help="with --pipeline: the last N launches of each timed burst run their bounce pass on the "
+                         "full persistent grid (bench.py --tail-grid)")
     ap.add_argument("--copy", action="store_true",
                     help="with --pipeline: after every step a slab-sized D2D copy on one more stream, waiting "
                          "for that step's frame (prices the RCCL gather's stream against the hardware queues)")
@@ -123,9 +126,14 @@ def pipelined(a):
             def run(n):
                 for i in range(n):
                     j = i % len(rs)
+                    tail = i >= n - a.tail_grid
+                    if tail:
+                        rs[j].set_option(mirt.abi.OPT_BOUNCE_BLOCKS, 0)
                     rs[j].render_frame_device(cam, fd, slabs[j].data_ptr(),
                                               accs[j].data_ptr() if accs[j] is not None else None,
                                               streams[j].cuda_stream)
+                    if tail:
+                        rs[j].set_option(mirt.abi.OPT_BOUNCE_BLOCKS, blocks)
                     if cstream is not None:
                         cstream.wait_stream(streams[j])
                         with torch.cuda.stream(cstream):
@@ -138,7 +146,7 @@ def pipelined(a):
             el = time.perf_counter() - t0
             per.append(W * H * frames / world * a.steps / el / 1e6)
         print(json.dumps({"spheres": a.spheres, "scene": a.scene, "size": [W, H], "spp": a.spp, "copy": a.copy,
-                          "batch": a.batch,
+                          "batch": a.batch, "tail_grid": a.tail_grid,
                           "world": world, "frames": frames, "pipeline": a.pipeline,
                           "blocks": blocks, "per_rank_mrays_s": [round(p, 1) for p in per],
                           "min_per_rank_mrays_s": round(min(per), 1),
