@@ -47,37 +47,61 @@ def row_sources(height, row_block, world, device=None):
     return shard, pos
 
 
+_SOURCES = {}
+
+
+def _sources(height, row_block, world, device):
+    """row_sources, built once per geometry and device (the gather runs every
+    frame: rebuilding the index tensors cost several launches each time)."""
+    key = (height, row_block, world, str(device))
+    if key not in _SOURCES:
+        _SOURCES[key] = row_sources(height, row_block, world, device)
+    return _SOURCES[key]
+
+
 def assemble(stacked, height, row_block):
     """stacked: (world, slab_rows, W) int32 slabs -> (height, W) int32 frame."""
     world = stacked.shape[0]
-    shard, pos = row_sources(height, row_block, world, stacked.device)
+    shard, pos = _sources(height, row_block, world, stacked.device)
     return stacked[shard, pos]
 
 
-def gather_frame(slab, height, row_block, group=None, dst=0):
+def assemble_frames(stacked, height, row_block):
+    """stacked: (world, frames, slab_rows, W) -> (frames, height, W): every
+    frame of a launch de-interleaved by ONE indexing kernel."""
+    world = stacked.shape[0]
+    shard, pos = _sources(height, row_block, world, stacked.device)
+    return stacked[shard, :, pos].transpose(0, 1)
+
+
+def gather_frame(slab, height, row_block, group=None, dst=0, recv=None):
     """Gather every rank's (slab_rows, W) int32 slab -- or (frames, slab_rows,
     W) slabs of several frames -- to `dst` and assemble the frame(s) there.
     Returns the (height, W) / (frames, height, W) int32 frame(s) on dst, None
-    elsewhere."""
+    elsewhere. recv: a preallocated (world, *slab.shape) buffer on dst (the
+    per-frame gather then allocates nothing)."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     if not dist.is_initialized():
-        bufs = [slab]
+        st = slab[None]
     else:
         # gloo gathers host tensors (a rehearsal / CPU run): stage device slabs
         # through host memory; RCCL gathers device memory directly
         staged = slab.is_cuda and dist.get_backend(group) == "gloo"
         src = slab.contiguous().cpu() if staged else slab.contiguous()
-        bufs = [torch.empty_like(src) for _ in range(world)] if rank == dst else None
+        if rank == dst:
+            if recv is None or staged or recv.shape[1:] != src.shape or recv.dtype != src.dtype:
+                recv = torch.empty((world, *src.shape), dtype=src.dtype, device=src.device)
+            bufs = list(recv.unbind(0))
+        else:
+            bufs = None
         dist.gather(src, bufs, dst=dst, group=group)
         if rank != dst:
             return None
-        if staged:
-            bufs = [b.to(slab.device) for b in bufs]
-    st = torch.stack(bufs)
+        st = recv.to(slab.device) if staged else recv
     if slab.dim() == 2:
         return assemble(st, height, row_block)
-    return torch.stack([assemble(st[:, j], height, row_block) for j in range(slab.shape[0])])
+    return assemble_frames(st, height, row_block)
 
 
 def as_rgba(frame_i32):
@@ -133,6 +157,7 @@ class ShardedFrame:
         self.k = 0
         self.slab = self.bufs[0][0][-1]
         self.stream = None
+        self.recv = []
 
     def desc(self, depth=5, use_bvh=True, seed=1, sample=0, accumulate=False, frames=1, jitter=False, samples=None):
         from .renderer import frame_desc
@@ -161,7 +186,17 @@ class ShardedFrame:
         stacked."""
         with torch.cuda.stream(self.stream):
             slab = self.slab if every is None else self.launched[every - 1::every]
-            return gather_frame(slab, self.height, self.row_block, self.group)
+            # one receive buffer per context on rank 0, reused every launch
+            # (a launch's gather and assembly run on its context's stream, so
+            # the buffer is free again when that context's next launch gathers)
+            i = (self.k - 1) % len(self.rs)
+            recv = self.recv[i] if i < len(self.recv) else None
+            if self.rank == 0 and self.world > 1 and (recv is None or recv.shape[1:] != slab.shape):
+                recv = torch.empty((self.world, *slab.shape), dtype=slab.dtype, device=slab.device)
+                while len(self.recv) <= i:
+                    self.recv.append(None)
+                self.recv[i] = recv
+            return gather_frame(slab, self.height, self.row_block, self.group, recv=recv)
 
     def render(self, cam, fd):
         """Render this rank's rows and gather; the (H, W) int32 frame on rank 0."""

@@ -29,4 +29,8 @@ step blocks256 120 $S --batch 4 --worlds 8 --blocks 256
 step b2p12 120 python3 scripts/shard_times.py --pipeline 12 --steps 10 --copy --batch 2 --worlds 8
 step b5 120 python3 scripts/shard_times.py --pipeline 8 --steps 4 --copy --batch 5 --worlds 8
 step base_r3 120 $S --batch 4 --worlds 1,8
+
+unset GPU_MAX_HW_QUEUES
+step gather_overhead 120 env MASTER_ADDR=127.0.0.1 MASTER_PORT=29741 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 python3 scripts/gather_overhead.py
+step rccl_tests 200 python -u -m pytest tests/test_bench_launch.py tests/test_gpu_parity.py -m gpu -x -q -k "rccl or shard" --timeout 120 --timeout-method thread
 echo done
