@@ -110,3 +110,35 @@ def test_multi_lanes_accumulating_loop(gpu, mirt, scene10k):
                 x.close()
     for k in range(len(seq)):
         assert (got[k] == want[k]).all(), k
+
+
+@pytest.mark.gpu
+def test_multi_jittered_samples_and_brute_force(gpu, mirt):
+    """BASELINE configs[4]'s shape at small size: several jittered samples
+    per call (each rank's slabs hold every sample, the display after the last
+    is gathered) over the benchmark scene, and the brute-force loop
+    (renderer.c:36-43), 3 same-device ranks: equal to one context's."""
+    s = mirt.create_benchmark_spheres(20000, 1)
+    b = mirt.build_bvh(s)
+    gpu.upload(s, b)
+    cam = mirt.default_camera()
+    cam.position.z = 900.0
+    with mirt.MultiRenderer([0, 0, 0]) as m:
+        m.upload(s, b)
+        for kw in (dict(samples=4, jitter=True), dict(samples=1, use_bvh=False), dict(samples=2)):
+            want = gpu.render_frame(cam, 320, 180, depth=5, seed=7, **kw)
+            got = m.render_frame(cam, 320, 180, depth=5, seed=7, **kw)
+            assert (got == want).all(), kw
+
+
+@pytest.mark.gpu
+def test_multi_rejects_sharded_descriptor(mirt, scene10k):
+    """The multi renderer shards the frame itself: a descriptor that is
+    already a shard is an error, not a silently wrong frame."""
+    s, b = scene10k
+    with mirt.MultiRenderer([0, 0]) as m:
+        m.upload(s, b)
+        fd = mirt.frame_desc(64, 36, shard=1, num_shards=2)
+        out = np.zeros((36, 64, 4), np.uint8)
+        with pytest.raises(mirt.MirtError):
+            m.render_frame_async(mirt.default_camera(), fd, out)
