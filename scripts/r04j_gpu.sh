@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round 4: chain bookkeeping in LDS (MIRT_CHAIN_LDS) at 5 and 6 bounce waves
+# per SIMD (6: 16-entry lane stacks so six workgroups' LDS fit the CU).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+T=r04j
+mkdir -p gpurun_out/$T
+L="ab/libmirt_base.so ab/libmirt_c5.so ab/libmirt_c6s16.so ab/libmirt_w6s16.so"
+for lib in ab/libmirt_c5.so ab/libmirt_c6s16.so; do
+  MIRT_LIB=$lib timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_full_frames.py -m gpu -x -q --timeout 120 --timeout-method thread -k "golden or full or shared or bounce or quad" > gpurun_out/$T/pytest_$(basename $lib .so).log 2>&1 || { tail -20 gpurun_out/$T/pytest_$(basename $lib .so).log; exit 1; }
+  tail -n 1 gpurun_out/$T/pytest_$(basename $lib .so).log
+done
+timeout -k 10 400 python scripts/ab_libs.py $L --rounds 2 --steps 20 > gpurun_out/$T/ab_10k.log 2>&1 || exit 1
+timeout -k 10 400 python scripts/ab_libs.py $L --rounds 2 --steps 20 --workload 1080p_100k > gpurun_out/$T/ab_100k.log 2>&1 || exit 1
+grep BEST gpurun_out/$T/ab_*.log
