@@ -111,6 +111,12 @@ PIPELINE_MULTI, HW_QUEUES_MULTI = 8, 16
 # 4K/1M 0% / 0%: within the rounds' spread at the metric's config, so the
 # bench keeps one launch plan for the whole burst (0).
 TAIL_GRID = 0
+# at N > 1 a rank's launch is 1/N of a frame per frame carried, and the
+# burst's drain is a larger share of the timed region: the last 2 of the 5
+# launches (K = 20, 4 frames each) on the full grid -- the one-frame split at
+# N = 8 emulated per shard (scripts/shard_times.py --tail-grid, copy stream,
+# 16 queues; profiles/r04g/): 15.4-15.6 -> 16.4 Grays/s (1 launch: 16.1)
+TAIL_GRID_MULTI = 2
 KERNEL = "bounce_kernel<true, 2, false>"   # dominant kernel of the default (wavefront, four-wide) schedule
 # the PMC-derived bound of the timed launch shape, per workload
 # (scripts/pmc_bench.sh over this script's own command + scripts/pmc_summary.py);
@@ -412,6 +418,18 @@ def gather_peak(probe, tcp_per_inst):
     return 1.0 / pts[-1][1], [pts[-1]]
 
 
+def trace_check():
+    """The same launch shape ALONE under rocprofv3 --kernel-trace --stats
+    (committed summary): its mean duration must agree with kernel_ms."""
+    path = os.path.join(ROOT, "profiles", "r04g", "exclusive_bounce_trace.json")
+    if W != 1920 or NSPH != 10000 or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    return {"mean_ms": d["mean_ms"], "median_ms": d["median_ms"], "dispatches": d["dispatches"],
+            "source": os.path.relpath(path, ROOT) + " (profiles/r04g/prof_exclusive_kernel_stats.csv)"}
+
+
 def vmem_roofline(pmc, pmc_path, ms_per_step, frames_per_launch):
     """roofline of the dominant kernel on the unit that binds it (VERDICT r3
     item 1): the bounce kernel's vector-memory gather path. achieved = its
@@ -467,6 +485,7 @@ def vmem_roofline(pmc, pmc_path, ms_per_step, frames_per_launch):
                        "vmem_rd_per_frame": vmem_step, "ginst_per_s": round(step_rate, 3),
                        "frac": round(step_rate / peak, 4)},
         "source": os.path.relpath(pmc_path, ROOT) + " + " + os.path.relpath(TD_PROBE, ROOT),
+        "kernel_ms_trace_check": trace_check(),
     }
 
 
@@ -507,9 +526,10 @@ def main():
                          "flight; weak: N frames per step at N GPUs (reported beside it as value_weak)")
     ap.add_argument("--batch", type=int, default=0,
                     help="steps' frames per launch (frames in flight inside a launch; 0 = DEFAULT_BATCH[N])")
-    ap.add_argument("--tail-grid", type=int, default=TAIL_GRID,
+    ap.add_argument("--tail-grid", type=int, default=-1,
                     help="the last N launches of a timed burst take the full persistent bounce grid (nothing "
-                         "later will share the chip); 0 = every launch at --bounce-blocks")
+                         "later will share the chip); 0 = every launch at --bounce-blocks; -1 = TAIL_GRID at "
+                         "N = 1, TAIL_GRID_MULTI at N > 1")
     ap.add_argument("--accumulate", action="store_true",
                     help="time the still-camera accumulating display loop (shared accumulation buffer) instead "
                          "of fresh frames")
@@ -536,6 +556,8 @@ def main():
         return dry_main(args, world, rank)
     if not args.pipeline:
         args.pipeline = 4 if world == 1 else PIPELINE_MULTI
+    if args.tail_grid < 0:
+        args.tail_grid = TAIL_GRID if world == 1 else TAIL_GRID_MULTI
     # MIRT_BENCH_SHARE_GPU=1: a rehearsal of the N > 1 path on a one-GPU box --
     # every rank on device 0 and gloo in place of RCCL (which refuses two ranks
     # on one device); the same launches, shard geometry, gathers (staged
