@@ -584,12 +584,6 @@ __device__ __forceinline__ bool shade_level(const DevScene& sc, const FrameConst
 #define MIRT_BOUNCE_WAVES 5
 #endif
 #define MIRT_BOUNCE_ATTR __attribute__((amdgpu_waves_per_eu(MIRT_BOUNCE_WAVES)))
-// MIRT_CHAIN_LDS (four-wide walk): a chain's bookkeeping (pixel, camera-hit
-// colour, RNG draw count | level) in three LDS rows of the lane's column
-// instead of four VGPRs live across the walk loop (read at the shading only)
-#ifndef MIRT_CHAIN_LDS
-#define MIRT_CHAIN_LDS 0
-#endif
 template <bool FAST, int WALK, bool DIAG = false>
 __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
                                                      float* __restrict__ acc, const BounceRec* __restrict__ queue,
@@ -613,8 +607,6 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
     // every bounce walk starts there, so those steps skip the vector-memory
     // path (TD, the kernel's busiest unit)
     __shared__ uint4 hcache[LANE4 ? 4 * kHCache : 1];
-    constexpr bool CHAIN_LDS = LANE4 && MIRT_CHAIN_LDS;
-    __shared__ uint32_t chain[CHAIN_LDS ? 3 * 256 : 1];   // rows: pixel, base0, k | level << 24
     uint32_t hc_n = 0;
     if constexpr (LANE4) {
         hc_n = min((uint32_t)kHCache, sc.num_hnodes);
@@ -664,16 +656,10 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                     ray = Ray{rec.ox, rec.oy, rec.oz, rec.dx, rec.dy, rec.dz};
                     sr = slab_ray(ray);
                     sp = sph_ray(ray);
-                    if constexpr (CHAIN_LDS) {
-                        chain[threadIdx.x] = rec.pixel;
-                        chain[256 + threadIdx.x] = rec.base0;
-                        chain[512 + threadIdx.x] = rec.k | (1u << 24);
-                    } else {
-                        pixel = rec.pixel;
-                        k = rec.k;
-                        base0 = rec.base0;
-                        level = 1;
-                    }
+                    pixel = rec.pixel;
+                    k = rec.k;
+                    base0 = rec.base0;
+                    level = 1;
                     w.start(sc);
                     best_t = INFINITY;
                     best_s = -1;
@@ -720,19 +706,8 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                 dg_chain += dg_steps;
                 dg_steps = 0;
             }
-            if constexpr (CHAIN_LDS) {
-                pixel = chain[threadIdx.x];
-                base0 = chain[256 + threadIdx.x];
-                const uint32_t kl = chain[512 + threadIdx.x];
-                k = kl & 0xffffffu;
-                level = (int)(kl >> 24);
-            }
-            const bool more = shade_level(sc, f, ray, best_t, best_s, level, k, chain_key(f, pixel), cs, cstride, base0,
-                                          pixel, out, acc, true);
-            if constexpr (CHAIN_LDS) {
-                if (more) chain[512 + threadIdx.x] = k | ((uint32_t)level << 24);
-            }
-            if (more) {
+            if (shade_level(sc, f, ray, best_t, best_s, level, k, chain_key(f, pixel), cs, cstride, base0, pixel, out,
+                            acc, true)) {
                 sr = slab_ray(ray);
                 sp = sph_ray(ray);
                 w.start(sc);
@@ -763,19 +738,10 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
             auto pull = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v); };
             auto pullf = [&](float v) { return __uint_as_float(pull(__float_as_uint(v))); };
             ray = Ray{pullf(ray.ox), pullf(ray.oy), pullf(ray.oz), pullf(ray.dx), pullf(ray.dy), pullf(ray.dz)};
-            if constexpr (CHAIN_LDS) {
-                const uint32_t col = (threadIdx.x & ~63u) + src;
-                pixel = chain[col];
-                base0 = chain[256 + col];
-                const uint32_t kl = chain[512 + col];
-                k = kl & 0xffffffu;
-                level = (int)(kl >> 24);
-            } else {
-                pixel = pull(pixel);
-                k = pull(k);
-                level = (int)pull((uint32_t)level);
-                base0 = pull(base0);
-            }
+            pixel = pull(pixel);
+            k = pull(k);
+            level = (int)pull((uint32_t)level);
+            base0 = pull(base0);
             best_t = pullf(best_t);
             best_s = (int)pull((uint32_t)best_s);
             pr = Prune{pullf(pr.m), pullf(pr.lim)};
