@@ -74,7 +74,10 @@ WORKLOADS = {
     "1080p_10k": dict(W=1920, H=1080, KIND="render", NSPH=10000, SPP=1, JITTER=False,
                       desc="1920x1080, 10000 random spheres, 1 primary ray/pixel, diffuse shading depth 5 "
                            "(BASELINE configs[1])"),
-    "1080p_100k": dict(W=1920, H=1080, KIND="render", NSPH=100000, SPP=1, JITTER=False,
+    # BB_PER_CU: persistent bounce workgroups per CU with frames in flight (1.5 unless stated): the
+    # 100k tree's walks are twice as long, and 2 per CU measured +4.5% there (1,019 / 1,044 -> 1,091 /
+    # 1,058 Mrays/s) while 1080p/10k and 4K lose with it (profiles/r04i/, r04k/)
+    "1080p_100k": dict(W=1920, H=1080, KIND="render", NSPH=100000, SPP=1, JITTER=False, BB_PER_CU=2.0,
                        desc="1920x1080, 100000 random spheres (deep BVH, LDS-stack stress), depth 5 "
                             "(BASELINE configs[2])"),
     "4k_10k": dict(W=3840, H=2160, KIND="render", NSPH=10000, SPP=1, JITTER=False,
@@ -520,7 +523,8 @@ def main():
                          "0 = 4 at N = 1, 8 at N > 1)")
     ap.add_argument("--bounce-blocks", type=int, default=-1,
                     help="persistent bounce workgroups per launch (MIRT_OPT_BOUNCE_BLOCKS) in the timed loop; "
-                         "-1 = 1.5 per CU with frames in flight (--pipeline > 1), else 0 (occupancy x CUs)")
+                         "-1 = the workload's BB_PER_CU (1.5 unless stated) per CU with frames in flight "
+                         "(--pipeline > 1), else 0 (occupancy x CUs)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="strong",
                     help="strong (default): every step is ONE frame (the N = 1 workload) split N ways, frames in "
                          "flight; weak: N frames per step at N GPUs (reported beside it as value_weak)")
@@ -597,7 +601,8 @@ def main():
     # serial measurement loop and the blocking call below use the full grid
     blocks = args.bounce_blocks
     if blocks < 0:
-        blocks = (3 * torch.cuda.get_device_properties(dev).multi_processor_count) // 2 if len(rs) > 1 else 0
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        blocks = int(wl.get("BB_PER_CU", 1.5) * cus) if len(rs) > 1 else 0
     for x in rs:
         x.upload(spheres, bvh)
         x.set_option(mirt.abi.OPT_BOUNCE_BLOCKS, blocks)
