@@ -2144,6 +2144,14 @@ int mirt_render_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc
 
 int mirt_render_frame_async(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, mirt_rgba8* out)
 {
+    // MIRT_OPT_ZERO_COPY 2: frames in flight into page-locked memory are
+    // written in place too (no DMA behind each frame's kernels)
+    if (c && c->zero_copy == 2 && out && frame_desc_valid(fd) && fd->samples <= 1 && !accum_chain(c)) {
+        if (uint32_t* d = host_mapped(out, (size_t)shard_row_count(fd) * fd->width * 4)) {
+            uint32_t* disp = nullptr;
+            return enqueue_frame(c, cam, fd, d, &disp, "mirt_render_frame_async");
+        }
+    }
     return enqueue_host_frame(c, cam, fd, out, "mirt_render_frame_async");
 }
 
@@ -2636,7 +2644,8 @@ int mirt_set_option(mirt_ctx* c, int option, int value)
         c->quad_batch = value != 0;
         return MIRT_OK;
     case MIRT_OPT_ZERO_COPY:
-        c->zero_copy = value != 0;
+        if (value < 0 || value > 2) break;
+        c->zero_copy = value;
         return MIRT_OK;
     case MIRT_OPT_LEAF_BATCH:
         if (value < 0 || value > 2) break;

@@ -330,6 +330,7 @@ def test_shared_accumulation_frames_in_flight(gpu, mirt, oracle, small, W, H, n)
         for k in range(8):
             seq = gpu.render_frame(cam, W, H, depth=5, seed=4, sample=k, accumulate=k > 0, frames=k + 1)
             assert (got[k] == seq).all(), k
+        seq_fresh = [gpu.render_frame(cam, W, H, depth=5, seed=4, sample=k) for k in range(8)]
         assert acc_shared.tobytes() == gpu.accum(W * H * 3).tobytes()
         if n <= 1000:
             t = oracle.build(small["render_1000_1_pre"].copy())
@@ -344,6 +345,23 @@ def test_shared_accumulation_frames_in_flight(gpu, mirt, oracle, small, W, H, n)
         rs[1].share_accum(None)
         with pytest.raises(mirt.MirtError):
             rs[1].accum(W * H * 3)
+        # frames in flight written in place (MIRT_OPT_ZERO_COPY 2) into the
+        # page-locked buffers: the same frames (private buffers again first)
+        for x in rs:
+            x.share_accum(None)
+            x.set_option(mirt.abi.OPT_ZERO_COPY, 2)
+        for k in range(8):
+            i = k % 4
+            rs[i].wait()
+            if k >= 4:
+                assert (bufs[i].array == seq_fresh[k - 4]).all(), k - 4
+            fd = mirt.frame_desc(W, H, depth=5, seed=4, sample=k)
+            rs[i].render_frame_async(cam, fd, bufs[i])
+        for k in range(4, 8):
+            rs[k % 4].wait()
+            assert (bufs[k % 4].array == seq_fresh[k]).all(), k
+        for x in rs:
+            x.set_option(mirt.abi.OPT_ZERO_COPY, 1)
     finally:
         for x in bufs:
             x.close()
