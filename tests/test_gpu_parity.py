@@ -330,8 +330,8 @@ def test_shared_accumulation_frames_in_flight(gpu, mirt, oracle, small, W, H, n)
         for k in range(8):
             seq = gpu.render_frame(cam, W, H, depth=5, seed=4, sample=k, accumulate=k > 0, frames=k + 1)
             assert (got[k] == seq).all(), k
-        seq_fresh = [gpu.render_frame(cam, W, H, depth=5, seed=4, sample=k) for k in range(8)]
         assert acc_shared.tobytes() == gpu.accum(W * H * 3).tobytes()
+        seq_fresh = [gpu.render_frame(cam, W, H, depth=5, seed=4, sample=k) for k in range(8)]
         if n <= 1000:
             t = oracle.build(small["render_1000_1_pre"].copy())
             acc = np.zeros(W * H * 3, np.float32)
