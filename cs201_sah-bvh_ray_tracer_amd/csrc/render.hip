@@ -569,6 +569,61 @@ __device__ __forceinline__ bool shade_level(const DevScene& sc, const FrameConst
     return false;
 }
 
+// MIRT_SOLO_DRAIN: the last ray of a bounce wave walked by all 16 of the
+// wave's quads at once (trace.h solo_step)
+#ifndef MIRT_SOLO_DRAIN
+#define MIRT_SOLO_DRAIN 1
+#endif
+
+// The rest of the chain of the wave's one remaining ray (held by the quad of
+// lane l0), every lane of the wave taking part: its state broadcast from l0,
+// its stack moved from its source lane's column to the wave layout of
+// solo_step, each level walked with solo_step and shaded as shade_level
+// (lane 0 stores the pixel).
+template <bool FAST>
+__device__ __forceinline__ void solo_chain(const DevScene& sc, const FrameConst& f, int l0, Ray ray, float best_t,
+                                        int best_s, Prune pr, QuadWalk qw, int level, uint32_t k, uint32_t pixel,
+                                        uint32_t base0, uint32_t src, uint32_t* wst, uint32_t* wcs,
+                                        uint32_t* __restrict__ out, float* __restrict__ acc, lds_uint4* hc,
+                                        uint32_t hc_n)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    auto bu = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l0); };
+    auto bf = [&](float v) { return __uint_as_float(bu(__float_as_uint(v))); };
+    ray = Ray{bf(ray.ox), bf(ray.oy), bf(ray.oz), bf(ray.dx), bf(ray.dy), bf(ray.dz)};
+    best_t = bf(best_t);
+    best_s = (int)bu((uint32_t)best_s);
+    pr = Prune{bf(pr.m), bf(pr.lim)};
+    level = (int)bu((uint32_t)level);
+    k = bu(k);
+    pixel = bu(pixel);
+    base0 = bu(base0);
+    src = bu(src);
+    const uint32_t cur = bu(qw.cur), end = bu(qw.end), top = bu(qw.top);
+    // the stack (top <= kWideStack entries, column src) to the wave layout
+    uint32_t v = 0;
+    if (lane < top) v = wst[lane * kWideStride + src];
+    __builtin_amdgcn_wave_barrier();
+    if (lane < top) *solo_slot(wst, lane) = v;
+    uint32_t* cs = wcs + src;  // the colour stack stays in the source column
+    SlabRay sr = slab_ray(ray);
+    SphRay sp = sph_ray(ray);
+    SoloWalk w{lane < 4 ? cur : kPNone, lane < 4 ? end : 0u, top};
+    for (;;) {
+        while (solo_step<FAST, kWideStack * 64>(sc, sr, sp, pr, w, wst, best_t, best_s, hc, hc_n)) {
+        }
+        if (!shade_level(sc, f, ray, best_t, best_s, level, k, chain_key(f, pixel), cs, kWideStride, base0, pixel, out,
+                         acc, lane == 0))
+            return;
+        sr = slab_ray(ray);
+        sp = sph_ray(ray);
+        w = SoloWalk{lane < 4 ? sc.wide_root : kPNone, 0u, 0u};
+        best_t = INFINITY;
+        best_s = -1;
+        pr = prune_off();
+    }
+}
+
 // Persistent bounce pass: each lane owns one pixel's chain of bounces,
 // refilled from the primary pass's queue. WALK 2 (default) ends with a QUAD
 // DRAIN: once the queue is dry and at most 16 of
@@ -757,6 +812,16 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
             if (DIAG) dg_tq = __builtin_amdgcn_s_memrealtime();
             while (__ballot(has)) {
                 if (DIAG) dg_qit++;
+                if (MIRT_SOLO_DRAIN && !DIAG) {
+                    // one ray left in the wave: every quad of the wave walks it
+                    const uint64_t rays = __ballot(has && (lane & 3) == 0);
+                    if (__popcll(rays) == 1) {
+                        solo_chain<FAST>(sc, f, __builtin_ctzll(rays), ray, best_t, best_s, pr, qw, level, k, pixel,
+                                         base0, src, wstack + (threadIdx.x & ~63u), cstack + (threadIdx.x & ~63u),
+                                         out, acc, (lds_uint4*)hcache, hc_n);
+                        break;
+                    }
+                }
                 if (has && qw.cur != kPNone)
                     quad_step<FAST, kWideStride, kWideStack>(sc, sr, sp, pr, qw, qstk, best_t, best_s,
                                                              (lds_uint4*)hcache, hc_n);
