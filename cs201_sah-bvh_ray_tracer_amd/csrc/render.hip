@@ -624,91 +624,6 @@ __device__ __forceinline__ void solo_chain(const DevScene& sc, const FrameConst&
     }
 }
 
-// MIRT_GROUP_RAYS (2 or 4): once the quad drain has 2..this many rays left,
-// each is walked by a group of 32 / 16 lanes (group_chain: an out-of-line
-// call, so the walk loop's registers stay as they are); 1: the solo drain only
-#ifndef MIRT_GROUP_RAYS
-#define MIRT_GROUP_RAYS 4
-#endif
-
-// The rest of the chains of the wave's last rays (the quads whose lane 0 is
-// set in `rays`; at most 64 / GL of them), ray r walked by the r-th group of
-// GL lanes: its state taken from its quad, its stack moved from its source
-// lane's column to the group's layout (group_step), each level walked with
-// group_step and shaded as shade_level (the group's first lane stores).
-template <bool FAST, int GL>
-__device__ __noinline__ void group_chain(const DevScene& sc, const FrameConst& f, uint64_t rays, Ray ray,
-                                            float best_t, int best_s, Prune pr, QuadWalk qw, int level, uint32_t k,
-                                            uint32_t pixel, uint32_t base0, uint32_t src, uint32_t* wst,
-                                            uint32_t* wcs, uint32_t* __restrict__ out, float* __restrict__ acc,
-                                            lds_uint4* hc, uint32_t hc_n)
-{
-    constexpr int kGroups = 64 / GL;
-    const uint32_t lane = threadIdx.x & 63, g0 = lane & ~(uint32_t)(GL - 1);
-    // the quad lane of group g's ray: the g-th set bit of `rays` (uniform)
-    int lsrc[kGroups];
-    uint64_t m = rays;
-#pragma unroll
-    for (int g = 0; g < kGroups; g++) {
-        lsrc[g] = m ? __builtin_ctzll(m) : -1;
-        m &= m ? m - 1 : 0;
-    }
-    const int mg = (int)(lane / GL);
-    bool mine = false;
-#pragma unroll
-    for (int g = 0; g < kGroups; g++) mine = mine || (mg == g && lsrc[g] >= 0);
-    // group-wise broadcast: readlane from each group's (uniform) source lane
-    auto bu = [&](uint32_t v) {
-        uint32_t r = v;
-#pragma unroll
-        for (int g = 0; g < kGroups; g++)
-            if (lsrc[g] >= 0) {
-                const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)v, lsrc[g]);
-                r = mg == g ? x : r;
-            }
-        return r;
-    };
-    auto bf = [&](float v) { return __uint_as_float(bu(__float_as_uint(v))); };
-    ray = Ray{bf(ray.ox), bf(ray.oy), bf(ray.oz), bf(ray.dx), bf(ray.dy), bf(ray.dz)};
-    best_t = bf(best_t);
-    best_s = (int)bu((uint32_t)best_s);
-    pr = Prune{bf(pr.m), bf(pr.lim)};
-    level = (int)bu((uint32_t)level);
-    k = bu(k);
-    pixel = bu(pixel);
-    base0 = bu(base0);
-    src = bu(src);
-    const uint32_t cur = bu(qw.cur), end = bu(qw.end), top = bu(qw.top);
-    // the stack (top <= kWideStack <= 2 GL entries, column src) to the group
-    // layout: every read is issued before any write
-    const uint32_t kk0 = lane - g0, kk1 = kk0 + GL;
-    uint32_t v0 = 0, v1 = 0;
-    if (mine && kk0 < top) v0 = wst[kk0 * kWideStride + src];
-    if (mine && kk1 < top) v1 = wst[kk1 * kWideStride + src];
-    __builtin_amdgcn_wave_barrier();
-    uint32_t* gst = wst + g0;
-    if (mine && kk0 < top) *group_slot<GL>(gst, kk0) = v0;
-    if (mine && kk1 < top) *group_slot<GL>(gst, kk1) = v1;
-    if (!mine) return;
-    uint32_t* cs = wcs + src;  // the colour stack stays in the source column
-    SlabRay sr = slab_ray(ray);
-    SphRay sp = sph_ray(ray);
-    GroupWalk w{lane - g0 < 4 ? cur : kPNone, lane - g0 < 4 ? end : 0u, top};
-    for (;;) {
-        while (group_step<FAST, GL>(sc, sr, sp, pr, w, gst, best_t, best_s, hc, hc_n)) {
-        }
-        if (!shade_level(sc, f, ray, best_t, best_s, level, k, chain_key(f, pixel), cs, kWideStride, base0, pixel, out,
-                         acc, lane == g0))
-            return;
-        sr = slab_ray(ray);
-        sp = sph_ray(ray);
-        w = GroupWalk{lane - g0 < 4 ? sc.wide_root : kPNone, 0u, 0u};
-        best_t = INFINITY;
-        best_s = -1;
-        pr = prune_off();
-    }
-}
-
 // Persistent bounce pass: each lane owns one pixel's chain of bounces,
 // refilled from the primary pass's queue. WALK 2 (default) ends with a QUAD
 // DRAIN: once the queue is dry and at most 16 of
@@ -904,17 +819,6 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                         solo_chain<FAST>(sc, f, __builtin_ctzll(rays), ray, best_t, best_s, pr, qw, level, k, pixel,
                                          base0, src, wstack + (threadIdx.x & ~63u), cstack + (threadIdx.x & ~63u),
                                          out, acc, (lds_uint4*)hcache, hc_n);
-                        break;
-                    }
-                    if (MIRT_GROUP_RAYS >= 2 && __popcll(rays) <= MIRT_GROUP_RAYS) {
-                        if (__popcll(rays) == 2)
-                            group_chain<FAST, 32>(sc, f, rays, ray, best_t, best_s, pr, qw, level, k, pixel, base0,
-                                                  src, wstack + (threadIdx.x & ~63u), cstack + (threadIdx.x & ~63u),
-                                                  out, acc, (lds_uint4*)hcache, hc_n);
-                        else
-                            group_chain<FAST, 16>(sc, f, rays, ray, best_t, best_s, pr, qw, level, k, pixel, base0,
-                                                  src, wstack + (threadIdx.x & ~63u), cstack + (threadIdx.x & ~63u),
-                                                  out, acc, (lds_uint4*)hcache, hc_n);
                         break;
                     }
                 }

@@ -1385,152 +1385,6 @@ __device__ __forceinline__ bool solo_step(const DevScene& sc, const SlabRay& sr,
     return true;
 }
 
-// ---------------------------------------------------------------- group walk
-// The last rays of a bounce wave (the queue is dry and the quad drain has at
-// most MIRT_GROUP_RAYS rays left): each ray is walked by a GROUP of GL lanes
-// (16, 32 or all 64: 4, 8 or 16 quads) at once. Each quad of a group visits
-// one node per step (slot j in lane j, as quad_step) and goes on with its
-// nearest passing child; the other passing children wait on the group's ONE
-// stack, spread over the group's GL LDS columns (entry k at row k / GL,
-// column k % GL: the wave's other chains are done, so their columns are
-// free), and idle quads take the stack's top entries. A step thus covers up
-// to GL / 4 nodes instead of one, so the launch's longest chains -- which set
-// when a persistent launch ends -- take far fewer dependent round trips. The
-// best hit is reduced over the group after every step (min t, a tie to the
-// larger sphere index: order-free, so the same closest hit as any other
-// walk). A node whose children would overflow the stack is walked as its
-// flat DFS segment by its quad (lane_step), as quad_step does.
-struct GroupWalk {
-    uint32_t cur, end;  // this quad's node (kPNone: idle) or flat DFS segment (end != 0)
-    uint32_t top;       // stack depth (group-uniform)
-};
-
-// Entry k of the stack of the group whose first column is `gst`.
-template <int GL>
-__device__ __forceinline__ uint32_t* group_slot(uint32_t* gst, uint32_t k)
-{
-    return gst + (k / GL) * kWideStride + (k % GL);
-}
-
-// One step of the group walk; false (group-uniform) once every quad of the
-// group is idle and its stack is empty. gst: the group's first LDS column.
-template <bool FAST, int GL>
-__device__ __forceinline__ bool group_step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
-                                           GroupWalk& w, uint32_t* gst, float& best_t, int& best_s, lds_uint4* hc,
-                                           uint32_t hc_n)
-{
-    constexpr uint32_t kCap = GL * kWideStack;
-    const uint32_t lane = threadIdx.x & 63, j = lane & 3;
-    const uint32_t g0 = lane & ~(uint32_t)(GL - 1);
-    const uint64_t gmask = GL == 64 ? ~0ull : (((1ull << GL) - 1) << g0);
-    // 1. idle quads take the stack's top entries (quad of idle rank r: entry top - 1 - r)
-    const uint64_t idle = __ballot(w.cur == kPNone && j == 0) & gmask;
-    const uint32_t take = min((uint32_t)__popcll(idle), w.top);
-    if (w.cur == kPNone) {
-        const uint32_t qb = lane & ~3u;
-        const uint32_t r = (uint32_t)__popcll(qb ? idle & ((1ull << qb) - 1) : 0ull);
-        if (r < take) w.cur = *group_slot<GL>(gst, w.top - 1 - r);
-    }
-    w.top -= take;
-    if (!(__ballot(w.cur != kPNone) & gmask)) return false;
-    float ct = INFINITY;   // this lane's candidate
-    int cs = -1;
-    bool push = false;
-    Counters cnt{0, 0, 0, 0, 0};
-    if (w.cur != kPNone && w.end) {
-        // a flat DFS segment: the quad's four lanes walk it alike
-        float bt = best_t;
-        int bs = best_s;
-        lane_step<FAST, false, true>(sc, sr, sp, pr, w.cur, bt, bs, cnt);
-        if (bs != best_s || bt != best_t) {
-            ct = bt;
-            cs = bs;
-        }
-        if (w.cur >= w.end) {
-            w.end = 0;
-            w.cur = kPNone;
-        }
-    }
-    uint32_t nx = 0, n_in = 0, qref = kPNone;
-    if (w.cur != kPNone && !w.end) {
-        uint4 q;
-        if (w.cur < hc_n)
-            q = lds_load(hc + 4 * w.cur + j);
-        else
-            q = ((const uint4*)(sc.hnodes + w.cur))[j];
-        qref = q.w;
-        float e = 0.0f;
-        const bool pass = slab_cons(sr, pr, h_lo(q.x), h_lo(q.y), h_lo(q.z), h_hi(q.x), h_hi(q.y), h_hi(q.z), e) &
-                          (q.w != kPNone);
-        if (pass && (q.w & kPLeaf)) {  // sphere first, the exact box only for a hit (wide_leaf)
-            const float4* lp = (const float4*)(sc.leaves + (q.w & ~kPLeaf));
-            const float t = sphere_t<FAST>(sp, lp[2], best_t);
-            if (t > 0.0f) {
-                const float4 l0 = lp[0], l1 = lp[1];
-                float ee;
-                if (slab_box<FAST>(sr, pr, l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, ee)) {
-                    ct = t;
-                    cs = __float_as_int(l1.z);
-                }
-            }
-        }
-        const bool inner = pass && !(q.w & kPLeaf);
-        const float key = inner ? fminf(e, 3.0e38f) : INFINITY;
-        const float k1 = __uint_as_float(quad_perm<kQuadXor1>(__float_as_uint(key)));
-        const float k2 = __uint_as_float(quad_perm<kQuadXor2>(__float_as_uint(key)));
-        const float k3 = __uint_as_float(quad_perm<kQuadXor3>(__float_as_uint(key)));
-        const uint32_t rank = (uint32_t)(k1 < key || (k1 == key && (j ^ 1) < j)) +
-                              (uint32_t)(k2 < key || (k2 == key && (j ^ 2) < j)) +
-                              (uint32_t)(k3 < key || (k3 == key && (j ^ 3) < j));
-        n_in = (uint32_t)__popcll((__ballot(inner) >> (lane & 60)) & 0xF);
-        nx = inner && rank == 0 ? q.w + 1 : 0u;  // + 1: 0 means none
-        nx |= quad_perm<kQuadXor1>(nx);
-        nx |= quad_perm<kQuadXor2>(nx);
-        push = inner && rank > 0;
-    }
-    // 2. the pushes of the group's quads, or -- if they would overflow its
-    // stack -- each pushing quad walks its node's subtree as a DFS segment
-    const uint64_t pm = __ballot(push) & gmask;
-    const uint32_t np = (uint32_t)__popcll(pm);
-    const bool seg_fallback = w.top + np > kCap;   // group-uniform
-    if (w.cur != kPNone && !w.end) {
-        if (seg_fallback && n_in > 1) {
-            const HAux ax = sc.haux[w.cur];
-            w.cur = ax.flat + 1;
-            w.end = ax.end;
-        } else {
-            w.cur = n_in ? nx - 1 : kPNone;
-        }
-    }
-    if (!seg_fallback) {
-        if (push)
-            *group_slot<GL>(gst, w.top + __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u))) = qref;
-        w.top += np;
-    }
-    // 3. the best hit over the group (every lane of it then holds it)
-    if (cs < 0 || !cand_better(ct, cs, best_t, best_s)) {
-        ct = best_t;
-        cs = best_s;
-    }
-#pragma unroll
-    for (int off = 1; off < GL; off <<= 1) {
-        const float ot = __shfl_xor(ct, off);
-        const int os = __shfl_xor(cs, off);
-        if (cand_better(ot, os, ct, cs)) {
-            ct = ot;
-            cs = os;
-        }
-    }
-    if (cs >= 0 && cand_better(ct, cs, best_t, best_s)) {
-        best_t = ct;
-        best_s = cs;
-    }
-    // the prune state follows the (now group-uniform) best
-    if (best_s >= 0 && sc.prune) prune_update(pr, sc, sr.ox, sr.oy, sr.oz, sp.a4(), best_t);
-    return true;
-}
-
 // Closest hit for every active lane: degenerate rays (a zero or tiny
 // direction component, `SlabRay::generic`) one at a time with the whole
 // wave (closest_bvh_chunked), the rest with the lane-parallel walk (or the
