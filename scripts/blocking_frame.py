@@ -11,7 +11,14 @@ SDL_RenderPresent) through the blocking call, by destination (VERDICT r3
 
 1080p / 10k depth 5 (bench.py's workload), median of 21 calls each, every
 frame checked against the first. Prints one JSON line.
-  python scripts/blocking_frame.py [--workload 1080p_10k]
+  python scripts/blocking_frame.py [--phases plain,torch,burst]
+
+--phases repeats the destination set after each step, in order: plain (as the
+process starts), torch (after torch's device context is up, as in bench.py),
+burst (after bench.py's pipelined leg: 4 ctxs at 384 bounce workgroups, 60
+frames in flight into page-locked buffers), close (the burst's extra ctxs
+destroyed again). Keys of later phases get the
+phase name as a prefix.
 """
 import argparse
 import importlib
@@ -30,6 +37,7 @@ m = importlib.import_module("cs201_sah-bvh_ray_tracer_amd")
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--calls", type=int, default=21)
+    ap.add_argument("--phases", default="plain")
     a = ap.parse_args()
     import torch
     W, H = 1920, 1080
@@ -52,23 +60,61 @@ def main():
     out = {"workload": "1920x1080, 10000 spheres, depth 5 (blocking mirt_render_frame per frame)"}
     page = np.zeros((H, W, 4), np.uint8)
     ok = True
-    out["pageable_ms"] = med(lambda: r.render_frame_into(cam, W, H, page, depth=5, seed=1))
-    ok = ok and bool((page == ref).all())
-    m.host_register(page)
-    hb = m.HostBuffer((H, W, 4))
-    try:
-        for zc, sfx in ((1, ""), (0, "_copy")):
-            r.set_option(m.abi.OPT_ZERO_COPY, zc)
-            page[:] = 0
-            out["registered" + sfx + "_ms"] = med(lambda: r.render_frame_into(cam, W, H, page, depth=5, seed=1))
-            ok = ok and bool((page == ref).all())
-            hb.array[:] = 0
-            out["pinned" + sfx + "_ms"] = med(lambda: r.render_frame_into(cam, W, H, hb.array, depth=5, seed=1))
-            ok = ok and bool((hb.array == ref).all())
-    finally:
-        r.set_option(m.abi.OPT_ZERO_COPY, 1)
-        m.host_unregister(page)
-        hb.close()
+
+    def dests(pre):
+        nonlocal ok
+        res = {}
+        res["pageable_ms"] = med(lambda: r.render_frame_into(cam, W, H, page, depth=5, seed=1))
+        ok = ok and bool((page == ref).all())
+        m.host_register(page)
+        hb = m.HostBuffer((H, W, 4))
+        try:
+            for zc, sfx in ((1, ""), (0, "_copy")):
+                r.set_option(m.abi.OPT_ZERO_COPY, zc)
+                page[:] = 0
+                res["registered" + sfx + "_ms"] = med(lambda: r.render_frame_into(cam, W, H, page, depth=5, seed=1))
+                ok = ok and bool((page == ref).all())
+                hb.array[:] = 0
+                res["pinned" + sfx + "_ms"] = med(lambda: r.render_frame_into(cam, W, H, hb.array, depth=5, seed=1))
+                ok = ok and bool((hb.array == ref).all())
+        finally:
+            r.set_option(m.abi.OPT_ZERO_COPY, 1)
+            m.host_unregister(page)
+            hb.close()
+        for k in list(res):
+            out[pre + k] = round(res[k], 4)
+            out[pre + k.replace("_ms", "_mrays_s")] = round(W * H / res[k] / 1e3, 1)
+
+    def burst():
+        rs = [r] + [m.Renderer(0) for _ in range(3)]
+        for x in rs[1:]:
+            x.upload(s, b)
+        for x in rs:
+            x.set_option(m.abi.OPT_BOUNCE_BLOCKS, 384)
+        fd = m.frame_desc(W, H, depth=5, seed=1)
+        bufs = [m.HostBuffer((H, W, 4)) for _ in rs]
+        for k in range(60):
+            rs[k % 4].wait()
+            rs[k % 4].render_frame_async(cam, fd, bufs[k % 4])
+        for x in rs:
+            x.wait()
+        r.set_option(m.abi.OPT_BOUNCE_BLOCKS, 0)
+        for x in bufs:
+            x.close()
+        return rs[1:]
+
+    extra = []
+    for ph in a.phases.split(","):
+        if ph == "torch":
+            torch.zeros(1, device="cuda")
+            torch.cuda.synchronize()
+        elif ph == "burst":
+            extra += burst()
+        elif ph == "close":
+            for x in extra:
+                x.close()
+            extra = []
+        dests("" if ph == "plain" else ph + "_")
     d = torch.zeros((H, W), dtype=torch.int32, device="cuda")
     fd = m.frame_desc(W, H, depth=5, seed=1)
     st = torch.cuda.Stream()
@@ -76,11 +122,12 @@ def main():
     def kern():
         r.render_frame_device(cam, fd, d.data_ptr(), None, st.cuda_stream)
         st.synchronize()
-    out["kernels_ms"] = med(kern)
-    for k in ("pageable", "registered", "registered_copy", "pinned", "pinned_copy", "kernels"):
-        out[k + "_mrays_s"] = round(W * H / out[k + "_ms"] / 1e3, 1)
-        out[k + "_ms"] = round(out[k + "_ms"], 4)
+    kms = med(kern)
+    out["kernels_ms"] = round(kms, 4)
+    out["kernels_mrays_s"] = round(W * H / kms / 1e3, 1)
     out["frames_equal"] = ok
+    for x in extra:
+        x.close()
     print(json.dumps(out), flush=True)
     r.close()
 
