@@ -68,6 +68,7 @@ shard = importlib.import_module("cs201_sah-bvh_ray_tracer_amd.shard")
 METRIC = "Mrays/s at 1080p, 10k spheres; 1/2/4/8 GPU + CPU baseline"
 W, H, NSPH, DEPTH, SEED, ROW_BLOCK = 1920, 1080, 10000, 5, 1, 8
 KIND, SPP, JITTER = "render", 1, False
+WORKLOAD = "1080p_10k"
 # --workload: BASELINE.json configs (the default is configs[1], the metric's
 # own configuration; the others are measured on request, one GPU or more)
 WORKLOADS = {
@@ -541,13 +542,17 @@ def main():
     ap.add_argument("--rank-timeout", type=float, default=420.0,
                     help="N > 1 started by this script: seconds before a still-running job is terminated (exit "
                          "124); each rank's process group times out 30 s earlier")
+    ap.add_argument("--blocking-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--opt", action="append", default=[],
                     help="OPTION=VALUE (mirt_set_option on every context; A/B of schedule options), repeatable")
     args = ap.parse_args()
-    global W, H, NSPH, KIND, SPP, JITTER
+    global W, H, NSPH, KIND, SPP, JITTER, WORKLOAD
+    WORKLOAD = args.workload
     wl = WORKLOADS[args.workload]
     W, H, NSPH, KIND, SPP, JITTER = wl["W"], wl["H"], wl["NSPH"], wl["KIND"], wl["SPP"], wl["JITTER"]
 
+    if args.blocking_child:
+        return blocking_child()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return spawn_ranks(args.gpus, args.rank_timeout)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -886,7 +891,8 @@ def host_inclusive(rs, cam, steps):
     """SURVEY §8(d) t_frame: frames delivered to host memory. Pipelined: ctx
     k % n renders frame k and copies it into its page-locked buffer
     (mirt_render_frame_async), waiting first for its frame k - n; blocking:
-    mirt_render_frame into a pageable array, one call at a time."""
+    one mirt_render_frame at a time (blocking_leg), in a child process and in
+    this one."""
     fdh = mirt.frame_desc(W, H, depth=DEPTH, seed=SEED, samples=SPP, jitter=JITTER)
     bufs = [mirt.HostBuffer((H, W, 4)) for _ in rs]
     n = len(rs)
@@ -905,20 +911,60 @@ def host_inclusive(rs, cam, steps):
     run(0, steps_h)
     el = time.perf_counter() - t0
     last = bufs[(steps_h - 1) % n].array.copy()
-    # the blocking call, one frame at a time (the full persistent grid), into
-    # the caller's own frame buffer registered in place (INTEGRATION.md's
-    # recipe for main.c's malloc'd buffer: the kernels write the pixels
-    # straight into it) and into plain pageable memory; medians: page faults
-    # make single calls noisy
+    for b in bufs:
+        b.close()
+    # the blocking call in THIS process too, after the four-context burst
+    # (same measurement as the child's; reported beside it)
     rs[0].set_option(mirt.abi.OPT_BOUNCE_BLOCKS, 0)
-    img = rs[0].render_frame(cam, W, H, depth=DEPTH, seed=SEED, samples=SPP, jitter=JITTER)
+    here = blocking_leg(rs[0], cam)
+    child = blocking_in_child()
+    out = {"host_inclusive_mrays_s": round(W * H * SPP * steps_h / el / 1e6, 3),
+           "host_inclusive_ms_per_frame": round(el / steps_h * 1e3, 4),
+           "host_inclusive_frames": steps_h,
+           "host_inclusive_method": f"{n} ctxs, kernels + async D2H into page-locked buffers "
+                                    "(mirt_render_frame_async), frame k waits for frame k - n",
+           "host_frame_equals_blocking_call": frame_sha(last) == here["sha"] and here["equal"]}
+    src = child if child else here
+    out.update({"host_blocking_mrays_s": src["pinned_mrays_s"], "host_blocking_ms": src["pinned_ms"],
+                "host_blocking_registered_mrays_s": src["registered_mrays_s"],
+                "host_blocking_pageable_mrays_s": src["pageable_mrays_s"],
+                "host_blocking_method": (
+                    "one blocking mirt_render_frame per frame (main.c:350-421's loop) into a frame buffer from "
+                    "mirt_host_alloc: the kernels write the pixels straight into it (MIRT_OPT_ZERO_COPY), median "
+                    "of 11; " + ("measured in a child process holding one ctx and its frame buffer, as main.c's "
+                                 "loop runs (bench.py --blocking-child)" if child else
+                                 "measured in this process (the child process failed)")),
+                "host_blocking_after_burst": {k: here[k] for k in ("pinned_mrays_s", "registered_mrays_s",
+                                                                    "pageable_mrays_s")}})
+    if child:
+        out["host_frame_equals_blocking_call"] = out["host_frame_equals_blocking_call"] and \
+            child["sha"] == here["sha"] and child["equal"]
+        out["host_blocking_after_burst"]["note"] = (
+            "the same calls in the bench's own process after its four-context burst: zero-copy stores run slower "
+            "there for the rest of the process (profiles/r04x: a child started at that point measures as a "
+            "fresh process does)")
+    return out
 
-    def blocking(dst, n=11):
-        rs[0].render_frame_into(cam, W, H, dst, depth=DEPTH, seed=SEED, samples=SPP, jitter=JITTER)
+
+def frame_sha(a):
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def blocking_leg(r, cam, n=11):
+    """The blocking call, one frame at a time (the full persistent grid), into
+    plain pageable memory, into the caller's own frame buffer registered in
+    place (INTEGRATION.md's recipe for main.c's malloc'd buffer: the kernels
+    write the pixels straight into it) and into mirt_host_alloc memory;
+    medians: page faults make single calls noisy."""
+    img = r.render_frame(cam, W, H, depth=DEPTH, seed=SEED, samples=SPP, jitter=JITTER)
+
+    def blocking(dst):
+        r.render_frame_into(cam, W, H, dst, depth=DEPTH, seed=SEED, samples=SPP, jitter=JITTER)
         dts = []
         for _ in range(n):
             t1 = time.perf_counter()
-            rs[0].render_frame_into(cam, W, H, dst, depth=DEPTH, seed=SEED, samples=SPP, jitter=JITTER)
+            r.render_frame_into(cam, W, H, dst, depth=DEPTH, seed=SEED, samples=SPP, jitter=JITTER)
             dts.append(time.perf_counter() - t1)
         return sorted(dts)[len(dts) // 2]
     page = np.zeros((H, W, 4), np.uint8)
@@ -930,23 +976,44 @@ def host_inclusive(rs, cam, steps):
         same = same and bool((page == img).all())
     finally:
         mirt.host_unregister(page)
-    dt_pin = blocking(bufs[0].array)
-    same = same and bool((bufs[0].array == img).all())
-    for b in bufs:
-        b.close()
-    return {"host_inclusive_mrays_s": round(W * H * SPP * steps_h / el / 1e6, 3),
-            "host_inclusive_ms_per_frame": round(el / steps_h * 1e3, 4),
-            "host_inclusive_frames": steps_h,
-            "host_inclusive_method": f"{n} ctxs, kernels + async D2H into page-locked buffers "
-                                     "(mirt_render_frame_async), frame k waits for frame k - n",
-            "host_frame_equals_blocking_call": bool((last == img).all()) and same,
-            "host_blocking_mrays_s": round(W * H * SPP / dt_pin / 1e6, 3),
-            "host_blocking_ms": round(dt_pin * 1e3, 4),
-            "host_blocking_method": "one blocking mirt_render_frame per frame (main.c:350-421's loop) into a frame "
-                                    "buffer from mirt_host_alloc: the kernels write the pixels straight into it "
-                                    "(MIRT_OPT_ZERO_COPY), median of 11",
-            "host_blocking_registered_mrays_s": round(W * H * SPP / dt_reg / 1e6, 3),
-            "host_blocking_pageable_mrays_s": round(W * H * SPP / dt_page / 1e6, 3)}
+    hb = mirt.HostBuffer((H, W, 4))
+    try:
+        dt_pin = blocking(hb.array)
+        same = same and bool((hb.array == img).all())
+    finally:
+        hb.close()
+    res = {"equal": same, "sha": frame_sha(img)}
+    for k, dt in (("pageable", dt_page), ("registered", dt_reg), ("pinned", dt_pin)):
+        res[k + "_ms"] = round(dt * 1e3, 4)
+        res[k + "_mrays_s"] = round(W * H * SPP / dt / 1e6, 3)
+    return res
+
+
+def blocking_child():
+    """bench.py --blocking-child: one ctx with the workload's scene, the
+    blocking leg, one JSON line (the parent's host_blocking_*)."""
+    spheres = (mirt.create_random_spheres(NSPH, SEED) if KIND == "render"
+               else mirt.create_benchmark_spheres(NSPH, SEED))
+    r = mirt.Renderer(0)
+    try:
+        r.upload(spheres, mirt.build_bvh(spheres))
+        print(json.dumps(blocking_leg(r, mirt.default_camera())), flush=True)
+    finally:
+        r.close()
+    return 0
+
+
+def blocking_in_child():
+    """The blocking leg in a fresh child process (a new program, not a fork
+    or an exec of this one, which has the GPU open); None if it fails."""
+    import subprocess
+    try:
+        res = subprocess.run([sys.executable, os.path.abspath(__file__), "--blocking-child", "--workload", WORKLOAD],
+                             capture_output=True, text=True, timeout=240)
+        line = [l for l in res.stdout.splitlines() if l.startswith("{")]
+        return json.loads(line[-1]) if res.returncode == 0 and line else None
+    except (subprocess.SubprocessError, ValueError, IndexError):
+        return None
 
 
 if __name__ == "__main__":
