@@ -38,6 +38,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--calls", type=int, default=21)
     ap.add_argument("--phases", default="plain")
+    ap.add_argument("--bounce-blocks", default="",
+                    help="comma list: the pinned zero-copy call again at these bounce grids (0: the full grid)")
     ap.add_argument("--child", action="store_true",
                     help="after the phases, the plain phase again in a fresh child process (this one still open)")
     a = ap.parse_args()
@@ -149,6 +151,14 @@ def main():
     def kern():
         r.render_frame_device(cam, fd, d.data_ptr(), None, st.cuda_stream)
         st.synchronize()
+    if a.bounce_blocks:
+        hb = m.HostBuffer((H, W, 4))
+        for bb in [int(v) for v in a.bounce_blocks.split(",")]:
+            r.set_option(m.abi.OPT_BOUNCE_BLOCKS, bb)
+            out[f"pinned_bb{bb}_ms"] = round(med(lambda: r.render_frame_into(cam, W, H, hb.array, depth=5, seed=1)), 4)
+            ok = ok and bool((hb.array == ref).all())
+        r.set_option(m.abi.OPT_BOUNCE_BLOCKS, 0)
+        hb.close()
     if a.child:
         import subprocess
         res = subprocess.run([sys.executable, os.path.abspath(__file__), "--phases", "plain"], capture_output=True,

@@ -13,3 +13,7 @@ L="ab/libmirt_base.so ab/libmirt_sq32.so"
 timeout -k 10 500 python scripts/ab_libs.py $L --rounds 3 --steps 20 > $OUT/ab_10k.log 2>&1 || exit 1
 timeout -k 10 500 python scripts/ab_libs.py $L --rounds 2 --steps 20 --workload 1080p_100k > $OUT/ab_100k.log 2>&1 || exit 1
 grep BEST $OUT/ab_*.log
+for lib in base sq32; do
+  timeout -k 10 200 env MIRT_LIB=ab/libmirt_$lib.so python scripts/blocking_frame.py --bounce-blocks 0,1280,1024,768,512 > $OUT/blocking_$lib.log 2>&1 || exit 1
+  echo "$lib $(tail -1 $OUT/blocking_$lib.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print({k: d[k] for k in d if k.startswith("pinned") and k.endswith("_ms") or k == "kernels_ms"}, d["frames_equal"])')"
+done
