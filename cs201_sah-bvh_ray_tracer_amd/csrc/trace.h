@@ -204,11 +204,7 @@ __device__ __forceinline__ void normalize3(float& x, float& y, float& z)
     float sq = x * x;
     sq = sq + y * y;
     sq = sq + z * z;
-#if MIRT_SQRT_F32
-    const float len = sqrtf(sq);
-#else
     const float len = (float)__dsqrt_rn((double)sq);
-#endif
     if (len != 0.0f) {
         x = x / len;
         y = y / len;
