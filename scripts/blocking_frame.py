@@ -38,6 +38,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--calls", type=int, default=21)
     ap.add_argument("--phases", default="plain")
+    ap.add_argument("--opt", action="append", default=[], help="OPTION=VALUE (mirt_set_option), repeatable")
     ap.add_argument("--bounce-blocks", default="",
                     help="comma list: the pinned zero-copy call again at these bounce grids (0: the full grid)")
     ap.add_argument("--child", action="store_true",
@@ -49,6 +50,9 @@ def main():
     b = m.build_bvh(s)
     r = m.Renderer(0)
     r.upload(s, b)
+    for ov in a.opt:
+        o, v = (int(t) for t in ov.split("="))
+        r.set_option(o, v)
     cam = m.default_camera()
 
     def med(fn):

@@ -107,6 +107,9 @@ def pipelined(a):
     for r in rs:
         r.upload(s, b)
         r.set_option(mirt.abi.OPT_BOUNCE_BLOCKS, blocks)
+        for ov in a.opt:
+            o, v = (int(x) for x in ov.split("="))
+            r.set_option(o, v)
     streams = [torch.cuda.ExternalStream(r.stream_handle) for r in rs]
     cam = mirt.default_camera()
     for world in (int(w) for w in a.worlds.split(",")):
