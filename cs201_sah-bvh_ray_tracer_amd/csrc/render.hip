@@ -569,47 +569,6 @@ __device__ __forceinline__ bool shade_level(const DevScene& sc, const FrameConst
     return false;
 }
 
-// CHAIN HANDOFF (MIRT_OPT_CHAINS, bounce_kernel<..., CHAINS>): once a wave
-// has found the queue dry, a chain that finishes a bounce level and goes on
-// is not continued by its lane: its next level (the re-aimed ray, the RNG
-// draw count, the colour stack) is appended to a continuation queue and the
-// lane goes idle, so the launch ends after the walks in flight, not after
-// the longest remaining CHAIN of every wave; the next bounce launch of the
-// frame takes the continuations as its queue, with every lane busy again.
-// A frame of depth D has at most D - 1 bounce launches (each moves every
-// continuation on by a level; the last one defers nothing).
-struct ContRec {
-    float ox, oy, oz, dx, dy, dz;
-    uint32_t pixel, k, base0, level;
-    uint32_t col[kMaxDepth - 2];  // colour stack rows 0 .. level - 2
-};
-static_assert(sizeof(ContRec) == 64, "continuation record is 64 B");
-
-// The calling lanes (any control flow) append their chains' continuations.
-__device__ __forceinline__ void defer_chain(ContRec* __restrict__ cout, uint32_t* __restrict__ cctl, const Ray& ray,
-                                            uint32_t pixel, uint32_t k, uint32_t base0, int level, const uint32_t* cs,
-                                            int cstride)
-{
-    const uint64_t m = __ballot(1);  // the lanes here
-    const int leader = __builtin_ctzll(m);
-    uint32_t base = 0;
-    if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(cctl, (uint32_t)__popcll(m));
-    base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
-    ContRec r;
-    r.ox = ray.ox;
-    r.oy = ray.oy;
-    r.oz = ray.oz;
-    r.dx = ray.dx;
-    r.dy = ray.dy;
-    r.dz = ray.dz;
-    r.pixel = pixel;
-    r.k = k;
-    r.base0 = base0;
-    r.level = (uint32_t)level;
-    for (int row = 0; row < kMaxDepth - 2; row++) r.col[row] = row < level - 1 ? cs[row * cstride] : 0u;
-    cout[base + lanes_below(m)] = r;
-}
-
 // MIRT_SOLO_DRAIN: the last ray of a bounce wave walked by all 16 of the
 // wave's quads at once (trace.h solo_step)
 #ifndef MIRT_SOLO_DRAIN
@@ -621,13 +580,12 @@ __device__ __forceinline__ void defer_chain(ContRec* __restrict__ cout, uint32_t
 // its stack moved from its source lane's column to the wave layout of
 // solo_step, each level walked with solo_step and shaded as shade_level
 // (lane 0 stores the pixel).
-template <bool FAST, bool CHAINS = false>
+template <bool FAST>
 __device__ __forceinline__ void solo_chain(const DevScene& sc, const FrameConst& f, int l0, Ray ray, float best_t,
                                         int best_s, Prune pr, QuadWalk qw, int level, uint32_t k, uint32_t pixel,
                                         uint32_t base0, uint32_t src, uint32_t* wst, uint32_t* wcs,
                                         uint32_t* __restrict__ out, float* __restrict__ acc, lds_uint4* hc,
-                                        uint32_t hc_n, ContRec* __restrict__ cout = nullptr,
-                                        uint32_t* __restrict__ cctl = nullptr, bool defer = false)
+                                        uint32_t hc_n)
 {
     const uint32_t lane = threadIdx.x & 63;
     auto bu = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l0); };
@@ -657,10 +615,6 @@ __device__ __forceinline__ void solo_chain(const DevScene& sc, const FrameConst&
         if (!shade_level(sc, f, ray, best_t, best_s, level, k, chain_key(f, pixel), cs, kWideStride, base0, pixel, out,
                          acc, lane == 0))
             return;
-        if (CHAINS && defer) {
-            if (lane == 0) defer_chain(cout, cctl, ray, pixel, k, base0, level, cs, kWideStride);
-            return;
-        }
         sr = slab_ray(ray);
         sp = sph_ray(ray);
         w = SoloWalk{lane < 4 ? sc.wide_root : kPNone, 0u, 0u};
@@ -685,14 +639,11 @@ __device__ __forceinline__ void solo_chain(const DevScene& sc, const FrameConst&
 #define MIRT_BOUNCE_WAVES 5
 #endif
 #define MIRT_BOUNCE_ATTR __attribute__((amdgpu_waves_per_eu(MIRT_BOUNCE_WAVES)))
-template <bool FAST, int WALK, bool DIAG = false, bool CHAINS = false>
+template <bool FAST, int WALK, bool DIAG = false>
 __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
                                                      float* __restrict__ acc, const BounceRec* __restrict__ queue,
                                                      uint32_t* __restrict__ qctl, int threshold, int quad_drain,
-                                                     uint64_t* __restrict__ diag = nullptr,
-                                                     const ContRec* __restrict__ cin = nullptr,
-                                                     ContRec* __restrict__ cout = nullptr,
-                                                     uint32_t* __restrict__ cctl = nullptr, int may_defer = 0)
+                                                     uint64_t* __restrict__ diag = nullptr)
 {
     uint64_t dg_it = 0, dg_lanes = 0, dg_it_x = 0, dg_lanes_x = 0, dg_tx = 0, dg_qit = 0, dg_tq = 0;
     const uint64_t dg_t0 = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -756,26 +707,14 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                 const uint32_t lane0 = threadIdx.x & 63;
                 const uint32_t idx = b + (uint32_t)__popcll(need & ((1ull << lane0) - 1));
                 if (idx < sz) {
-                    if (CHAINS && cin) {
-                        // a continuation: its level and colour stack too
-                        const ContRec rec = cin[lo + idx];
-                        ray = Ray{rec.ox, rec.oy, rec.oz, rec.dx, rec.dy, rec.dz};
-                        pixel = rec.pixel;
-                        k = rec.k;
-                        base0 = rec.base0;
-                        level = (int)rec.level;
-                        for (int row = 0; row < kMaxDepth - 2; row++)
-                            if (row < level - 1) cs[row * cstride] = rec.col[row];
-                    } else {
-                        const BounceRec rec = queue[lo + idx];
-                        ray = Ray{rec.ox, rec.oy, rec.oz, rec.dx, rec.dy, rec.dz};
-                        pixel = rec.pixel;
-                        k = rec.k;
-                        base0 = rec.base0;
-                        level = 1;
-                    }
+                    const BounceRec rec = queue[lo + idx];
+                    ray = Ray{rec.ox, rec.oy, rec.oz, rec.dx, rec.dy, rec.dz};
                     sr = slab_ray(ray);
                     sp = sph_ray(ray);
+                    pixel = rec.pixel;
+                    k = rec.k;
+                    base0 = rec.base0;
+                    level = 1;
                     w.start(sc);
                     best_t = INFINITY;
                     best_s = -1;
@@ -824,17 +763,12 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
             }
             if (shade_level(sc, f, ray, best_t, best_s, level, k, chain_key(f, pixel), cs, cstride, base0, pixel, out,
                             acc, true)) {
-                if (CHAINS && may_defer && exhausted) {
-                    defer_chain(cout, cctl, ray, pixel, k, base0, level, cs, cstride);
-                    has = false;
-                } else {
-                    sr = slab_ray(ray);
-                    sp = sph_ray(ray);
-                    w.start(sc);
-                    best_t = INFINITY;
-                    best_s = -1;
-                    pr = prune_off();
-                }
+                sr = slab_ray(ray);
+                sp = sph_ray(ray);
+                w.start(sc);
+                best_t = INFINITY;
+                best_s = -1;
+                pr = prune_off();
             } else {
                 has = false;
                 if (DIAG) {
@@ -882,10 +816,9 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                     // one ray left in the wave: every quad of the wave walks it
                     const uint64_t rays = __ballot(has && (lane & 3) == 0);
                     if (__popcll(rays) == 1) {
-                        solo_chain<FAST, CHAINS>(sc, f, __builtin_ctzll(rays), ray, best_t, best_s, pr, qw, level, k,
-                                                 pixel, base0, src, wstack + (threadIdx.x & ~63u),
-                                                 cstack + (threadIdx.x & ~63u), out, acc, (lds_uint4*)hcache, hc_n,
-                                                 cout, cctl, may_defer != 0);
+                        solo_chain<FAST>(sc, f, __builtin_ctzll(rays), ray, best_t, best_s, pr, qw, level, k, pixel,
+                                         base0, src, wstack + (threadIdx.x & ~63u), cstack + (threadIdx.x & ~63u),
+                                         out, acc, (lds_uint4*)hcache, hc_n);
                         break;
                     }
                 }
@@ -895,18 +828,12 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                 if (has && qw.cur == kPNone) {
                     if (shade_level(sc, f, ray, best_t, best_s, level, k, chain_key(f, pixel), qcs, kWideStride, base0, pixel, out,
                                     acc, (lane & 3) == 0)) {
-                        if (CHAINS && may_defer) {
-                            if ((lane & 3) == 0) defer_chain(cout, cctl, ray, pixel, k, base0, level, qcs, kWideStride);
-                            has = false;
-                            qw.cur = kPNone;
-                        } else {
-                            sr = slab_ray(ray);
-                            sp = sph_ray(ray);
-                            qw = QuadWalk{sc.wide_root, 0u, 0u};
-                            best_t = INFINITY;
-                            best_s = -1;
-                            pr = prune_off();
-                        }
+                        sr = slab_ray(ray);
+                        sp = sph_ray(ray);
+                        qw = QuadWalk{sc.wide_root, 0u, 0u};
+                        best_t = INFINITY;
+                        best_s = -1;
+                        pr = prune_off();
                     } else {
                         has = false;
                     }
@@ -1397,9 +1324,6 @@ struct mirt_ctx {
     bool leaf_big = false;      // the four-wide tree (HNodes + LeafRecs) exceeds the chip's L2
     void* d_queue = nullptr;    // wavefront: {count, head} + bounce records
     size_t queue_cap = 0;
-    void* d_cont = nullptr;     // MIRT_OPT_CHAINS: two continuation queues, each {count, heads} + records
-    size_t cont_cap = 0;
-    int chains = 0;             // MIRT_OPT_CHAINS: hand chains over between bounce launches once the queue is dry
     uint32_t* d_defer = nullptr;  // [count, list...]
     size_t defer_cap = 0;
     unsigned long long* d_keys = nullptr;  // chunked brute force: per-ray (t, index) keys
@@ -1911,28 +1835,7 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
             primary_kernel<false, false><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ph1[ps], s));
-        if (c->chains && sc.wide && c->fast_slab && !d_bdiag && !leaf_batch(c) && f.depth > 2) {
-            // the chain handoff: up to depth - 1 bounce launches, launch j
-            // reading the continuations launch j - 1 appended (ping-pong)
-            const size_t one = kQCtlBytes + sizeof(ContRec) * pixels;
-            if (int rc2 = ensure(&c->d_cont, &c->cont_cap, 2 * one)) return rc2;
-            auto ctl = [&](int j) { return (uint32_t*)((char*)c->d_cont + (size_t)(j & 1) * one); };
-            auto recs = [&](int j) { return (ContRec*)((char*)c->d_cont + (size_t)(j & 1) * one + kQCtlBytes); };
-            const int launches = f.depth - 1;
-            for (int j = 0; j < launches; j++) {
-                const int defer = j + 1 < launches;
-                if (defer) HIP_TRY(hipMemsetAsync(ctl(j), 0, kQCtlBytes, s));
-                if (j == 0)
-                    bounce_kernel<true, 2, false, true><<<bblocks, 256, blds, s>>>(
-                        sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, nullptr, nullptr,
-                        recs(j), ctl(j), defer);
-                else
-                    bounce_kernel<true, 2, false, true><<<bblocks, 256, blds, s>>>(
-                        sc, f, d_out, d_acc, nullptr, ctl(j - 1), c->bounce_threshold, c->quad_drain, nullptr,
-                        recs(j - 1), recs(j), ctl(j), defer);
-                HIP_TRY(hipGetLastError());
-            }
-        } else if (d_bdiag && sc.wide)
+        if (d_bdiag && sc.wide)
             bounce_kernel<true, 2, true><<<bblocks, 256, blds, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, d_bdiag);
         else if (d_bdiag)
             bounce_kernel<true, 0, true><<<bblocks, 256, blds, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, d_bdiag);
@@ -2060,7 +1963,7 @@ void mirt_destroy(mirt_ctx* c)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     accum_release(c->acc);
     for (void* p : {(void*)c->d_nodes, (void*)c->d_nodes32, (void*)c->d_geo, (void*)c->d_color, (void*)c->d_out,
-                    c->d_in, c->d_res, (void*)c->d_counts, (void*)c->d_defer, c->d_queue, c->d_cont, (void*)c->d_keys, (void*)c->d_pnodes,
+                    c->d_in, c->d_res, (void*)c->d_counts, (void*)c->d_defer, c->d_queue, (void*)c->d_keys, (void*)c->d_pnodes,
                     (void*)c->d_hnodes, (void*)c->d_haux, (void*)c->d_leaves, (void*)c->d_ndepth,
                     (void*)c->d_overlay})
         if (p) (void)hipFree(p);
@@ -2809,10 +2712,6 @@ int mirt_set_option(mirt_ctx* c, int option, int value)
         if (value < 0 || value > 2) break;
         c->zero_copy = value;
         return MIRT_OK;
-    case MIRT_OPT_CHAINS:
-        if (value < 0 || value > 1) break;
-        c->chains = value;
-        return MIRT_OK;
     case MIRT_OPT_LEAF_BATCH:
         if (value < 0 || value > 2) break;
         c->leaf_batch_opt = value;
@@ -2842,7 +2741,6 @@ int mirt_get_option(mirt_ctx* c, int option)
     if (option == MIRT_OPT_QUAD_DRAIN) return c->quad_drain;
     if (option == MIRT_OPT_QUAD_BATCH) return c->quad_batch;
     if (option == MIRT_OPT_ZERO_COPY) return c->zero_copy;
-    if (option == MIRT_OPT_CHAINS) return c->chains;
     if (option == MIRT_OPT_LEAF_BATCH) return leaf_batch(c) ? 1 : 0;  // in effect for the uploaded scene
     set_error("mirt_get_option: bad option %d", option);
     return MIRT_E_INVALID;

@@ -412,18 +412,13 @@ enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3,
        MIRT_OPT_QUAD_BATCH = 15,    /* mirt_intersect_rays / mirt_any_hit_rays with the BVH: 1
                                        (default) = a batch too small to fill the chip one ray per
                                        lane walks one ray per four lanes (benchmark.c's 10k rays) */
-       MIRT_OPT_ZERO_COPY = 17,     /* frames of one sample into PAGE-LOCKED memory
+       MIRT_OPT_ZERO_COPY = 17      /* frames of one sample into PAGE-LOCKED memory
                                        (mirt_host_alloc / mirt_host_register; the ctx's own
                                        accumulation): the frame kernels store every pixel
                                        straight into it instead of a DMA copy after them --
                                        1 (default) for the blocking mirt_render_frame, 2 for
                                        mirt_render_frame_async too, 0 never. Pageable memory:
-                                       a copy. */
-       MIRT_OPT_CHAINS = 18         /* four-wide bounce walk, depth >= 3: 1 = once a bounce wave
-                                       finds the queue dry, a chain that goes on to its next level
-                                       is handed to the frame's next bounce launch (up to depth - 1
-                                       launches) instead of being continued by its lane; 0
-                                       (default) = every chain finishes in its wave */ };
+                                       a copy. */ };
 /* Traversal ids keep their first-release values (mirt 0.1: TILE 0, WAVEFRONT 5).
    ABI note: the mirt 0.2 header numbered WAVEFRONT 1; mirt_set_option accepts
    1 as a deprecated alias of MIRT_TRAV_WAVEFRONT (mirt_get_option reads back
