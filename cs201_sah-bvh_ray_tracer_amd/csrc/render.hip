@@ -350,7 +350,8 @@ template <bool FAST, bool ORD>
 #define MIRT_PRIMARY_ATTR __attribute__((amdgpu_waves_per_eu(ORD ? MIRT_PRIMARY_WAVES : 1)))
 __global__ __launch_bounds__(256) MIRT_PRIMARY_ATTR void primary_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
                                                       float* __restrict__ acc, Deferred dfr,
-                                                      BounceRec* __restrict__ queue, uint32_t* __restrict__ qctl)
+                                                      BounceRec* __restrict__ queue, uint32_t* __restrict__ qctl,
+                                                      int octants = 1)
 {
     __shared__ uint32_t cstack[ORD ? 1 : kMaxDepth * 256];
     Counters cnt{0, 0, 0, 0, 0};
@@ -440,7 +441,11 @@ __global__ __launch_bounds__(256) MIRT_PRIMARY_ATTR void primary_kernel(DevScene
         if (__builtin_amdgcn_readfirstlane(prev) != (blockDim.x >> 6) - 1) return;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         // the last wave: octant of each record's direction, counts per
-        // (wave, octant), then every record to base + its octant's offset
+        // (wave, octant), then every record to base + its octant's offset.
+        // octants == 0 (a frame alone on its ctx: the blocking call): tile
+        // order, still one queue atomic per workgroup -- measured (DESIGN
+        // §8): the lone frame's bounce pass is 2-4% shorter in tile order,
+        // frames in flight are 1% faster grouped
         const int nw = blockDim.x >> 6;
         uint32_t oct[4], tot[8] = {0, 0, 0, 0, 0, 0, 0, 0}, total = 0;
         bool has[4];
@@ -448,7 +453,7 @@ __global__ __launch_bounds__(256) MIRT_PRIMARY_ATTR void primary_kernel(DevScene
             const uint32_t n = gcount[w];
             has[w] = (uint32_t)lane < n;
             const BounceRec& r = grec[w * 64 + (has[w] ? lane : 0)];
-            oct[w] = (r.dx < 0.0f ? 1u : 0u) | (r.dy < 0.0f ? 2u : 0u) | (r.dz < 0.0f ? 4u : 0u);
+            oct[w] = octants ? (r.dx < 0.0f ? 1u : 0u) | (r.dy < 0.0f ? 2u : 0u) | (r.dz < 0.0f ? 4u : 0u) : 0u;
             for (uint32_t o = 0; o < 8; o++) tot[o] += (uint32_t)__popcll(__ballot(has[w] && oct[w] == o));
             total += n;
         }
@@ -1324,6 +1329,7 @@ struct mirt_ctx {
     bool leaf_big = false;      // the four-wide tree (HNodes + LeafRecs) exceeds the chip's L2
     void* d_queue = nullptr;    // wavefront: {count, head} + bounce records
     size_t queue_cap = 0;
+    bool lone_frame = false;    // mirt_render_frame's frame: the first bounces queued in tile order
     uint32_t* d_defer = nullptr;  // [count, list...]
     size_t defer_cap = 0;
     unsigned long long* d_keys = nullptr;  // chunked brute force: per-ray (t, index) keys
@@ -1828,11 +1834,11 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
         const int bblocks = c->bounce_blocks_opt ? c->bounce_blocks_opt : c->bounce_blocks;
         const size_t blds = bounce_lds_bytes(f.depth);
         if (c->fast_slab && sc.ordered)
-            primary_kernel<true, true><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
+            primary_kernel<true, true><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl, c->lone_frame ? 0 : 1);
         else if (c->fast_slab)
-            primary_kernel<true, false><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
+            primary_kernel<true, false><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl, c->lone_frame ? 0 : 1);
         else
-            primary_kernel<false, false><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
+            primary_kernel<false, false><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl, c->lone_frame ? 0 : 1);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ph1[ps], s));
         if (d_bdiag && sc.wide)
@@ -2186,7 +2192,20 @@ uint32_t* host_mapped(const void* p, size_t bytes)
 
 }  // namespace
 
+static int render_frame_blocking(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, mirt_rgba8* out);
+
+// The blocking call renders one frame with nothing after it on the ctx: its
+// first bounces go to the queue in tile order (lone_frame), which the
+// bounce pass walks 2-4% faster when no other frame shares the chip.
 int mirt_render_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, mirt_rgba8* out)
+{
+    if (c) c->lone_frame = true;
+    const int rc = render_frame_blocking(c, cam, fd, out);
+    if (c) c->lone_frame = false;
+    return rc;
+}
+
+static int render_frame_blocking(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, mirt_rgba8* out)
 {
     // a page-locked destination (the recipe for main.c's reused frame buffer:
     // mirt_host_register): the frame kernels store each pixel straight into
