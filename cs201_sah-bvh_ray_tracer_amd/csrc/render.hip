@@ -1330,6 +1330,7 @@ struct mirt_ctx {
     void* d_queue = nullptr;    // wavefront: {count, head} + bounce records
     size_t queue_cap = 0;
     bool lone_frame = false;    // mirt_render_frame's frame: the first bounces queued in tile order
+    int queue_order = 0;        // MIRT_OPT_QUEUE_ORDER: 0 auto (tile order for lone_frame), 1 octants, 2 tile order
     uint32_t* d_defer = nullptr;  // [count, list...]
     size_t defer_cap = 0;
     unsigned long long* d_keys = nullptr;  // chunked brute force: per-ray (t, index) keys
@@ -1733,6 +1734,14 @@ AccumShare* accum_chain(const mirt_ctx* c)
     return c->acc && c->acc->refs > 1 ? c->acc : nullptr;
 }
 
+// The first bounces grouped by direction octant in the queue (frames in
+// flight) or in tile order (a frame alone: the blocking call), or as
+// MIRT_OPT_QUEUE_ORDER forces.
+int octant_queue(const mirt_ctx* c)
+{
+    return c->queue_order == 1 || (c->queue_order == 0 && !c->lone_frame) ? 1 : 0;
+}
+
 int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_acc, hipStream_t s, bool timed,
                   mirt_counts* d_counts, uint32_t* d_wave_stats = nullptr, uint64_t* d_bdiag = nullptr)
 {
@@ -1834,11 +1843,11 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
         const int bblocks = c->bounce_blocks_opt ? c->bounce_blocks_opt : c->bounce_blocks;
         const size_t blds = bounce_lds_bytes(f.depth);
         if (c->fast_slab && sc.ordered)
-            primary_kernel<true, true><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl, c->lone_frame ? 0 : 1);
+            primary_kernel<true, true><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl, octant_queue(c));
         else if (c->fast_slab)
-            primary_kernel<true, false><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl, c->lone_frame ? 0 : 1);
+            primary_kernel<true, false><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl, octant_queue(c));
         else
-            primary_kernel<false, false><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl, c->lone_frame ? 0 : 1);
+            primary_kernel<false, false><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl, octant_queue(c));
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ph1[ps], s));
         if (d_bdiag && sc.wide)
@@ -2731,6 +2740,10 @@ int mirt_set_option(mirt_ctx* c, int option, int value)
         if (value < 0 || value > 2) break;
         c->zero_copy = value;
         return MIRT_OK;
+    case MIRT_OPT_QUEUE_ORDER:
+        if (value < 0 || value > 2) break;
+        c->queue_order = value;
+        return MIRT_OK;
     case MIRT_OPT_LEAF_BATCH:
         if (value < 0 || value > 2) break;
         c->leaf_batch_opt = value;
@@ -2760,6 +2773,7 @@ int mirt_get_option(mirt_ctx* c, int option)
     if (option == MIRT_OPT_QUAD_DRAIN) return c->quad_drain;
     if (option == MIRT_OPT_QUAD_BATCH) return c->quad_batch;
     if (option == MIRT_OPT_ZERO_COPY) return c->zero_copy;
+    if (option == MIRT_OPT_QUEUE_ORDER) return c->queue_order;
     if (option == MIRT_OPT_LEAF_BATCH) return leaf_batch(c) ? 1 : 0;  // in effect for the uploaded scene
     set_error("mirt_get_option: bad option %d", option);
     return MIRT_E_INVALID;

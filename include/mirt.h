@@ -412,13 +412,18 @@ enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3,
        MIRT_OPT_QUAD_BATCH = 15,    /* mirt_intersect_rays / mirt_any_hit_rays with the BVH: 1
                                        (default) = a batch too small to fill the chip one ray per
                                        lane walks one ray per four lanes (benchmark.c's 10k rays) */
-       MIRT_OPT_ZERO_COPY = 17      /* frames of one sample into PAGE-LOCKED memory
+       MIRT_OPT_ZERO_COPY = 17,     /* frames of one sample into PAGE-LOCKED memory
                                        (mirt_host_alloc / mirt_host_register; the ctx's own
                                        accumulation): the frame kernels store every pixel
                                        straight into it instead of a DMA copy after them --
                                        1 (default) for the blocking mirt_render_frame, 2 for
                                        mirt_render_frame_async too, 0 never. Pageable memory:
-                                       a copy. */ };
+                                       a copy. */
+       MIRT_OPT_QUEUE_ORDER = 18    /* wavefront: order of a frame's first bounces in the bounce
+                                       queue -- 0 (default) = tile order for the blocking
+                                       mirt_render_frame (a frame alone on the chip), grouped by
+                                       direction octant per workgroup for frames in flight;
+                                       1 = always grouped; 2 = always tile order. Speed only. */ };
 /* Traversal ids keep their first-release values (mirt 0.1: TILE 0, WAVEFRONT 5).
    ABI note: the mirt 0.2 header numbered WAVEFRONT 1; mirt_set_option accepts
    1 as a deprecated alias of MIRT_TRAV_WAVEFRONT (mirt_get_option reads back

@@ -683,6 +683,37 @@ def test_bounce_modes_identical(gpu, mirt, golden, drain, threshold, blocks):
     assert sha(img) == golden["frames"][key]["sha"]
 
 
+@pytest.mark.parametrize("order", [0, 1, 2])
+def test_queue_orders_identical(gpu, mirt, golden, order):
+    """MIRT_OPT_QUEUE_ORDER (the first bounces' queue order: auto, octant
+    groups, tile order) changes only who walks which chain when: the golden
+    1080p frame through the blocking call and through a device frame at the
+    bench's 384-workgroup grid."""
+    import torch
+    abi = mirt.abi
+    s, b = _scene(mirt, "render", 10000)
+    gpu.upload(s, b)
+    cam = mirt.default_camera()
+    key = "1920x1080_render10000_d5_m1_b1_s1_c0_step1"
+    out = torch.zeros((1080, 1920), dtype=torch.int32, device="cuda")
+    try:
+        gpu.set_option(abi.OPT_QUEUE_ORDER, order)
+        assert gpu.get_option(abi.OPT_QUEUE_ORDER) == order
+        img = gpu.render_frame(cam, 1920, 1080, depth=5, seed=1)
+        gpu.set_option(abi.OPT_BOUNCE_BLOCKS, 384)
+        gpu.render_frame_device(cam, mirt.frame_desc(1920, 1080, depth=5, seed=1), out.data_ptr(), None,
+                                torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        with pytest.raises(mirt.MirtError):
+            gpu.set_option(abi.OPT_QUEUE_ORDER, 3)
+    finally:
+        gpu.set_option(abi.OPT_QUEUE_ORDER, 0)
+        gpu.set_option(abi.OPT_BOUNCE_BLOCKS, 0)
+    assert sha(img) == golden["frames"][key]["sha"]
+    dev = out.cpu().numpy().view(np.uint8).reshape(1080, 1920, 4)
+    assert sha(dev) == golden["frames"][key]["sha"]
+
+
 def test_traversal_v02_alias(gpu, mirt):
     """the mirt 0.2 header's MIRT_TRAV_WAVEFRONT (1) is accepted as
     a deprecated alias and reads back as 5; the retired ids stay errors."""
