@@ -193,6 +193,5 @@ OPT_TRAVERSAL, OPT_FAST_SLAB, OPT_BLOCK_WAVES, OPT_DEFER, OPT_BOUNCE_THRESHOLD, 
     1, 2, 3, 4, 5, 6, 7)
 OPT_BOUNCE_BLOCKS, OPT_QUAD_DRAIN, OPT_LEAF_BATCH, OPT_QUAD_BATCH, OPT_ZERO_COPY = 9, 11, 14, 15, 17
 OPT_QUEUE_ORDER = 18
-OPT_PRIMARY_CHAIN = 19
 TRAV_TILE, TRAV_WAVEFRONT = 0, 5
 MULTI_COPY = 1

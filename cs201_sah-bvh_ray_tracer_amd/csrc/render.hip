@@ -1331,7 +1331,6 @@ struct mirt_ctx {
     size_t queue_cap = 0;
     bool lone_frame = false;    // mirt_render_frame's frame: the first bounces queued in tile order
     int queue_order = 0;        // MIRT_OPT_QUEUE_ORDER: 0 auto (tile order for lone_frame), 1 octants, 2 tile order
-    int primary_chain = 0;      // MIRT_OPT_PRIMARY_CHAIN: camera-packet passes one after another across ctxs
     uint32_t* d_defer = nullptr;  // [count, list...]
     size_t defer_cap = 0;
     unsigned long long* d_keys = nullptr;  // chunked brute force: per-ray (t, index) keys
@@ -1735,18 +1734,6 @@ AccumShare* accum_chain(const mirt_ctx* c)
     return c->acc && c->acc->refs > 1 ? c->acc : nullptr;
 }
 
-// The last camera-packet pass a ctx with MIRT_OPT_PRIMARY_CHAIN launched on a
-// device (process-wide; the ctxs of one frame loop share it).
-struct PrimaryChain {
-    hipEvent_t ev = nullptr;
-    bool has = false;
-};
-PrimaryChain& primary_chain(int device)
-{
-    static PrimaryChain chains[64];
-    return chains[device & 63];
-}
-
 // The first bounces grouped by direction octant in the queue (frames in
 // flight) or in tile order (a frame alone: the blocking call), or as
 // MIRT_OPT_QUEUE_ORDER forces.
@@ -1855,12 +1842,6 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
         const int pblocks = (ptiles + 3) / 4 + dfr.blocks;
         const int bblocks = c->bounce_blocks_opt ? c->bounce_blocks_opt : c->bounce_blocks;
         const size_t blds = bounce_lds_bytes(f.depth);
-        // MIRT_OPT_PRIMARY_CHAIN: this camera-packet pass starts after the
-        // one the process launched last on this device (any ctx): frames in
-        // flight then overlap one packet pass with the others' bounce passes
-        // instead of packet passes with each other
-        PrimaryChain& pc = primary_chain(c->device);
-        if (c->primary_chain && pc.has) HIP_TRY(hipStreamWaitEvent(s, pc.ev, 0));
         if (c->fast_slab && sc.ordered)
             primary_kernel<true, true><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl, octant_queue(c));
         else if (c->fast_slab)
@@ -1868,11 +1849,6 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
         else
             primary_kernel<false, false><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl, octant_queue(c));
         HIP_TRY(hipGetLastError());
-        if (c->primary_chain) {
-            if (!pc.ev) HIP_TRY(hipEventCreateWithFlags(&pc.ev, hipEventDisableTiming));
-            HIP_TRY(hipEventRecord(pc.ev, s));
-            pc.has = true;
-        }
         HIP_TRY(hipEventRecord(c->ph1[ps], s));
         if (d_bdiag && sc.wide)
             bounce_kernel<true, 2, true><<<bblocks, 256, blds, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, d_bdiag);
@@ -2768,10 +2744,6 @@ int mirt_set_option(mirt_ctx* c, int option, int value)
         if (value < 0 || value > 2) break;
         c->queue_order = value;
         return MIRT_OK;
-    case MIRT_OPT_PRIMARY_CHAIN:
-        if (value < 0 || value > 1) break;
-        c->primary_chain = value;
-        return MIRT_OK;
     case MIRT_OPT_LEAF_BATCH:
         if (value < 0 || value > 2) break;
         c->leaf_batch_opt = value;
@@ -2802,7 +2774,6 @@ int mirt_get_option(mirt_ctx* c, int option)
     if (option == MIRT_OPT_QUAD_BATCH) return c->quad_batch;
     if (option == MIRT_OPT_ZERO_COPY) return c->zero_copy;
     if (option == MIRT_OPT_QUEUE_ORDER) return c->queue_order;
-    if (option == MIRT_OPT_PRIMARY_CHAIN) return c->primary_chain;
     if (option == MIRT_OPT_LEAF_BATCH) return leaf_batch(c) ? 1 : 0;  // in effect for the uploaded scene
     set_error("mirt_get_option: bad option %d", option);
     return MIRT_E_INVALID;

@@ -419,16 +419,11 @@ enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3,
                                        1 (default) for the blocking mirt_render_frame, 2 for
                                        mirt_render_frame_async too, 0 never. Pageable memory:
                                        a copy. */
-       MIRT_OPT_QUEUE_ORDER = 18,   /* wavefront: order of a frame's first bounces in the bounce
+       MIRT_OPT_QUEUE_ORDER = 18    /* wavefront: order of a frame's first bounces in the bounce
                                        queue -- 0 (default) = tile order for the blocking
                                        mirt_render_frame (a frame alone on the chip), grouped by
                                        direction octant per workgroup for frames in flight;
-                                       1 = always grouped; 2 = always tile order. Speed only. */
-       MIRT_OPT_PRIMARY_CHAIN = 19  /* wavefront: 1 = this ctx's camera-packet pass waits for the
-                                       last one any ctx with this option launched on the device
-                                       (frames in flight overlap a packet pass with bounce
-                                       passes, not with another packet pass); 0 (default) = no
-                                       wait. Speed only. */ };
+                                       1 = always grouped; 2 = always tile order. Speed only. */ };
 /* Traversal ids keep their first-release values (mirt 0.1: TILE 0, WAVEFRONT 5).
    ABI note: the mirt 0.2 header numbered WAVEFRONT 1; mirt_set_option accepts
    1 as a deprecated alias of MIRT_TRAV_WAVEFRONT (mirt_get_option reads back
