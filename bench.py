@@ -103,6 +103,10 @@ DEFAULT_BATCH = {1: 1, 2: 1, 4: 4, 8: 4}
 # a gather-sized copy on a fifth stream 11.9 Grays/s, 8 queues 13.2; 8 ctxs on
 # 8 queues without the copy 15.2; profiles/r03f/)
 PIPELINE_MULTI, HW_QUEUES_MULTI = 8, 16
+# at N = 1 the environment's queues stay (0): 8 queues for the four contexts
+# measured 2,662-2,674 vs 2,625-2,633 in one session (profiles/r04an/) and
+# 2,621-2,654 vs 2,617-2,664 in the next (three rounds, profiles/r04ao/)
+HW_QUEUES_SINGLE = 0
 # the last TAIL_GRID launches of a timed burst run their bounce pass on the
 # full persistent grid: with frames in flight every launch takes 1.5
 # workgroups per CU so the frames share the chip, but the burst's last frame
@@ -542,6 +546,9 @@ def main():
     ap.add_argument("--rank-timeout", type=float, default=420.0,
                     help="N > 1 started by this script: seconds before a still-running job is terminated (exit "
                          "124); each rank's process group times out 30 s earlier")
+    ap.add_argument("--hw-queues", type=int, default=-1,
+                    help="raise GPU_MAX_HW_QUEUES to this before the HIP runtime starts (-1: the environment's at "
+                         "N = 1, 16 at N > 1; 0: keep the environment's)")
     ap.add_argument("--blocking-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--opt", action="append", default=[],
                     help="OPTION=VALUE (mirt_set_option on every context; A/B of schedule options), repeatable")
@@ -572,7 +579,8 @@ def main():
     # on one device); the same launches, shard geometry, gathers (staged
     # through host memory) and max-over-ranks timing. Not a measurement.
     rehearse = world > 1 and os.environ.get("MIRT_BENCH_SHARE_GPU") == "1"
-    if world > 1 and not rehearse:
+    want_q = args.hw_queues if args.hw_queues >= 0 else (HW_QUEUES_MULTI if world > 1 else HW_QUEUES_SINGLE)
+    if want_q and not rehearse:
         # one hardware queue per context stream plus RCCL's, read when the HIP
         # runtime starts (before the first GPU call below). The GPU boxes export
         # GPU_MAX_HW_QUEUES=4 (HIP's default), which would put the 8 contexts
@@ -583,8 +591,8 @@ def main():
             have = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
         except ValueError:
             have = 0
-        if have < HW_QUEUES_MULTI:
-            os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES_MULTI)
+        if have < want_q:
+            os.environ["GPU_MAX_HW_QUEUES"] = str(want_q)
     dev = (0 if rehearse else local) if world > 1 else 0
     if world > 1:
         torch.cuda.set_device(dev)
