@@ -1,64 +1,56 @@
 """Headline benchmark: Mrays/s of the primary-ray render path at 1920x1080 with
 10,000 random spheres (BASELINE.json configs[1]): camera rays -> BVH
 traversal + ray/sphere tests -> diffuse shading (depth 5, the reference's
-MAX_DEPTH, main.c:19/366) -> RGBA8 framebuffer.
+MAX_DEPTH, main.c:19/366) -> RGBA8 framebuffer IN HOST MEMORY (SURVEY §8(d)
+t_frame: the end point of main.c:371-372's display).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...     (N > 1)
+    torchrun --nproc-per-node N bench.py --gpus N ...
 
-`python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment
-starts the N rank processes itself (one per GPU, MASTER_ADDR 127.0.0.1); the
-parent never touches the GPU and exits with the worst rank's status.
+Every N runs the C-ABI multi-GPU renderer of include/mirt_multi.h -- the
+path a C caller of main.c's loop uses -- in ONE process:
+mirt_multi_create over devices 0..N-1 (RCCL communicators from
+ncclCommInitAll), the scene replicated, `pipeline` lanes of per-GPU contexts
+keeping launches in flight, and every frame gathered and delivered into
+page-locked host memory. A step is ONE fresh frame (main.c:358-374) split N
+ways by interleaved 8-row blocks ("scaling": "strong"); value = W*H*spp*K /
+the timed region (mirt_multi_wait + wall clock on both sides: every frame of
+the K steps has reached host memory when the clock stops).
 
-One step at N GPUs = N successive frames of the reference's accumulating
-display loop (main.c:379-408: the camera holds still, frame j adds RNG sample
-j), each 1920x1080 at 1 primary ray per pixel: every rank renders its
-interleaved 8-row blocks of all N frames in ONE launch into its HBM slabs
-(scene resident, uploaded once), folds them into its accumulation buffer on
-the device, and for N > 1 the displayed slabs are gathered to rank 0 over
-RCCL and de-interleaved there. Per-GPU work is one frame's worth of rays
-whatever N is ("scaling": "weak"). At N > 1 the line also carries
-`value_strong`: ONE frame split N ways per step, timed the same way (its
-per-GPU launch shrinks with N until the bounce pass's longest chains set the
-time); `--scaling strong` makes that the headline. value = W*H primary rays
-per frame * frames per step * K / (max over ranks of the timed region).
+Processes. N = 1 measures in this process. N > 1: this process never
+touches a GPU; it starts ONE fresh child (`--measure-child`) with
+GPU_MAX_HW_QUEUES raised to 16 in its environment (read when the child's
+HIP runtime starts: one hardware queue per lane's stream) and relays its
+line; a child still running after --rank-timeout seconds is terminated and
+the parent exits 124. Under torchrun the same happens in rank 0; the other
+ranks hold no GPU work and join rank 0 only at a gloo barrier at the end.
 
-Successive steps are quadruple-buffered (`--pipeline 4`, default): four device
-contexts with the scene resident in each take turns on their own streams (one
-per hardware queue), so step k + 1's launches fill the CU slots that step k's
-bounce pass frees while its last chains drain. With frames in flight each
-context's persistent bounce pass runs 1.5 workgroups per CU
-(`--bounce-blocks`, MIRT_OPT_BOUNCE_BLOCKS; a launch alone keeps the full
-occupancy x CUs): the four frames' passes then share the chip instead of the
-first holding every slot. Each frame is still rendered whole and its bytes do
-not change; only the gap between frames closes. The timed region brackets all
-K steps (barrier + synchronize on both sides).
+The schedule: `pipeline` lanes (4 at N = 1, 8 at N > 1), each
+context's bounce pass at 1.5 persistent workgroups per CU, `batch` frames
+per launch (1 at N <= 2, 4 at N >= 4), the burst's last `tail_grid`
+launches on the full grid at N > 1 (mirt_multi's MIRT_MULTI_FULL_GRID).
 
-Also in the line (N = 1): `host_inclusive_mrays_s`, SURVEY §8(d)'s t_frame
-(call -> RGBA8 frame in host memory): the same four contexts, each frame's
-D2H copy into page-locked memory enqueued behind its kernels
-(mirt_render_frame_async) so it overlaps the next frame; the blocking
-single-call rate into pageable memory beside it. `roofline`: the dominant
-kernel (the bounce pass) priced per §8(d) plus the bound the PMC counters
-measured (profiles/r02_pmc_bound.json). `cpu_baseline`: the unmodified
-reference sources (oracle/_ref) on this host's cores.
+Also in the line: `device_resident_mrays_s` (the same loop with the frames
+left in device 0's HBM: the previous rounds' headline), depth 1, the
+blocking call per frame (N = 1, a child process holding one context, as
+main.c's loop runs), `roofline` (the bounce kernel on its binding unit, the
+vector-memory gather path; profiles/), `cpu_baseline` (the unmodified
+reference sources, oracle/_ref, on this host's cores; N = 1 only).
 
-`--dry` (CPU only, gloo): the same launcher, shard geometry, gather and
-max-over-ranks timing with a synthetic slab in place of the GPU frame --
-a plumbing check for CPU tests; its line says "dry": true and is no measurement.
+`--dry` (CPU only): the launcher, the shard geometry and both deliveries'
+index math (multi.hip's de-interleave and strided host copies, restated in
+shard.py) over synthetic slabs -- a plumbing check; its line says "dry": true.
 """
 import argparse
 import importlib
 import json
 import os
-import socket
 import subprocess
 import sys
 import time
 
 import numpy as np
 import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -129,7 +121,7 @@ KERNEL = "bounce_kernel<true, 2, false>"   # dominant kernel of the default (wav
 # the PMC-derived bound of the timed launch shape, per workload
 # (scripts/pmc_bench.sh over this script's own command + scripts/pmc_summary.py);
 # the newest round's file wins
-PMC_BOUND = {wl: [os.path.join(ROOT, "profiles", f"r0{r}_pmc_bound_{wl}.json") for r in (4, 3)] for wl in WORKLOADS}
+PMC_BOUND = {wl: [os.path.join(ROOT, "profiles", f"r0{r}_pmc_bound_{wl}.json") for r in (5, 4, 3)] for wl in WORKLOADS}
 # the chip's gather peak by access shape (scripts/td_probe.hip + its counter
 # passes, scripts/td_probe_summary.py): the roofline's denominator
 TD_PROBE = os.path.join(ROOT, "profiles", "r04_td_probe.json")
@@ -277,124 +269,7 @@ def cpu_baseline(target_s=10.0):
     return out
 
 
-# ------------------------------------------------------------- launching
-
-def free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
-def spawn_ranks(n, deadline_s):
-    """Start n copies of this script as ranks 0..n-1 (the torchrun contract's
-    environment) and wait; a failing rank ends the others. Runs before any
-    GPU call in this process (the ranks are fresh processes, never a re-exec).
-    A job still running after `deadline_s` seconds (a rank stuck in RCCL init
-    or a gather) is ended: every rank is terminated (killed 5 s later if it
-    ignores that), the stuck ranks are named on stderr and the parent exits
-    124, so the driver records a failure instead of waiting out its limit."""
-    port = free_port()
-    procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rc = 0
-    live = list(procs)
-    t_end = time.monotonic() + deadline_s
-    while live:
-        for p in list(live):
-            code = p.poll()
-            if code is None:
-                continue
-            live.remove(p)
-            if code != 0 and rc == 0:
-                rc = code if code > 0 else 128 - code
-                for q in live:
-                    q.terminate()
-        if live and time.monotonic() > t_end:
-            stuck = [procs.index(p) for p in live]
-            print(f"bench.py: ranks {stuck} still running after the {deadline_s:.0f} s deadline "
-                  "(--rank-timeout); terminating the job", file=sys.stderr, flush=True)
-            for q in live:
-                q.terminate()
-            t_kill = time.monotonic() + 5.0
-            for q in live:
-                try:
-                    q.wait(timeout=max(0.1, t_kill - time.monotonic()))
-                except subprocess.TimeoutExpired:
-                    q.kill()
-                    q.wait()
-            return 124
-        time.sleep(0.05)
-    return rc
-
-
-def pg_timeout(args):
-    """The process group's timeout: a collective (or the rendezvous) that
-    waits longer raises in the rank instead of hanging it."""
-    import datetime
-    return datetime.timedelta(seconds=max(10.0, args.rank_timeout - 30.0))
-
-
-def timed(world, launches, body):
-    """barrier + synchronize, body(*l) for every launch l of the timed steps,
-    synchronize + barrier; seconds."""
-    cuda = torch.cuda.is_initialized()
-    if world > 1:
-        dist.barrier()
-    if cuda:
-        torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for launch in launches:
-        body(*launch)
-    if cuda:
-        torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    return time.perf_counter() - t0
-
-
-def dry_main(args, world, rank):
-    """CPU plumbing check: synthetic slabs through the shard geometry, the
-    gather and the timing of the GPU path (gloo). MIRT_BENCH_DRY_HANG=r makes
-    rank r ("all": every rank) sleep before joining (the deadline tests)."""
-    if os.environ.get("MIRT_BENCH_DRY_HANG") in (str(rank), "all"):
-        time.sleep(3600)
-    if world > 1:
-        dist.init_process_group("gloo", timeout=pg_timeout(args))
-    fd = mirt.frame_desc(W, H, depth=DEPTH, row_block=ROW_BLOCK, shard=rank, num_shards=world)
-    rows = mirt.shard_rows(fd)
-    slab = torch.zeros((shard.slab_rows(H, ROW_BLOCK, world), W), dtype=torch.int32)
-    slab[:len(rows)] = torch.from_numpy(rows.astype(np.int64)[:, None] * W + np.arange(W)).to(torch.int32)
-    frame = [None]
-
-    def step():
-        frame[0] = shard.gather_frame(slab, H, ROW_BLOCK) if world > 1 else shard.assemble(slab[None], H, ROW_BLOCK)
-
-    for _ in range(args.warmup):
-        step()
-    el = timed(world, [()] * args.steps, step)
-    t = torch.tensor([el], dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    if rank == 0:
-        want = torch.arange(H * W, dtype=torch.int64).reshape(H, W).to(torch.int32)
-        ok = bool(torch.equal(frame[0], want))
-        print(json.dumps({"metric": METRIC, "value": None, "unit": "Mrays/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-                          "ms_per_step": None, "higher_is_better": True,
-                          "scaling": args.scaling, "vs_baseline": None, "dtype": "f32", "dry": True,
-                          "data": "synthetic slabs (no rendering): launcher / gather plumbing check",
-                          "frame_assembled_ok": ok, "gather_ms_per_step": round(float(t[0]) / args.steps * 1e3, 4),
-                          "config": {"workload": WORKLOADS[args.workload]["desc"], "name": args.workload,
-                                     "parallelism": f"row-block shard x{world}" + (" + gloo gather" if world > 1 else "")}}),
-              flush=True)
-    if world > 1:
-        dist.destroy_process_group()
-    return 0
-
-
-# ------------------------------------------------------------------ main
+# ------------------------------------------------------------------ roofline
 
 def load_pmc_bound(name):
     """The PMC-derived bound of the frame kernels of workload `name` in the
@@ -515,232 +390,323 @@ def bound_line(pb, exec_b, ref_b, ms):
             "executed_vs_reference_bytes": round(exec_b / max(ref_b, 1), 4)}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--no-host", action="store_true", help="skip the host-inclusive (D2H) leg")
-    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="1080p_10k")
-    ap.add_argument("--pipeline", type=int, default=0,
-                    help="device contexts alternating successive launches on their own streams (1 = serial; "
-                         "0 = 4 at N = 1, 8 at N > 1)")
-    ap.add_argument("--bounce-blocks", type=int, default=-1,
-                    help="persistent bounce workgroups per launch (MIRT_OPT_BOUNCE_BLOCKS) in the timed loop; "
-                         "-1 = the workload's BB_PER_CU (1.5 unless stated) per CU with frames in flight "
-                         "(--pipeline > 1), else 0 (occupancy x CUs)")
-    ap.add_argument("--scaling", choices=("weak", "strong"), default="strong",
-                    help="strong (default): every step is ONE frame (the N = 1 workload) split N ways, frames in "
-                         "flight; weak: N frames per step at N GPUs (reported beside it as value_weak)")
-    ap.add_argument("--batch", type=int, default=0,
-                    help="steps' frames per launch (frames in flight inside a launch; 0 = DEFAULT_BATCH[N])")
-    ap.add_argument("--tail-grid", type=int, default=-1,
-                    help="the last N launches of a timed burst take the full persistent bounce grid (nothing "
-                         "later will share the chip); 0 = every launch at --bounce-blocks; -1 = TAIL_GRID at "
-                         "N = 1, TAIL_GRID_MULTI at N > 1")
-    ap.add_argument("--accumulate", action="store_true",
-                    help="time the still-camera accumulating display loop (shared accumulation buffer) instead "
-                         "of fresh frames")
-    ap.add_argument("--dry", action="store_true", help="CPU plumbing check over gloo (no GPU, no measurement)")
-    ap.add_argument("--rank-timeout", type=float, default=420.0,
-                    help="N > 1 started by this script: seconds before a still-running job is terminated (exit "
-                         "124); each rank's process group times out 30 s earlier")
-    ap.add_argument("--hw-queues", type=int, default=-1,
-                    help="raise GPU_MAX_HW_QUEUES to this before the HIP runtime starts (-1: the environment's at "
-                         "N = 1, 16 at N > 1; 0: keep the environment's)")
-    ap.add_argument("--blocking-child", action="store_true", help=argparse.SUPPRESS)
-    ap.add_argument("--opt", action="append", default=[],
-                    help="OPTION=VALUE (mirt_set_option on every context; A/B of schedule options), repeatable")
-    args = ap.parse_args()
-    global W, H, NSPH, KIND, SPP, JITTER, WORKLOAD
-    WORKLOAD = args.workload
-    wl = WORKLOADS[args.workload]
-    W, H, NSPH, KIND, SPP, JITTER = wl["W"], wl["H"], wl["NSPH"], wl["KIND"], wl["SPP"], wl["JITTER"]
+# ------------------------------------------------------------- launching
 
-    if args.blocking_child:
-        return blocking_child()
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        return spawn_ranks(args.gpus, args.rank_timeout)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}; measuring {world} rank(s)", file=sys.stderr)
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    if args.dry:
-        return dry_main(args, world, rank)
-    if not args.pipeline:
-        args.pipeline = 4 if world == 1 else PIPELINE_MULTI
-    if args.tail_grid < 0:
-        args.tail_grid = TAIL_GRID if world == 1 else TAIL_GRID_MULTI
-    # MIRT_BENCH_SHARE_GPU=1: a rehearsal of the N > 1 path on a one-GPU box --
-    # every rank on device 0 and gloo in place of RCCL (which refuses two ranks
-    # on one device); the same launches, shard geometry, gathers (staged
-    # through host memory) and max-over-ranks timing. Not a measurement.
-    rehearse = world > 1 and os.environ.get("MIRT_BENCH_SHARE_GPU") == "1"
-    want_q = args.hw_queues if args.hw_queues >= 0 else (HW_QUEUES_MULTI if world > 1 else HW_QUEUES_SINGLE)
-    if want_q and not rehearse:
-        # one hardware queue per context stream plus RCCL's, read when the HIP
-        # runtime starts (before the first GPU call below). The GPU boxes export
-        # GPU_MAX_HW_QUEUES=4 (HIP's default), which would put the 8 contexts
-        # and RCCL on 4 queues: the one-frame split emulated per shard ran 11.9
-        # Grays/s at N = 8 there against 13.8 on 16 (profiles/r03f/, r03g/), so
-        # a lower value is raised to HW_QUEUES_MULTI (one rank per GPU)
+def spawn_child(extra_env, deadline_s, argv):
+    """Run this script again as a FRESH process (never a re-exec: the caller
+    has not touched the GPU, and the child is a new program) with `argv`,
+    relaying its output. A child still running after `deadline_s` seconds
+    (a rank stuck in RCCL init or a gather) is terminated (killed 5 s later if
+    it ignores that) and 124 is returned, so the driver records a failure
+    instead of waiting out its own limit."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK")}
+    env.update(extra_env)
+    p = subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env)
+    try:
+        return p.wait(timeout=deadline_s)
+    except subprocess.TimeoutExpired:
+        print(f"bench.py: the measuring process (pid {p.pid}) is still running after the {deadline_s:.0f} s "
+              "deadline (--rank-timeout); terminating it", file=sys.stderr, flush=True)
+        p.terminate()
         try:
-            have = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
-        except ValueError:
-            have = 0
-        if have < want_q:
-            os.environ["GPU_MAX_HW_QUEUES"] = str(want_q)
-    dev = (0 if rehearse else local) if world > 1 else 0
-    if world > 1:
-        torch.cuda.set_device(dev)
-        if rehearse:
-            dist.init_process_group("gloo", timeout=pg_timeout(args))
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=pg_timeout(args))
-    else:
-        torch.cuda.set_device(0)
+            p.wait(timeout=5.0)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+        return 124
 
+
+def child_argv():
+    """This process's arguments plus --measure-child (for spawn_child)."""
+    return [a for a in sys.argv[1:] if a != "--measure-child"] + ["--measure-child"]
+
+
+def launcher_main(args, world_env, rank):
+    """N > 1 (or --dry): the parent / every torchrun rank. Rank 0 (or the
+    lone parent) measures in one fresh child over all N GPUs; other torchrun
+    ranks only meet rank 0 at the end."""
+    import datetime
+
+    import torch.distributed as dist
+    pg = world_env > 1
+    if pg:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=args.rank_timeout + 60.0))
+    rc = 0
+    if rank == 0:
+        q = args.hw_queues if args.hw_queues >= 0 else (HW_QUEUES_MULTI if args.gpus > 1 else HW_QUEUES_SINGLE)
+        env = {}
+        if q and not args.dry:
+            try:
+                have = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
+            except ValueError:
+                have = 0
+            if have < q:
+                env["GPU_MAX_HW_QUEUES"] = str(q)
+        rc = spawn_child(env, args.rank_timeout, child_argv())
+    if pg:
+        # the job ends together: rank 0 reports the child's status
+        t = torch.tensor([rc], dtype=torch.int64)
+        dist.broadcast(t, src=0)
+        rc = int(t[0])
+        dist.barrier()
+        dist.destroy_process_group()
+    return rc
+
+
+def dry_main(args):
+    """CPU plumbing check (the measuring child with --dry): synthetic shard
+    slabs through both deliveries' index math (shard.py's restatements of
+    multi.hip's deinterleave_kernel and strided host copies), the frame plan
+    and the timing. MIRT_BENCH_DRY_HANG=1 makes the child hang (the deadline
+    tests)."""
+    if os.environ.get("MIRT_BENCH_DRY_HANG") == "1":
+        time.sleep(3600)
+    n = args.gpus
+    frames = frames_per_launch(args, n)
+    slabs = []
+    for s in range(n):
+        fd = mirt.frame_desc(W, H, depth=DEPTH, row_block=ROW_BLOCK, shard=s, num_shards=n)
+        rows = mirt.shard_rows(fd).astype(np.int64)
+        # frame j's pixel (y, x) = j * H * W + y * W + x
+        slabs.append(np.stack([(j * H + rows[:, None]) * W + np.arange(W) for j in range(frames)]).astype(np.int64))
+    want = np.arange(frames * H * W, dtype=np.int64).reshape(frames, H, W)
+    t0 = time.perf_counter()
+    got_g = shard.assemble_gather(slabs, H, ROW_BLOCK)
+    got_d = shard.assemble_direct(slabs, H, ROW_BLOCK)
+    dt = time.perf_counter() - t0
+    ok = bool((got_g == want).all() and (got_d == want).all())
+    print(json.dumps({"metric": METRIC, "value": None, "unit": "Mrays/s", "n_gpus": n, "steps": args.steps,
+                      "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "strong",
+                      "vs_baseline": None, "dtype": "f32", "dry": True,
+                      "data": "synthetic slabs (no rendering): launcher / shard geometry / delivery plumbing check",
+                      "frame_assembled_ok": ok, "assemble_ms": round(dt * 1e3, 3),
+                      "config": {"workload": WORKLOADS[args.workload]["desc"], "name": args.workload,
+                                 "frames_per_launch": frames,
+                                 "parallelism": f"row-block shard x{n}, one process (mirt_multi)"}}), flush=True)
+    return 0
+
+
+# ------------------------------------------------------------- the frame loop
+
+def frame_desc_for(f0, n, depth, accumulate):
+    """The descriptor of a launch of frames f0 .. f0 + n - 1: fresh frames
+    (main.c:358-374) of RNG samples f0 * SPP ..., or successive frames of
+    the still-camera display loop (main.c:379-408) with --accumulate; a
+    frame of SPP > 1 jittered samples is one launch of its own."""
+    acc = accumulate and f0 > 0
+    return mirt.frame_desc(W, H, depth=depth, seed=SEED, sample=f0 * SPP, accumulate=acc,
+                           frames=f0 * SPP + 1 if acc else 1, row_block=ROW_BLOCK, samples=SPP if n == 1 else 1,
+                           jitter=JITTER)
+
+
+def plan(f0, steps, per):
+    """(first frame, frames) of the launches covering `steps` frames from f0"""
+    out, f, end = [], f0, f0 + steps
+    while f < end:
+        k = min(per, end - f)
+        out.append((f, k))
+        f += k
+    return out
+
+
+def run_launches(m, cam, launches, bufs, depth, accumulate=False, tail=(), device_only=False):
+    """Enqueue every launch (on lane m.launches % lanes, frame j into
+    bufs[lane][j]; device_only: the frames stay on the devices)."""
+    for f0, k in launches:
+        lane = m.launches % m.lanes
+        outs = None if device_only else bufs[lane][:k]
+        m.render_frames_async(cam, frame_desc_for(f0, k, depth, accumulate), outs, nframes=k, full_grid=f0 in tail)
+
+
+def timed_loop(m, cam, warm, timed_launches, bufs, depth, accumulate=False, tail=(), device_only=False):
+    """Warm-up launches, then the timed ones bracketed by mirt_multi_wait on
+    both sides (every frame delivered when the clock stops); seconds."""
+    run_launches(m, cam, warm, bufs, depth, accumulate, (), device_only)
+    m.wait()
+    t0 = time.perf_counter()
+    run_launches(m, cam, timed_launches, bufs, depth, accumulate, tail, device_only)
+    m.wait()
+    return time.perf_counter() - t0
+
+
+def make_scene():
     spheres = (mirt.create_random_spheres(NSPH, SEED) if KIND == "render"
                else mirt.create_benchmark_spheres(NSPH, SEED))
     t0 = time.perf_counter()
     bvh = mirt.build_bvh(spheres)
-    build_s = time.perf_counter() - t0
-    rs = [mirt.Renderer(dev) for _ in range(max(1, args.pipeline))]
-    # bounce workgroups per launch with frames in flight (measured: 1080p/10k
-    # 2,400 -> 2,650 Mrays/s at 4 contexts, profiles/r02_ab/r02au_*); the
-    # serial measurement loop and the blocking call below use the full grid
+    return spheres, bvh, time.perf_counter() - t0
+
+
+def open_multi(n, lanes, host_direct, spheres, bvh, blocks, opts, timeout_ms=120000):
+    m = mirt.MultiRenderer(list(range(n)), lanes=lanes, host_direct=host_direct)
+    m.set_option(mirt.abi.MULTI_OPT_TIMEOUT_MS, timeout_ms)
+    m.upload(spheres, bvh)
+    if blocks >= 0:
+        m.set_option(mirt.abi.OPT_BOUNCE_BLOCKS, blocks)
+    for ov in opts:
+        o, v = (int(t) for t in ov.split("="))
+        m.set_option(o, v)
+    return m
+
+
+def host_bufs(lanes, per):
+    return [[mirt.HostBuffer((H, W, 4)) for _ in range(per)] for _ in range(lanes)]
+
+
+def close_bufs(bufs):
+    for lane in bufs:
+        for b in lane:
+            b.close()
+
+
+def frames_per_launch(args, n):
+    if SPP > 1 and not args.accumulate:
+        return 1             # one fresh frame of SPP samples per launch (the fold restarts per launch)
+    return args.batch if args.batch > 0 else DEFAULT_BATCH.get(n, 1 if n <= 2 else 4)
+
+
+def schedule(args, n):
+    """(lanes, frames per launch, tail launches, bounce workgroups) of the timed loop at n GPUs."""
+    lanes = args.pipeline or (4 if n == 1 else PIPELINE_MULTI)
+    per = frames_per_launch(args, n)
+    tail = args.tail_grid if args.tail_grid >= 0 else (TAIL_GRID if n == 1 else TAIL_GRID_MULTI)
     blocks = args.bounce_blocks
     if blocks < 0:
-        cus = torch.cuda.get_device_properties(dev).multi_processor_count
-        blocks = int(wl.get("BB_PER_CU", 1.5) * cus) if len(rs) > 1 else 0
-    for x in rs:
-        x.upload(spheres, bvh)
-        x.set_option(mirt.abi.OPT_BOUNCE_BLOCKS, blocks)
-        for ov in args.opt:
-            o, v = (int(t) for t in ov.split("="))
-            x.set_option(o, v)
-    r = rs[0]
+        cus = torch.cuda.get_device_properties(0).multi_processor_count
+        blocks = int(WORKLOADS[WORKLOAD].get("BB_PER_CU", 1.5) * cus) if lanes > 1 else 0
+    return lanes, per, tail, blocks
+
+
+def tail_of(launches, tail, lanes, blocks):
+    if lanes < 2 or not blocks or tail <= 0:
+        return set()
+    return {f0 for f0, _ in launches[-tail:]}
+
+
+def measure(args):
+    """The GPU measurement over args.gpus devices in THIS process."""
+    n = args.gpus
+    lanes, per, tail_n, blocks = schedule(args, n)
+    spheres, bvh, build_s = make_scene()
     cam = mirt.default_camera()
-    # The steps are successive frames, `fps` per step: 1 (strong, the N = 1
-    # workload at every N) or N (weak). A frame is main.c:358-374's fresh
-    # frame (the camera moved), shown after its SPP samples (4k_1m_4spp: 4
-    # jittered samples folded like main.c:379-408's accumulation); with
-    # --accumulate the frames are instead successive frames of the
-    # still-camera display loop (main.c:379-408), the ctxs sharing one
-    # accumulation buffer (mirt_ctx_share_accum). A launch carries `batch`
-    # steps' frames (frames in flight inside one launch; each frame's display
-    # its own slab) and, at N > 1, every displayed frame is gathered to rank 0.
-    fps = world if args.scaling == "weak" else 1
-    batch = args.batch if args.batch > 0 else DEFAULT_BATCH.get(world, 1)
-    if SPP > 1 and not args.accumulate:
-        batch = 1          # one fresh frame of SPP samples per launch (the fold restarts per launch)
-    per_launch = fps * batch if SPP == 1 or args.accumulate else 1
-    if SPP > 1 and not args.accumulate and fps > 1:
-        raise SystemExit("--scaling weak with several samples per frame needs --accumulate")
-    sf = shard.ShardedFrame(r, W, H, ROW_BLOCK, samples=SPP * per_launch, renderers=rs,
-                            share_accum=args.accumulate, accum=SPP > 1 or args.accumulate)
-    my_rows = shard.shard_row_count(H, ROW_BLOCK, world, rank)
+    m = open_multi(n, lanes, args.delivery == "host-direct", spheres, bvh, blocks, args.opt)
+    bufs = host_bufs(lanes, per)
+    warm = plan(0, args.warmup, per)
+    timed_launches = plan(args.warmup, args.steps, per)
+    tail = tail_of(timed_launches, tail_n, lanes, blocks)
+    elapsed = timed_loop(m, cam, warm, timed_launches, bufs, DEPTH, args.accumulate, tail)
+    # the last frame delivered must be the frame one context renders alone
+    last_f0, last_k = timed_launches[-1]
+    last_lane = (m.launches - 1) % lanes
+    last_frame = bufs[last_lane][last_k - 1].array.copy()
+    # the passes of rank 0's timed launches (HIP events on each launch's own
+    # stream, under the overlap of the lanes in flight)
+    phases = []
+    for lane in range(lanes):
+        k_lane = sum(1 for i in range(len(warm), len(warm) + len(timed_launches)) if i % lanes == lane)
+        if k_lane:
+            phases += m.phase_log(lane, 0, min(k_lane, 64))
+    primary_ms, bounce_ms = (float(v) for v in np.mean(np.array(phases), axis=0)) if phases else (0.0, 0.0)
+    # the same loop with the frames left on the devices (no D2H)
+    el_dev = timed_loop(m, cam, plan(0, 2, per), plan(args.warmup, args.steps, per), bufs, DEPTH, args.accumulate,
+                        tail, device_only=True)
+    # depth 1 (camera rays and their shading only), frames to host memory
+    el_d1 = timed_loop(m, cam, plan(0, 2, per), plan(args.warmup, args.steps, per), bufs, 1, False, tail)
+    m.close()
+    close_bufs(bufs)
+    # the last delivered frame against one context rendering the same frame
+    # alone (the N-GPU frame must equal the one-GPU frame byte for byte)
+    same = None
+    if not args.accumulate:
+        with mirt.Renderer(0) as r1:
+            r1.upload(spheres, bvh)
+            one = r1.render_frame(cam, W, H, depth=DEPTH, seed=SEED, sample=(last_f0 + last_k - 1) * SPP,
+                                  samples=SPP, jitter=JITTER)
+        same = frame_sha(one) == frame_sha(last_frame)
+    # the other delivery at N > 1 (a second renderer, same schedule)
+    other = None
+    if n > 1 and not args.no_other:
+        od = "gather" if args.delivery == "host-direct" else "host-direct"
+        m2 = open_multi(n, lanes, od == "host-direct", spheres, bvh, blocks, args.opt)
+        bufs2 = host_bufs(lanes, per)
+        el2 = timed_loop(m2, cam, plan(0, args.warmup, per), plan(args.warmup, args.steps, per), bufs2, DEPTH,
+                         args.accumulate, tail)
+        other = {"delivery": od, "mrays_s": round(W * H * SPP * args.steps / el2 / 1e6, 3),
+                 "ms_per_step": round(el2 / args.steps * 1e3, 4)}
+        m2.close()
+        close_bufs(bufs2)
 
-    # algorithmic work of one full launch of this rank (instrumented build,
-    # untimed): the walk as configured (pruned), and the reference's
-    # exhaustive DFS
-    counts = r.count_frame(cam, W, H, depth=DEPTH, seed=SEED, row_block=ROW_BLOCK, shard=rank, num_shards=world,
-                           samples=SPP * per_launch, jitter=JITTER)
+    value = W * H * SPP * args.steps / elapsed / 1e6
+    line = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "Mrays/s",
+        "n_gpus": n,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (create_random_sphere scene, srand(1); default camera main.c:203-211)",
+        "config": {"workload": WORKLOADS[WORKLOAD]["desc"], "name": WORKLOAD,
+                   "width": W, "height": H, "spheres": NSPH, "scene": KIND, "max_depth": DEPTH, "spp": SPP,
+                   "jitter": JITTER, "frames_per_step": 1, "frames_per_launch": per,
+                   "launches": len(timed_launches), "pipeline": lanes, "bounce_blocks": blocks,
+                   "tail_grid": len(tail), "bvh_nodes": len(bvh), "row_block": ROW_BLOCK,
+                   "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+                   "delivery": args.delivery,
+                   "step": ("1 frame of the still-camera display loop (main.c:379-408), lanes sharing one "
+                            "accumulation buffer" if args.accumulate else "1 fresh frame (main.c:358-374)")
+                           + f", {SPP} sample(s), {per} frame(s) per launch, launches rotating over {lanes} lanes, "
+                             "every frame delivered to page-locked host memory",
+                   "parallelism": (f"row-block shard x{n}, one process: mirt_multi over ncclCommInitAll, "
+                                   + ("RCCL gather to GPU 0 + D2H" if args.delivery == "gather"
+                                      else "per-GPU strided D2H into the host frame"))},
+        "timing": "one process drives all GPUs (include/mirt_multi.h); the timed region is bracketed by "
+                  "mirt_multi_wait on both sides, so it ends when every frame is in host memory on every lane",
+        "device_resident_mrays_s": round(W * H * SPP * args.steps / el_dev / 1e6, 3),
+        "device_resident_note": "the same launches with the frames left on the devices (gathered on GPU 0; no D2H)",
+        "depth1_mrays_s": round(W * H * SPP * args.steps / el_d1 / 1e6, 3),
+        "bvh_build_s": round(build_s, 4),
+        "frame_sha_last": frame_sha(last_frame),
+        "last_frame_equals_one_context": same,
+        "phases_under_overlap_ms": {"primary": round(primary_ms, 4), "bounce": round(bounce_ms, 4),
+                                    "launches": len(phases)},
+    }
+    if other:
+        line["value_" + other["delivery"].replace("-", "_")] = other["mrays_s"]
+        line["other_delivery"] = other
+    if args.opt:
+        line["options"] = args.opt
+    if n == 1:
+        line.update(single_gpu_extras(args, spheres, bvh, cam, value, elapsed, bounce_ms, primary_ms, per))
+    print(json.dumps(line), flush=True)
+    return 0
+
+
+def single_gpu_extras(args, spheres, bvh, cam, value, elapsed, bounce_ms, primary_ms, per):
+    """N = 1: the work counters, the serial launch, the roofline, the blocking
+    call and the CPU baseline."""
+    r = mirt.Renderer(0)
+    r.upload(spheres, bvh)
+    samples = SPP * per
+    counts = r.count_frame(cam, W, H, depth=DEPTH, seed=SEED, row_block=ROW_BLOCK, samples=samples, jitter=JITTER)
     r.set_option(mirt.abi.OPT_PRUNE, 0)
-    ref_counts = r.count_frame(cam, W, H, depth=DEPTH, seed=SEED, row_block=ROW_BLOCK, shard=rank,
-                               num_shards=world, samples=SPP * per_launch, jitter=JITTER)
+    ref_counts = r.count_frame(cam, W, H, depth=DEPTH, seed=SEED, row_block=ROW_BLOCK, samples=samples,
+                               jitter=JITTER)
     r.set_option(mirt.abi.OPT_PRUNE, 1)
-
-    # a non-default stream for the serial measurement loop below (the timed
-    # loop runs on the ShardedFrame's own streams when pipelined)
+    # the same launch alone, serial, full persistent grid: torch events
+    # around the launch and the library's HIP events around its passes
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
-
-    def plan(f0, steps, per):
-        """(first frame, frames) of the launches covering `steps` steps from frame f0"""
-        out, f, end = [], f0, f0 + steps * fps
-        while f < end:
-            n = min(per, end - f)
-            out.append((f, n))
-            f += n
-        return out
-
-    def launcher(s, depth, tail=()):
-        """The launch of frames f0 .. f0 + n - 1 on the next context; a launch
-        whose first frame is in `tail` (the burst's last launches) runs its
-        bounce pass on the full persistent grid instead of `blocks`."""
-        def run(f0, n):
-            acc = args.accumulate and f0 > 0
-            x = s.rs[s.k % len(s.rs)] if f0 in tail else None
-            if x is not None:
-                keep = x.get_option(mirt.abi.OPT_BOUNCE_BLOCKS)
-                x.set_option(mirt.abi.OPT_BOUNCE_BLOCKS, 0)
-            s.render_local(cam, s.desc(depth=depth, seed=SEED, sample=f0 * SPP, accumulate=acc,
-                                       frames=f0 * SPP + 1 if acc else 1, jitter=JITTER, samples=n * SPP))
-            if x is not None:
-                x.set_option(mirt.abi.OPT_BOUNCE_BLOCKS, keep)
-            if world > 1:
-                s.gather(every=SPP)       # every frame's display; N = 1: the slabs are the frames
-        return run
-
-    def tail_of(pl):
-        """first frames of the last --tail-grid launches of a pipelined plan"""
-        if len(rs) < 2 or not blocks or args.tail_grid <= 0:
-            return ()
-        return {f0 for f0, _ in pl[-args.tail_grid:]}
-
-    warm = plan(0, args.warmup, per_launch)
-    timed_plan = plan(args.warmup * fps, args.steps, per_launch)
-    run = launcher(sf, DEPTH, tail_of(timed_plan))
-    for p in warm:
-        run(*p)
-    elapsed = timed(world, timed_plan, run)
-
-    # the two passes of every timed launch, from the HIP events the library
-    # records on each launch's own stream around its primary and bounce
-    # kernels (mirt_phase_log): their durations UNDER the overlap of the timed
-    # loop (launch j on ctx j % P, the warm-up launches first)
-    P = len(rs)
-    timed_phases = []
-    for i, x in enumerate(rs):
-        n_i = sum(1 for j in range(len(warm), len(warm) + len(timed_plan)) if j % P == i)
-        if n_i:
-            timed_phases += x.phase_log(min(n_i, 64))
-    primary_ms, bounce_ms = (float(v) for v in np.mean(np.array(timed_phases), axis=0))
-
-    # SURVEY §8(d): depth 1 alongside (camera rays and their shading only)
-    plan_d1 = plan(0, args.steps, per_launch)
-    run1 = launcher(sf, 1, tail_of(plan_d1))
-    for p in plan(0, 2, per_launch):
-        run1(*p)
-    elapsed_d1 = timed(world, plan_d1, run1)
-
-    # the other scaling mode at N > 1 (same contexts, its own slabs)
-    elapsed_other, fps_other = None, None
-    if world > 1:
-        fps_other = 1 if args.scaling == "weak" else world
-        fps_main, fps = fps, fps_other
-        per_other = fps_other * batch if SPP == 1 or args.accumulate else 1
-        sf2 = shard.ShardedFrame(r, W, H, ROW_BLOCK, samples=SPP * per_other, renderers=rs,
-                                 share_accum=args.accumulate, accum=SPP > 1 or args.accumulate)
-        plan2 = plan(args.warmup * fps_other, args.steps, per_other)
-        run2 = launcher(sf2, DEPTH, tail_of(plan2))
-        for p in plan(0, args.warmup, per_other):
-            run2(*p)
-        elapsed_other = timed(world, plan2, run2)
-        fps = fps_main
-
-    # the same launch alone, one context, serial (untimed loop: each launch
-    # waits for its events): torch events around the launch and the HIP
-    # events the library records around the primary and bounce passes
-    fd = sf.desc(depth=DEPTH, seed=SEED, jitter=JITTER)          # one full launch
-    slabs = torch.zeros((SPP * per_launch, sf.rows, W), dtype=torch.int32, device="cuda")
-    acc = torch.zeros((sf.rows, W, 3), dtype=torch.float32, device="cuda") if SPP > 1 or args.accumulate else None
+    fd = mirt.frame_desc(W, H, depth=DEPTH, seed=SEED, row_block=ROW_BLOCK, samples=samples, jitter=JITTER)
+    slabs = torch.zeros((samples, H, W), dtype=torch.int32, device="cuda")
+    acc = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda") if SPP > 1 else None
     phases, launch = [], []
-    r.set_option(mirt.abi.OPT_BOUNCE_BLOCKS, 0)   # one launch alone: the full persistent grid
     for _ in range(min(args.steps, 20)):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
@@ -752,206 +718,141 @@ def main():
         launch.append(e0.elapsed_time(e1))
     serial_primary_ms, serial_bounce_ms = (float(v) for v in np.mean(np.array(phases), axis=0))
     kernel_ms = float(np.mean(launch))
-    r.set_option(mirt.abi.OPT_BOUNCE_BLOCKS, blocks)
-
-    t = torch.tensor([elapsed, kernel_ms, elapsed_d1, elapsed_other or 0.0], dtype=torch.float64, device="cuda")
-    # the whole job's reference-DFS bytes per launch (every
-    # rank's shard), for B / t / (G x 8 TB/s)
-    job_b = torch.tensor([algorithmic_bytes(ref_counts, my_rows * W * SPP * per_launch)], dtype=torch.float64,
-                         device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(job_b, op=dist.ReduceOp.SUM)
-    elapsed, kernel_ms_max, elapsed_d1, elapsed_other = (float(v) for v in t)
-    job_bytes_per_launch = float(job_b[0])
-
-    host = None
-    if rank == 0 and world == 1 and not args.no_host:
-        for x in rs:
-            x.share_accum(None)          # a private buffer per ctx again (--accumulate shared one)
-        host = host_inclusive(rs, cam, args.steps)
-
-    if rank == 0:
-        value = W * H * SPP * fps * args.steps / elapsed / 1e6   # primary rays: W*H per sample
-        pixels = my_rows * W * SPP * per_launch
-        ref_frame_bytes = algorithmic_bytes(ref_counts, pixels)
-        exec_frame_bytes = algorithmic_bytes(counts, pixels)
-        ref_b = bounce_bytes(ref_counts)
-        exec_b = bounce_bytes(counts)
-        achieved = ref_b / (bounce_ms / 1e3) / 1e9
-        pmc, pmc_path = load_pmc_bound(args.workload) if world == 1 else (None, None)
-        pb = pmc["kernels"].get("timed/bounce", {}).get("derived", {}) if pmc else {}
-        pp = pmc["kernels"].get("timed/primary", {}).get("derived", {}) if pmc else {}
-        traffic = pb.get("hbm_bytes")
-        bm = bound_line(pb, exec_b, ref_b, pb.get("kernel_ms_at_2400MHz") or bounce_ms)
-        kname = KERNEL.replace("<true, 2,", "<true, 4,") if r.get_option(mirt.abi.OPT_LEAF_BATCH) else KERNEL
-        roof = vmem_roofline(pmc, pmc_path, elapsed / args.steps * 1e3, per_launch)
-        if roof is None:
-            # no counter file for this workload: the roofline is not measured here (never priced against
-            # the HBM peak with the reference's bytes: VERDICT r3)
-            roof = {"bound": "vmem", "achieved": None, "peak": None, "unit": "Ginst/s", "frac": None,
-                    "traffic": traffic, "note": "no profiles/r0N_pmc_bound_<workload>.json or td_probe table for "
-                                                "this workload"}
-        roof["kernel"] = kname
-        if bm:
-            bm["source"] = (os.path.relpath(pmc_path, ROOT) + " (medians over the dispatches of the timed launch "
-                            "shape, one rocprofv3 --pmc pass of this command per counter set; rocprofv3 serialises "
-                            "the dispatches it counts)")
-        line = {
-            "metric": METRIC,
-            "value": round(value, 3),
-            "unit": "Mrays/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": args.scaling,
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic (create_random_sphere scene, srand(1); default camera main.c:203-211)"
-                    + ("; REHEARSAL: all ranks on one GPU over gloo, not a measurement" if rehearse else ""),
-            "config": {"workload": wl["desc"], "name": args.workload,
-                       "width": W, "height": H, "spheres": NSPH, "scene": KIND, "max_depth": DEPTH, "spp": SPP,
-                       "jitter": JITTER,
-                       "frames_per_step": fps, "frames_per_launch": per_launch, "launches": len(timed_plan),
-                       "pipeline": len(rs), "bounce_blocks": blocks, "tail_grid": len(tail_of(timed_plan)), "bvh_nodes": len(bvh),
-                       "row_block": ROW_BLOCK, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
-                       "step": (f"{fps} frame(s) of the still-camera display loop (main.c:379-408), ctxs sharing "
-                                "one accumulation buffer (mirt_ctx_share_accum)" if args.accumulate else
-                                f"{fps} fresh frame(s) (main.c:358-374)")
-                               + f", {SPP} sample(s) each, {per_launch} frame(s) per launch with every frame's "
-                                 "display in its own slab, launches rotating over `pipeline` ctxs",
-                       "parallelism": f"row-block shard x{world}" + (" + RCCL gather of every frame" if world > 1
-                                                                     else "")},
-            "roofline": roof,
-            # SURVEY 8(d)'s figure, kept beside the roofline under its own name: the REFERENCE's work per
-            # second, not a use of any unit (it exceeds HBM peak because the walk skips most
-            # of it and the tree is cache-resident)
-            "reference_work": {
-                "definition": "SURVEY 8(d): bytes of the REFERENCE's exhaustive DFS (hit.c:91-109, no pruning) at "
-                              "32 B/node test + 16 B/sphere test + 4 B/hit colour + 4 B/pixel, per second. The "
-                              "walk executes a fraction of them (executed_vs_reference) from an L2/MALL-resident "
-                              "tree, so this is the reference's work replaced per second, not HBM use.",
-                "bounce_bytes_per_launch": int(ref_b),
-                "bounce_launch_ms_under_overlap": round(bounce_ms, 4),
-                "bounce_launch_ms_source": f"mean over the {len(timed_phases)} timed launches of HIP events on each "
-                                           "launch's own stream around its bounce kernel (mirt_phase_log): "
-                                           "durations UNDER the overlap of `pipeline` launches, so longer than "
-                                           "the kernel's share of a step",
-                "reference_work_gbs": round(achieved, 1),
-                "reference_work_vs_hbm_peak": round(achieved / PEAK_HBM_GBS, 4),
-                "executed_vs_reference_bytes": round(exec_b / max(ref_b, 1), 4),
-                "hbm_measured": None if traffic is None else {
-                    "bytes_per_launch": traffic,
-                    "gbs_over_exclusive_time": round(traffic / (pb["kernel_ms_at_2400MHz"] / 1e3) / 1e9, 2),
-                    "frac": round(traffic / (pb["kernel_ms_at_2400MHz"] / 1e3) / 1e9 / PEAK_HBM_GBS, 5)},
-                "bound_measured": bm,
-                "primary_launch_ms_under_overlap": round(primary_ms, 4),
-                "primary_bytes_per_launch": int(ref_frame_bytes - ref_b),
-                "primary_bound_measured": bound_line(pp, exec_frame_bytes - exec_b, ref_frame_bytes - ref_b,
-                                                     pp.get("kernel_ms_at_2400MHz") or primary_ms),
-                "launch_bytes": int(ref_frame_bytes),
-                "launch_executed_bytes": int(exec_frame_bytes),
-                "frame_period_ms": round(elapsed / args.steps * 1e3, 4),
-                "frame_reference_gbs": round(ref_frame_bytes / batch / (elapsed / args.steps) / 1e9, 1),
-                "job": {"note": "SURVEY 8(e): every rank's reference-DFS bytes over the timed launches / the "
-                                "max-over-ranks timed region",
-                        "bytes_per_launch": int(job_bytes_per_launch),
-                        "gbs": round(job_bytes_per_launch * len(timed_plan) / elapsed / 1e9, 1)},
-                "serial_launch": {
-                    "note": "the same launch alone (untimed serial loop, the full persistent bounce grid): not "
-                            "the timed configuration",
-                    "frame_ms": round(kernel_ms, 4), "primary_ms": round(serial_primary_ms, 4),
-                    "bounce_ms": round(serial_bounce_ms, 4),
-                    "bounce_reference_gbs": round(ref_b / (serial_bounce_ms / 1e3) / 1e9, 1)}},
-            "work": {k: int(v) for k, v in counts.items()},
-            "work_reference_dfs": {k: int(v) for k, v in ref_counts.items() if k != "lane_steps"},
-            "traced_rays_per_s_M": round(counts["rays"] * world / (elapsed / args.steps) / 1e6, 3),
-            "depth1_mrays_s": round(W * H * SPP * fps * args.steps / elapsed_d1 / 1e6, 3),
-            "bvh_build_s": round(build_s, 4),
-        }
-        if args.opt:
-            line["options"] = args.opt
-        if elapsed_other:
-            other = W * H * SPP * fps_other * args.steps / elapsed_other / 1e6
-            line["value_weak"] = round(value if args.scaling == "weak" else other, 3)
-            line["value_strong"] = round(other if args.scaling == "weak" else value, 3)
-        if host is not None:
-            line.update(host)
-        if world == 1 and not args.no_cpu:
-            cb = cpu_baseline()
-            line["cpu_baseline"] = cb
-            line["speedup_vs_cpu"] = round(value / cb["value"], 1)
-            line["speedup_vs_cpu_single_core"] = round(value / cb["single_core_value"], 1)
-            line["speedup_vs_cpu_all_core_estimate"] = round(value / cb["all_core_estimate"]["value"], 1)
-            if host is not None:
-                line["host_inclusive_speedup_vs_cpu"] = round(host["host_inclusive_mrays_s"] / cb["value"], 1)
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
-    for x in rs:
-        x.close()
-    return 0
-
-
-def host_inclusive(rs, cam, steps):
-    """SURVEY §8(d) t_frame: frames delivered to host memory. Pipelined: ctx
-    k % n renders frame k and copies it into its page-locked buffer
-    (mirt_render_frame_async), waiting first for its frame k - n; blocking:
-    one mirt_render_frame at a time (blocking_leg), in a child process and in
-    this one."""
-    fdh = mirt.frame_desc(W, H, depth=DEPTH, seed=SEED, samples=SPP, jitter=JITTER)
-    bufs = [mirt.HostBuffer((H, W, 4)) for _ in rs]
-    n = len(rs)
-
-    def run(k0, count):
-        for k in range(k0, k0 + count):
-            i = k % n
-            rs[i].wait()
-            rs[i].render_frame_async(cam, fdh, bufs[i])
-        for x in rs:
-            x.wait()
-
-    run(0, 2 * n)
-    steps_h = max(steps, 50)
-    t0 = time.perf_counter()
-    run(0, steps_h)
-    el = time.perf_counter() - t0
-    last = bufs[(steps_h - 1) % n].array.copy()
-    for b in bufs:
-        b.close()
-    # the blocking call in THIS process too, after the four-context burst
-    # (same measurement as the child's; reported beside it)
-    rs[0].set_option(mirt.abi.OPT_BOUNCE_BLOCKS, 0)
-    here = blocking_leg(rs[0], cam)
-    child = blocking_in_child()
-    out = {"host_inclusive_mrays_s": round(W * H * SPP * steps_h / el / 1e6, 3),
-           "host_inclusive_ms_per_frame": round(el / steps_h * 1e3, 4),
-           "host_inclusive_frames": steps_h,
-           "host_inclusive_method": f"{n} ctxs, kernels + async D2H into page-locked buffers "
-                                    "(mirt_render_frame_async), frame k waits for frame k - n",
-           "host_frame_equals_blocking_call": frame_sha(last) == here["sha"] and here["equal"]}
-    src = child if child else here
-    out.update({"host_blocking_mrays_s": src["pinned_mrays_s"], "host_blocking_ms": src["pinned_ms"],
-                "host_blocking_registered_mrays_s": src["registered_mrays_s"],
-                "host_blocking_pageable_mrays_s": src["pageable_mrays_s"],
-                "host_blocking_method": (
-                    "one blocking mirt_render_frame per frame (main.c:350-421's loop) into a frame buffer from "
-                    "mirt_host_alloc: the kernels write the pixels straight into it (MIRT_OPT_ZERO_COPY), median "
-                    "of 11; " + ("measured in a child process holding one ctx and its frame buffer, as main.c's "
-                                 "loop runs (bench.py --blocking-child)" if child else
-                                 "measured in this process (the child process failed)")),
-                "host_blocking_after_burst": {k: here[k] for k in ("pinned_mrays_s", "registered_mrays_s",
-                                                                    "pageable_mrays_s")}})
-    if child:
-        out["host_frame_equals_blocking_call"] = out["host_frame_equals_blocking_call"] and \
-            child["sha"] == here["sha"] and child["equal"]
-        out["host_blocking_after_burst"]["note"] = (
-            "the same calls in the bench's own process after its four-context burst: zero-copy stores run slower "
-            "there for the rest of the process (profiles/r04x: a child started at that point measures as a "
-            "fresh process does)")
+    pixels = H * W * samples
+    ref_frame_bytes = algorithmic_bytes(ref_counts, pixels)
+    exec_frame_bytes = algorithmic_bytes(counts, pixels)
+    ref_b = bounce_bytes(ref_counts)
+    exec_b = bounce_bytes(counts)
+    achieved = ref_b / (max(bounce_ms, 1e-6) / 1e3) / 1e9
+    pmc, pmc_path = load_pmc_bound(WORKLOAD)
+    pb = pmc["kernels"].get("timed/bounce", {}).get("derived", {}) if pmc else {}
+    pp = pmc["kernels"].get("timed/primary", {}).get("derived", {}) if pmc else {}
+    traffic = pb.get("hbm_bytes")
+    bm = bound_line(pb, exec_b, ref_b, pb.get("kernel_ms_at_2400MHz") or bounce_ms)
+    kname = KERNEL.replace("<true, 2,", "<true, 4,") if r.get_option(mirt.abi.OPT_LEAF_BATCH) else KERNEL
+    roof = vmem_roofline(pmc, pmc_path, elapsed / args.steps * 1e3, per)
+    if roof is None:
+        roof = {"bound": "vmem", "achieved": None, "peak": None, "unit": "Ginst/s", "frac": None,
+                "traffic": traffic, "note": "no profiles/r0N_pmc_bound_<workload>.json or td_probe table for "
+                                            "this workload"}
+    roof["kernel"] = kname
+    if bm:
+        bm["source"] = (os.path.relpath(pmc_path, ROOT) + " (medians over the dispatches of the timed launch shape, "
+                        "one rocprofv3 --pmc pass of this command per counter set; rocprofv3 serialises the "
+                        "dispatches it counts)")
+    r.close()
+    out = {
+        "roofline": roof,
+        # SURVEY 8(d)'s figure, kept beside the roofline under its own name: the REFERENCE's work per second,
+        # not a use of any unit (it exceeds HBM peak because the walk skips most of it from cache)
+        "reference_work": {
+            "definition": "SURVEY 8(d): bytes of the REFERENCE's exhaustive DFS (hit.c:91-109, no pruning) at "
+                          "32 B/node test + 16 B/sphere test + 4 B/hit colour + 4 B/pixel, per second. The walk "
+                          "executes a fraction of them (executed_vs_reference) from an L2/MALL-resident tree, so "
+                          "this is the reference's work replaced per second, not HBM use.",
+            "bounce_bytes_per_launch": int(ref_b),
+            "bounce_launch_ms_under_overlap": round(bounce_ms, 4),
+            "reference_work_gbs": round(achieved, 1),
+            "reference_work_vs_hbm_peak": round(achieved / PEAK_HBM_GBS, 4),
+            "executed_vs_reference_bytes": round(exec_b / max(ref_b, 1), 4),
+            "hbm_measured": None if traffic is None else {
+                "bytes_per_launch": traffic,
+                "gbs_over_exclusive_time": round(traffic / (pb["kernel_ms_at_2400MHz"] / 1e3) / 1e9, 2),
+                "frac": round(traffic / (pb["kernel_ms_at_2400MHz"] / 1e3) / 1e9 / PEAK_HBM_GBS, 5)},
+            "bound_measured": bm,
+            "primary_launch_ms_under_overlap": round(primary_ms, 4),
+            "primary_bytes_per_launch": int(ref_frame_bytes - ref_b),
+            "primary_bound_measured": bound_line(pp, exec_frame_bytes - exec_b, ref_frame_bytes - ref_b,
+                                                 pp.get("kernel_ms_at_2400MHz") or primary_ms),
+            "launch_bytes": int(ref_frame_bytes),
+            "launch_executed_bytes": int(exec_frame_bytes),
+            "frame_period_ms": round(elapsed / args.steps * 1e3, 4),
+            "frame_reference_gbs": round(ref_frame_bytes / per / (elapsed / args.steps) / 1e9, 1),
+            "serial_launch": {
+                "note": "the same launch alone (untimed serial loop, the full persistent bounce grid): not the "
+                        "timed configuration",
+                "frame_ms": round(kernel_ms, 4), "primary_ms": round(serial_primary_ms, 4),
+                "bounce_ms": round(serial_bounce_ms, 4),
+                "bounce_reference_gbs": round(ref_b / (serial_bounce_ms / 1e3) / 1e9, 1)}},
+        "work": {k: int(v) for k, v in counts.items()},
+        "work_reference_dfs": {k: int(v) for k, v in ref_counts.items() if k != "lane_steps"},
+        "traced_rays_per_s_M": round(counts["rays"] / per / (elapsed / args.steps) / 1e6, 3),
+    }
+    if not args.no_host:
+        child = blocking_in_child()
+        if child:
+            out.update({"host_blocking_mrays_s": child["pinned_mrays_s"], "host_blocking_ms": child["pinned_ms"],
+                        "host_blocking_registered_mrays_s": child["registered_mrays_s"],
+                        "host_blocking_pageable_mrays_s": child["pageable_mrays_s"],
+                        "host_blocking_equals_frames": child["equal"],
+                        "host_blocking_sha": child["sha"],
+                        "host_blocking_method": (
+                            "one blocking mirt_render_frame per frame (main.c:350-421's loop) into a frame buffer "
+                            "from mirt_host_alloc: the kernels write the pixels straight into it "
+                            "(MIRT_OPT_ZERO_COPY), median of 11, in a child process holding one ctx and its frame "
+                            "buffer, as main.c's loop runs (bench.py --blocking-child); pageable = the caller's "
+                            "plain malloc'd buffer, the same process")})
+    if not args.no_cpu:
+        cb = cpu_baseline()
+        out["cpu_baseline"] = cb
+        out["speedup_vs_cpu"] = round(value / cb["value"], 1)
+        out["speedup_vs_cpu_single_core"] = round(value / cb["single_core_value"], 1)
+        out["speedup_vs_cpu_all_core_estimate"] = round(value / cb["all_core_estimate"]["value"], 1)
     return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-host", action="store_true", help="skip the blocking-call leg (child process)")
+    ap.add_argument("--no-other", action="store_true", help="N > 1: skip the other delivery's leg")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="1080p_10k")
+    ap.add_argument("--delivery", choices=("gather", "host-direct"), default="gather",
+                    help="gather: RCCL gather of the slabs to GPU 0, de-interleave, one D2H per frame (SURVEY "
+                         "8(e)); host-direct: every GPU copies its row blocks straight into the host frame")
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="lanes of contexts keeping launches in flight (0 = 4 at N = 1, 8 at N > 1)")
+    ap.add_argument("--bounce-blocks", type=int, default=-1,
+                    help="persistent bounce workgroups per launch (MIRT_OPT_BOUNCE_BLOCKS); -1 = the workload's "
+                         "BB_PER_CU (1.5 unless stated) per CU with lanes > 1, else 0 (occupancy x CUs)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="frames per launch (0 = DEFAULT_BATCH[N])")
+    ap.add_argument("--tail-grid", type=int, default=-1,
+                    help="the last N launches of the timed burst take the full persistent bounce grid; -1 = "
+                         "TAIL_GRID at N = 1, TAIL_GRID_MULTI at N > 1")
+    ap.add_argument("--accumulate", action="store_true",
+                    help="time the still-camera accumulating display loop instead of fresh frames")
+    ap.add_argument("--dry", action="store_true", help="CPU plumbing check (no GPU, no measurement)")
+    ap.add_argument("--rank-timeout", type=float, default=420.0,
+                    help="N > 1: seconds before a still-running measuring process is terminated (exit 124)")
+    ap.add_argument("--hw-queues", type=int, default=-1,
+                    help="GPU_MAX_HW_QUEUES for the measuring process (-1: the environment's at N = 1, 16 at "
+                         "N > 1; 0: keep the environment's)")
+    ap.add_argument("--measure-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--blocking-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--opt", action="append", default=[],
+                    help="OPTION=VALUE (mirt_multi_set_option on every context), repeatable")
+    args = ap.parse_args()
+    global W, H, NSPH, KIND, SPP, JITTER, WORKLOAD
+    WORKLOAD = args.workload
+    wl = WORKLOADS[args.workload]
+    W, H, NSPH, KIND, SPP, JITTER = wl["W"], wl["H"], wl["NSPH"], wl["KIND"], wl["SPP"], wl["JITTER"]
+
+    if args.blocking_child:
+        return blocking_child()
+    if args.measure_child:
+        return dry_main(args) if args.dry else measure(args)
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world_env > 1 and world_env != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} under WORLD_SIZE {world_env}: measuring {args.gpus} GPU(s) from rank 0",
+              file=sys.stderr)
+    if args.gpus > 1 or args.dry or world_env > 1:
+        return launcher_main(args, world_env, rank)
+    return measure(args)
 
 
 def frame_sha(a):

@@ -180,18 +180,24 @@ SIGNATURES = [
     ("mirt_multi_size", I, [P]),
     ("mirt_multi_lanes", I, [P]),
     ("mirt_multi_backend", C.c_char_p, [P]),
+    ("mirt_multi_delivery", C.c_char_p, [P]),
+    ("mirt_multi_failed", I, [P]),
     ("mirt_multi_ctx", P, [P, I, I]),
     ("mirt_multi_set_option", I, [P, I, I]),
+    ("mirt_multi_get_option", I, [P, I]),
     ("mirt_multi_scene_upload", I, [P, P, I, P]),
     ("mirt_multi_scene_upload_flat", I, [P, P, I, P, I]),
     ("mirt_multi_render_frame", I, [P, P, P, P]),
     ("mirt_multi_render_frame_async", I, [P, P, P, P]),
+    ("mirt_multi_render_frames_async", I, [P, P, P, I, I, C.POINTER(P)]),
     ("mirt_multi_wait", I, [P]),
 ]
 
 OPT_TRAVERSAL, OPT_FAST_SLAB, OPT_BLOCK_WAVES, OPT_DEFER, OPT_BOUNCE_THRESHOLD, OPT_PRUNE, OPT_ORDERED = (
     1, 2, 3, 4, 5, 6, 7)
 OPT_BOUNCE_BLOCKS, OPT_QUAD_DRAIN, OPT_LEAF_BATCH, OPT_QUAD_BATCH, OPT_ZERO_COPY = 9, 11, 14, 15, 17
-OPT_QUEUE_ORDER = 18
+OPT_QUEUE_ORDER, OPT_DEBUG_STALL_MS = 18, 19
 TRAV_TILE, TRAV_WAVEFRONT = 0, 5
-MULTI_COPY = 1
+MULTI_COPY, MULTI_HOST_DIRECT = 1, 2
+MULTI_FULL_GRID = 1
+MULTI_OPT_TIMEOUT_MS, MULTI_OPT_EMULATE_WORLD, MULTI_OPT_EMULATE_RANK = 256, 257, 258

@@ -26,8 +26,12 @@ int validate_flat(const mirt_node* nd, int nn, int num_spheres, int sphere_lo, c
 // the ctx's own stream into d_out (fd->samples slabs of the shard; the ctx's
 // own buffer when null) with the ctx's (possibly shared) accumulation buffer;
 // *d_display = the slab holding the display after the last frame.
+// independent (fd->samples > 1, !fd->accumulate): the samples are successive
+// FRESH frames (main.c:358-374 each), left raw in their slabs, the last one
+// folded into the accumulation buffer as a fresh frame; otherwise they fold in
+// order (a frame of several samples / the accumulating display loop).
 int enqueue_frame_device(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, uint32_t* d_out,
-                         uint32_t** d_display, const char* fn);
+                         uint32_t** d_display, const char* fn, bool independent = false);
 int ctx_device(const mirt_ctx* c);
 
 }  // namespace mirt

@@ -1,16 +1,27 @@
 // include/mirt_multi.h: one frame loop over the GPUs of a node from one host
 // thread (SURVEY.md §8(b) mirt_init(num_gpus), §8(e) row-tile shard + RCCL
 // gather). The reference's pixel loop (main.c:356-374 / 379-408) becomes, per
-// frame: every rank renders its interleaved row blocks with the single-GPU
-// kernels into a compact slab (render.hip, mirt::enqueue_frame_device), the
-// slabs go to rank 0 -- one RCCL group of ncclSend / ncclRecv over
-// communicators from ncclCommInitAll, or device copies in "copy" mode --
-// deinterleave_kernel writes the row-major frame, and one D2H copy delivers it.
+// launch of `nframes` successive frames: every rank renders its interleaved
+// row blocks of all of them with the single-GPU kernels into compact slabs
+// (render.hip, mirt::enqueue_frame_device), then either
+//   gather (default): the slabs go to rank 0 -- one RCCL group of ncclSend /
+//     ncclRecv over communicators from ncclCommInitAll, or device copies in
+//     "copy" mode -- deinterleave_kernel writes the row-major frames and one
+//     D2H copy per frame delivers them; or
+//   host-direct (MIRT_MULTI_HOST_DIRECT): every rank copies its row blocks
+//     straight into the host frames (one strided DMA per frame over its own
+//     host link), no exchange between GPUs.
+// `lanes` sets of contexts keep launches in flight. Every wait is bounded
+// (MIRT_MULTI_OPT_TIMEOUT_MS): a lane that does not finish fails the object
+// with the stuck rank named and the communicators aborted, never a hang.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <new>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/mirt_multi.h"
@@ -20,21 +31,32 @@ using namespace mirt;
 
 namespace {
 
-// The gathered slabs (rank r's compact rows at gathered + r * slab_elems) ->
-// the row-major frame. Image row y lies in row block b = y / rb, which rank
-// b % n rendered as its compact row (b / n) * rb + y % rb (host_scene.cpp
-// shard_row_count's geometry). One thread per pixel, rows across blockIdx.y:
-// both sides are coalesced row segments.
+constexpr int kMaxShards = 64;  // shards of one frame (ranks, or the emulated world)
+
+// Rows of every shard (kernel argument of deinterleave_kernel).
+struct ShardRows {
+    int rows[kMaxShards];
+};
+
+// The gathered slabs -> the row-major frames. Shard s's `nframes` displays
+// lie at gathered + s * shard_stride, frame j at + j * rows[s] * width. Image
+// row y lies in row block b = y / rb, which shard b % n rendered as its
+// compact row (b / n) * rb + y % rb (host_scene.cpp shard_row_count's
+// geometry). One thread per pixel, rows across blockIdx.y, frames across
+// blockIdx.z: both sides are coalesced row segments.
 __global__ void __launch_bounds__(256) deinterleave_kernel(const uint32_t* __restrict__ gathered,
-                                                           uint32_t* __restrict__ frame, int width, int height,
-                                                           int rb, int n, size_t slab_elems)
+                                                           uint32_t* __restrict__ frames, int width, int height,
+                                                           int rb, int n, size_t shard_stride, ShardRows sr)
 {
     const int x = blockIdx.x * 256 + threadIdx.x;
     const int y = blockIdx.y;
+    const int j = blockIdx.z;
     if (x >= width || y >= height) return;
     const int b = y / rb;
+    const int s = b % n;
     const size_t row = (size_t)(b / n) * rb + y % rb;
-    frame[(size_t)y * width + x] = gathered[(size_t)(b % n) * slab_elems + row * width + x];
+    frames[((size_t)j * height + y) * width + x] =
+        gathered[(size_t)s * shard_stride + ((size_t)j * sr.rows[s] + row) * width + x];
 }
 
 int hip_err(hipError_t e, const char* what)
@@ -73,16 +95,19 @@ int grow(int dev, uint32_t** p, size_t* cap, size_t bytes)
     return MIRT_OK;
 }
 
-// One frame in flight: a context per rank, the gather buffer and the frame
-// on rank 0, and the copy-mode events.
+// One launch in flight: a context per rank, the gather buffer and the frames
+// on rank 0, the copy-mode events and each rank's completion event.
 struct Lane {
     std::vector<mirt_ctx*> ctx;       // rank r's context (device dev[r], its own stream)
-    std::vector<hipEvent_t> rendered; // copy mode: rank r's slab is complete
-    uint32_t* gathered = nullptr;     // rank 0: n slabs of slab_elems
+    std::vector<hipEvent_t> rendered; // copy mode: rank r's slabs are complete
+    std::vector<hipEvent_t> done;     // rank r's stream: the launch's last operation there
+    uint32_t* gathered = nullptr;     // rank 0: every shard's displays
     size_t gathered_cap = 0;
-    uint32_t* frame = nullptr;        // rank 0: the de-interleaved frame
+    uint32_t* frame = nullptr;        // rank 0: the de-interleaved frames
     size_t frame_cap = 0;
-    bool pending = false;             // a frame was enqueued and not yet waited for
+    // a launch was (possibly partly) enqueued and not yet waited for: set
+    // before the first enqueue, cleared only once every rank's work is done
+    bool pending = false;
 };
 
 }  // namespace
@@ -91,97 +116,242 @@ struct mirt_multi {
     int n = 0;
     std::vector<int> dev;
     bool rccl = false;
+    bool direct = false;              // MIRT_MULTI_HOST_DIRECT
     std::vector<ncclComm_t> comm;
     std::vector<Lane> lanes;
     int next = 0;
+    int timeout_ms = 60000;           // MIRT_MULTI_OPT_TIMEOUT_MS (0: unbounded)
+    int emu_world = 0, emu_rank = 0;  // MIRT_MULTI_OPT_EMULATE_*: this one rank plays shard emu_rank of emu_world
+    bool failed = false;              // a wait timed out or a device call failed: every call returns fail_msg
+    std::string fail_msg;
 };
 
 namespace {
 
 hipStream_t stream_of(mirt_ctx* c) { return (hipStream_t)mirt_ctx_stream(c); }
 
-int wait_lane(mirt_multi* m, Lane& L)
+int failed_status(const mirt_multi* m, const char* fn)
 {
+    set_error("%s: %s", fn, m->fail_msg.c_str());
+    return MIRT_E_DEVICE;
+}
+
+// The object cannot go on: abort the communicators (an RCCL kernel stuck on a
+// peer polls the abort flag and exits), remember why, and fail from now on.
+int fail_multi(mirt_multi* m, const std::string& why)
+{
+    m->failed = true;
+    m->fail_msg = why;
+    for (ncclComm_t& c : m->comm)
+        if (c) {
+            (void)ncclCommAbort(c);
+            c = nullptr;
+        }
+    set_error("%s", why.c_str());
+    return MIRT_E_DEVICE;
+}
+
+// Wait for lane `li`'s launch on every rank, polling each rank's completion
+// event against the deadline (no unbounded hipStreamSynchronize).
+int wait_lane(mirt_multi* m, int li)
+{
+    if (m->failed) return failed_status(m, "mirt_multi");
+    Lane& L = m->lanes[li];
     if (!L.pending) return MIRT_OK;
-    L.pending = false;
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     for (int r = 0; r < m->n; r++) {
-        MHIP(hipSetDevice(m->dev[r]));
-        MHIP(hipStreamSynchronize(stream_of(L.ctx[r])));
+        for (long polls = 0;; polls++) {
+            const hipError_t e = hipEventQuery(L.done[r]);
+            if (e == hipSuccess) break;
+            if (e != hipErrorNotReady) {
+                (void)hipGetLastError();
+                return fail_multi(m, std::string("rank ") + std::to_string(r) + " (device " +
+                                         std::to_string(m->dev[r]) + "): " + hipGetErrorString(e));
+            }
+            const double ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+            if (m->timeout_ms > 0 && ms > m->timeout_ms) {
+                std::string stuck;
+                for (int q = r; q < m->n; q++)
+                    if (hipEventQuery(L.done[q]) == hipErrorNotReady)
+                        stuck += (stuck.empty() ? "" : ", ") + std::to_string(q) + " (device " +
+                                 std::to_string(m->dev[q]) + ")";
+                (void)hipGetLastError();
+                return fail_multi(m, "lane " + std::to_string(li) + " not done after " +
+                                         std::to_string(m->timeout_ms) + " ms (MIRT_MULTI_OPT_TIMEOUT_MS); stuck rank(s) " +
+                                         stuck + "; communicators aborted, the object is unusable");
+            }
+            // spin briefly (a frame in flight is usually about to end), then
+            // give the core back between polls
+            if (polls < 2000)
+                std::this_thread::yield();
+            else
+                std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
     }
+    L.pending = false;
     return MIRT_OK;
 }
 
-// Frame k on lane L: every rank's shard, the gather to rank 0, the
-// de-interleave and the D2H copy into `out`, all enqueued.
-int enqueue(mirt_multi* m, Lane& L, const mirt_camera* cam, const mirt_frame_desc* fd, mirt_rgba8* out)
+// After a failed enqueue: whatever part of the launch reached the streams is
+// covered by the completion events, so the lane's next wait sees it.
+void mark_partial(mirt_multi* m, Lane& L)
+{
+    for (int r = 0; r < m->n; r++) {
+        (void)hipSetDevice(m->dev[r]);
+        (void)hipEventRecord(L.done[r], stream_of(L.ctx[r]));
+    }
+    (void)hipGetLastError();
+}
+
+// Launch on lane L: `nframes` frames (RNG samples fd->sample + j) on every
+// rank, then the gather / host delivery into outs[j] (outs null: the frames
+// stay on the devices).
+int enqueue(mirt_multi* m, Lane& L, const mirt_camera* cam, const mirt_frame_desc* fd, int nframes, int flags,
+            mirt_rgba8* const* outs)
 {
     const int n = m->n;
+    const bool emu = m->emu_world > 1;
+    const int world = emu ? m->emu_world : n;   // shards of the frame
+    const int spp = std::max(1, fd->samples);
+    const int W = fd->width, H = fd->height;
     mirt_frame_desc sd = *fd;
     sd.row_block = fd->row_block > 0 ? fd->row_block : 8;
-    sd.num_shards = n;
-    // the widest shard (rank 0's: it holds the first block) sets the slab stride
-    sd.shard = 0;
-    const size_t slab_elems = (size_t)shard_row_count(&sd) * fd->width;
+    sd.num_shards = world;
+    sd.samples = spp * nframes;
+    const int rb = sd.row_block;
+    ShardRows sr{};
+    for (int s = 0; s < world; s++) {
+        sd.shard = s;
+        sr.rows[s] = shard_row_count(&sd);
+    }
+    const size_t slab_elems = (size_t)sr.rows[0] * W;          // shard 0 holds the most rows
+    const size_t shard_stride = slab_elems * nframes;           // gathered: shard s's displays
+    const size_t frame_elems = (size_t)W * H;
     const int dev0 = m->dev[0];
-    int rc = grow(dev0, &L.gathered, &L.gathered_cap, 4 * slab_elems * n + 4);
-    if (!rc && n > 1) rc = grow(dev0, &L.frame, &L.frame_cap, 4 * (size_t)fd->width * fd->height + 4);
-    if (rc) return rc;
-    // rank r renders its row blocks: its `samples` slabs in the ctx's own
-    // buffer (the display is the last), with its (lane-shared) accumulation
-    std::vector<uint32_t*> disp(n, nullptr);
-    std::vector<size_t> elems(n, 0);
-    for (int r = 0; r < n; r++) {
-        sd.shard = r;
-        elems[r] = (size_t)shard_row_count(&sd) * fd->width;
-        rc = enqueue_frame_device(L.ctx[r], cam, &sd, nullptr, &disp[r], "mirt_multi_render_frame");
+    const bool gather = !m->direct || !outs;                    // frames to device 0
+    const bool rank0_assembles = gather && (!emu || m->emu_rank == 0);
+    if (gather) {
+        int rc = grow(dev0, &L.gathered, &L.gathered_cap, 4 * shard_stride * world + 4);
+        if (!rc && world > 1 && rank0_assembles) rc = grow(dev0, &L.frame, &L.frame_cap, 4 * frame_elems * nframes + 4);
         if (rc) return rc;
     }
-    hipStream_t s0 = stream_of(L.ctx[0]);
-    if (m->rccl) {
-        // one group: every rank (rank 0 included, a self send/recv, so every
-        // slab takes one path) sends its display slab to rank 0, which
-        // receives slab r at gathered + r * slab_elems; each op on the stream
-        // that rendered it, so it starts when that rank's frame is done
-        MNCCL(ncclGroupStart());
-        for (int r = 0; r < n; r++) {
-            ncclResult_t e = ncclSend(disp[r], elems[r], ncclUint32, 0, m->comm[r], stream_of(L.ctx[r]));
-            if (e == ncclSuccess)
-                e = ncclRecv(L.gathered + (size_t)r * slab_elems, elems[r], ncclUint32, r, m->comm[0], s0);
-            if (e != ncclSuccess) {
-                (void)ncclGroupEnd();
-                return nccl_err(e, "mirt_multi_render_frame: ncclSend/ncclRecv");
-            }
-        }
-        MNCCL(ncclGroupEnd());
-    } else {
-        // copy mode: rank 0's stream waits for each rank's frame, then copies
-        // its slab (peer-to-peer across devices, device-local otherwise)
-        for (int r = 0; r < n; r++) {
-            if (r > 0) {
-                MHIP(hipSetDevice(m->dev[r]));
-                MHIP(hipEventRecord(L.rendered[r], stream_of(L.ctx[r])));
-                MHIP(hipSetDevice(dev0));
-                MHIP(hipStreamWaitEvent(s0, L.rendered[r], 0));
-            }
-            MHIP(hipSetDevice(dev0));
-            uint32_t* dst = L.gathered + (size_t)r * slab_elems;
-            if (m->dev[r] == dev0)
-                MHIP(hipMemcpyAsync(dst, disp[r], 4 * elems[r], hipMemcpyDeviceToDevice, s0));
-            else
-                MHIP(hipMemcpyPeerAsync(dst, dev0, disp[r], m->dev[r], 4 * elems[r], s0));
-        }
-    }
-    MHIP(hipSetDevice(dev0));
-    const uint32_t* src = L.gathered;   // n == 1: the one slab is the frame
-    if (n > 1) {
-        const dim3 grid((fd->width + 255) / 256, fd->height);
-        deinterleave_kernel<<<grid, 256, 0, s0>>>(L.gathered, L.frame, fd->width, fd->height, sd.row_block, n,
-                                                  slab_elems);
-        MHIP(hipGetLastError());
-        src = L.frame;
-    }
-    MHIP(hipMemcpyAsync(out, src, 4 * (size_t)fd->width * fd->height, hipMemcpyDeviceToHost, s0));
     L.pending = true;
+    // every rank renders its row blocks of all frames: `samples` slabs in the
+    // ctx's own buffer, frame j's display in slab (j + 1) * spp - 1 (one frame
+    // of several samples: its last slab)
+    std::vector<uint32_t*> src(n, nullptr);
+    std::vector<size_t> cnt(n, 0);
+    std::vector<int> shard(n, 0);
+    for (int r = 0; r < n; r++) {
+        shard[r] = emu ? m->emu_rank : r;
+        sd.shard = shard[r];
+        const size_t elems = (size_t)sr.rows[shard[r]] * W;
+        int keep = 0;
+        if (flags & MIRT_MULTI_FULL_GRID) {
+            keep = mirt_get_option(L.ctx[r], MIRT_OPT_BOUNCE_BLOCKS);
+            (void)mirt_set_option(L.ctx[r], MIRT_OPT_BOUNCE_BLOCKS, 0);
+        }
+        uint32_t* disp = nullptr;
+        int rc = enqueue_frame_device(L.ctx[r], cam, &sd, nullptr, &disp, "mirt_multi_render_frames_async",
+                                      nframes > 1);
+        if (flags & MIRT_MULTI_FULL_GRID) (void)mirt_set_option(L.ctx[r], MIRT_OPT_BOUNCE_BLOCKS, keep);
+        if (rc) return rc;
+        src[r] = disp - (size_t)(nframes - 1) * elems;   // spp == 1 when nframes > 1: slab j = frame j
+        cnt[r] = elems * nframes;
+    }
+    hipStream_t s0 = stream_of(L.ctx[0]);
+    if (gather) {
+        if (m->rccl) {
+            // one group: every rank (rank 0 included, a self send/recv, so
+            // every slab takes one path) sends its displays to rank 0, which
+            // receives shard s at gathered + s * shard_stride; each op on the
+            // stream that rendered it, so it starts when that rank's frames
+            // are done
+            MNCCL(ncclGroupStart());
+            for (int r = 0; r < n; r++) {
+                ncclResult_t e = ncclSend(src[r], cnt[r], ncclUint32, 0, m->comm[r], stream_of(L.ctx[r]));
+                if (e == ncclSuccess)
+                    e = ncclRecv(L.gathered + (size_t)shard[r] * shard_stride, cnt[r], ncclUint32, r, m->comm[0], s0);
+                if (e != ncclSuccess) {
+                    (void)ncclGroupEnd();
+                    return nccl_err(e, "mirt_multi_render_frames_async: ncclSend/ncclRecv");
+                }
+            }
+            MNCCL(ncclGroupEnd());
+        } else {
+            // copy mode: rank 0's stream waits for each rank's frames, then
+            // copies its slabs (peer-to-peer across devices, device-local
+            // otherwise)
+            for (int r = 0; r < n; r++) {
+                if (r > 0) {
+                    MHIP(hipSetDevice(m->dev[r]));
+                    MHIP(hipEventRecord(L.rendered[r], stream_of(L.ctx[r])));
+                    MHIP(hipSetDevice(dev0));
+                    MHIP(hipStreamWaitEvent(s0, L.rendered[r], 0));
+                }
+                MHIP(hipSetDevice(dev0));
+                uint32_t* dst = L.gathered + (size_t)shard[r] * shard_stride;
+                if (m->dev[r] == dev0)
+                    MHIP(hipMemcpyAsync(dst, src[r], 4 * cnt[r], hipMemcpyDeviceToDevice, s0));
+                else
+                    MHIP(hipMemcpyPeerAsync(dst, dev0, src[r], m->dev[r], 4 * cnt[r], s0));
+            }
+        }
+        MHIP(hipSetDevice(dev0));
+        if (emu && m->emu_rank == 0) {
+            // emulated rank 0 of a `world`-rank job: the other shards' slabs
+            // arrive too (HBM writes of the receives; the xGMI wire time is
+            // not modelled), copied from this rank's own
+            for (int s = 1; s < world; s++)
+                MHIP(hipMemcpyAsync(L.gathered + (size_t)s * shard_stride, src[0],
+                                    4 * std::min(cnt[0], (size_t)sr.rows[s] * W * nframes), hipMemcpyDeviceToDevice,
+                                    s0));
+        }
+        if (rank0_assembles) {
+            const uint32_t* frames = L.gathered;   // one shard: its displays are the frames
+            if (world > 1) {
+                const dim3 grid((W + 255) / 256, H, nframes);
+                deinterleave_kernel<<<grid, 256, 0, s0>>>(L.gathered, L.frame, W, H, rb, world, shard_stride, sr);
+                MHIP(hipGetLastError());
+                frames = L.frame;
+            }
+            if (outs)
+                for (int j = 0; j < nframes; j++)
+                    MHIP(hipMemcpyAsync(outs[j], frames + (size_t)j * frame_elems, 4 * frame_elems,
+                                        hipMemcpyDeviceToHost, s0));
+        }
+    } else {
+        // host-direct: rank r's row blocks of frame j straight into outs[j]:
+        // its full blocks b = s, s + world, ... as one strided copy (rows of
+        // rb * W pixels, the destination pitch world * rb rows), the image's
+        // short last block (if it is this shard's) after it
+        const int blocks = (H + rb - 1) / rb;
+        const int last = blocks - 1;
+        const bool short_last = H % rb != 0;
+        for (int r = 0; r < n; r++) {
+            const int s = shard[r];
+            const int nb = s < blocks ? (last - s) / world + 1 : 0;     // this shard's blocks
+            const bool has_short = short_last && nb > 0 && last % world == s;
+            const int nfull = nb - (has_short ? 1 : 0);
+            const size_t elems = (size_t)sr.rows[s] * W;
+            MHIP(hipSetDevice(m->dev[r]));
+            for (int j = 0; j < nframes; j++) {
+                const uint32_t* sj = src[r] + (size_t)j * elems;
+                uint32_t* dj = (uint32_t*)outs[j];
+                if (nfull > 0)
+                    MHIP(hipMemcpy2DAsync(dj + (size_t)s * rb * W, (size_t)world * rb * W * 4, sj, (size_t)rb * W * 4,
+                                          (size_t)rb * W * 4, nfull, hipMemcpyDeviceToHost, stream_of(L.ctx[r])));
+                if (has_short)
+                    MHIP(hipMemcpyAsync(dj + (size_t)last * rb * W, sj + (size_t)nfull * rb * W,
+                                        (size_t)(H - last * rb) * W * 4, hipMemcpyDeviceToHost, stream_of(L.ctx[r])));
+            }
+        }
+    }
+    for (int r = 0; r < n; r++) {
+        MHIP(hipSetDevice(m->dev[r]));
+        MHIP(hipEventRecord(L.done[r], stream_of(L.ctx[r])));
+    }
     return MIRT_OK;
 }
 
@@ -191,17 +361,30 @@ bool multi_ok(mirt_multi* m, const char* fn)
     return m != nullptr;
 }
 
-int check_frame(const mirt_camera* cam, const mirt_frame_desc* fd, mirt_rgba8* out, const char* fn)
+int check_frame(const mirt_multi* m, const mirt_camera* cam, const mirt_frame_desc* fd, int nframes,
+                mirt_rgba8* const* outs, const char* fn)
 {
-    if (!cam || !fd || !out || fd->shard != 0 || fd->num_shards > 1 || fd->num_shards < 0 || fd->row_block < 0) {
+    if (!cam || !fd || fd->shard != 0 || fd->num_shards > 1 || fd->num_shards < 0 || fd->row_block < 0 ||
+        nframes < 1) {
         set_error("%s: invalid arguments (fd describes the whole frame: shard 0, num_shards 0 or 1)", fn);
         return MIRT_E_INVALID;
     }
+    if (nframes > 1 && fd->samples > 1) {
+        set_error("%s: several frames per launch need one sample per frame (fd->samples <= 1)", fn);
+        return MIRT_E_INVALID;
+    }
+    if (outs)
+        for (int j = 0; j < nframes; j++)
+            if (!outs[j]) {
+                set_error("%s: outs[%d] is null", fn, j);
+                return MIRT_E_INVALID;
+            }
     mirt_frame_desc whole = *fd;
-    whole.num_shards = 1;
+    whole.num_shards = m->emu_world > 1 ? m->emu_world : m->n;
     whole.row_block = fd->row_block > 0 ? fd->row_block : 8;
-    if (!frame_desc_valid(&whole)) {
-        set_error("%s: invalid frame descriptor", fn);
+    whole.samples = std::max(1, fd->samples) * nframes;
+    if (!frame_desc_valid(&whole) || whole.num_shards > kMaxShards) {
+        set_error("%s: invalid frame descriptor (or more than 64 frames / samples per launch)", fn);
         return MIRT_E_INVALID;
     }
     return MIRT_OK;
@@ -213,7 +396,7 @@ extern "C" {
 
 int mirt_multi_create(const int* devices, int n, int lanes, int flags, mirt_multi** out)
 try {
-    if (!out || n <= 0 || lanes <= 0 || (flags & ~MIRT_MULTI_COPY)) {
+    if (!out || n <= 0 || n > kMaxShards || lanes <= 0 || (flags & ~(MIRT_MULTI_COPY | MIRT_MULTI_HOST_DIRECT))) {
         set_error("mirt_multi_create: invalid arguments");
         return MIRT_E_INVALID;
     }
@@ -232,6 +415,7 @@ try {
         }
         for (int q = 0; q < r; q++) distinct = distinct && m->dev[q] != m->dev[r];
     }
+    m->direct = (flags & MIRT_MULTI_HOST_DIRECT) != 0;
     m->rccl = distinct && !(flags & MIRT_MULTI_COPY);
     auto fail = [&](int rc) {
         mirt_multi_destroy(m);
@@ -262,12 +446,24 @@ try {
         Lane& L = m->lanes[l];
         L.ctx.assign(n, nullptr);
         L.rendered.assign(n, nullptr);
+        L.done.assign(n, nullptr);
         for (int r = 0; r < n; r++) {
             int rc = mirt_create(m->dev[r], &L.ctx[r]);
             if (rc) return fail(rc);
             (void)hipSetDevice(m->dev[r]);
             hipError_t e = hipEventCreateWithFlags(&L.rendered[r], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&L.done[r], hipEventDisableTiming);
             if (e != hipSuccess) return fail(hip_err(e, "mirt_multi_create: hipEventCreate"));
+            if (lanes > 1) {
+                // launches in flight share the chip: each bounce pass at 1.5
+                // persistent workgroups per CU instead of the full grid
+                // (2,400 -> 2,648 Mrays/s at four in flight)
+                int cus = 0;
+                e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, m->dev[r]);
+                if (e != hipSuccess) return fail(hip_err(e, "mirt_multi_create: hipDeviceGetAttribute"));
+                rc = mirt_set_option(L.ctx[r], MIRT_OPT_BOUNCE_BLOCKS, std::max(1, 3 * cus / 2));
+                if (rc) return fail(rc);
+            }
             // the lanes of a rank keep ONE accumulation buffer: frames in
             // flight of the accumulating loop (main.c:379-408) fold in order
             if (l > 0) {
@@ -286,13 +482,19 @@ try {
 void mirt_multi_destroy(mirt_multi* m)
 {
     if (!m) return;
-    for (Lane& L : m->lanes) (void)wait_lane(m, L);
+    for (int l = 0; l < (int)m->lanes.size() && !m->failed; l++) (void)wait_lane(m, l);
+    if (m->failed) {
+        // work may still be queued on a stuck device: freeing its buffers or
+        // destroying its streams would wait for it, so they are left to the
+        // process's exit (the communicators were aborted when it failed)
+        delete m;
+        return;
+    }
     for (Lane& L : m->lanes) {
         for (int r = 0; r < (int)L.ctx.size(); r++) {
-            if (L.rendered[r]) {
-                (void)hipSetDevice(m->dev[r]);
-                (void)hipEventDestroy(L.rendered[r]);
-            }
+            (void)hipSetDevice(m->dev[r]);
+            if (L.rendered[r]) (void)hipEventDestroy(L.rendered[r]);
+            if (L.done[r]) (void)hipEventDestroy(L.done[r]);
             mirt_destroy(L.ctx[r]);
         }
         (void)hipSetDevice(m->dev[0]);
@@ -307,6 +509,8 @@ void mirt_multi_destroy(mirt_multi* m)
 int mirt_multi_size(const mirt_multi* m) { return m ? m->n : MIRT_E_INVALID; }
 int mirt_multi_lanes(const mirt_multi* m) { return m ? (int)m->lanes.size() : MIRT_E_INVALID; }
 const char* mirt_multi_backend(const mirt_multi* m) { return !m ? "" : m->rccl ? "rccl" : "copy"; }
+const char* mirt_multi_delivery(const mirt_multi* m) { return !m ? "" : m->direct ? "host-direct" : "gather"; }
+int mirt_multi_failed(const mirt_multi* m) { return !m ? MIRT_E_INVALID : m->failed ? 1 : 0; }
 
 mirt_ctx* mirt_multi_ctx(mirt_multi* m, int lane, int rank)
 {
@@ -317,17 +521,50 @@ mirt_ctx* mirt_multi_ctx(mirt_multi* m, int lane, int rank)
 int mirt_multi_set_option(mirt_multi* m, int option, int value)
 {
     if (!multi_ok(m, "mirt_multi_set_option")) return MIRT_E_INVALID;
-    for (Lane& L : m->lanes)
-        for (mirt_ctx* c : L.ctx)
-            if (int rc = mirt_set_option(c, option, value)) return rc;
-    return MIRT_OK;
+    if (m->failed) return failed_status(m, "mirt_multi_set_option");
+    switch (option) {
+    case MIRT_MULTI_OPT_TIMEOUT_MS:
+        if (value < 0) break;
+        m->timeout_ms = value;
+        return MIRT_OK;
+    case MIRT_MULTI_OPT_EMULATE_WORLD:
+        // launches in flight would mix shard geometries: only between frames
+        if (value < 0 || value > kMaxShards || (value > 1 && m->n != 1)) break;
+        for (int l = 0; l < (int)m->lanes.size(); l++)
+            if (int rc = wait_lane(m, l)) return rc;
+        m->emu_world = value;
+        if (m->emu_rank >= std::max(1, value)) m->emu_rank = 0;
+        return MIRT_OK;
+    case MIRT_MULTI_OPT_EMULATE_RANK:
+        if (value < 0 || value >= std::max(1, m->emu_world)) break;
+        for (int l = 0; l < (int)m->lanes.size(); l++)
+            if (int rc = wait_lane(m, l)) return rc;
+        m->emu_rank = value;
+        return MIRT_OK;
+    default:
+        for (Lane& L : m->lanes)
+            for (mirt_ctx* c : L.ctx)
+                if (int rc = mirt_set_option(c, option, value)) return rc;
+        return MIRT_OK;
+    }
+    set_error("mirt_multi_set_option: invalid option %d / value %d", option, value);
+    return MIRT_E_INVALID;
+}
+
+int mirt_multi_get_option(mirt_multi* m, int option)
+{
+    if (!multi_ok(m, "mirt_multi_get_option")) return MIRT_E_INVALID;
+    if (option == MIRT_MULTI_OPT_TIMEOUT_MS) return m->timeout_ms;
+    if (option == MIRT_MULTI_OPT_EMULATE_WORLD) return m->emu_world;
+    if (option == MIRT_MULTI_OPT_EMULATE_RANK) return m->emu_rank;
+    return mirt_get_option(m->lanes[0].ctx[0], option);
 }
 
 int mirt_multi_scene_upload(mirt_multi* m, const mirt_sphere* spheres, int num_spheres, const mirt_bvh_node* root)
 {
     if (!multi_ok(m, "mirt_multi_scene_upload")) return MIRT_E_INVALID;
-    for (Lane& L : m->lanes)
-        if (int rc = wait_lane(m, L)) return rc;
+    for (int l = 0; l < (int)m->lanes.size(); l++)
+        if (int rc = wait_lane(m, l)) return rc;
     for (Lane& L : m->lanes)
         for (mirt_ctx* c : L.ctx)
             if (int rc = mirt_scene_upload(c, spheres, num_spheres, root)) return rc;
@@ -338,41 +575,56 @@ int mirt_multi_scene_upload_flat(mirt_multi* m, const mirt_sphere* spheres, int 
                                  int num_nodes)
 {
     if (!multi_ok(m, "mirt_multi_scene_upload_flat")) return MIRT_E_INVALID;
-    for (Lane& L : m->lanes)
-        if (int rc = wait_lane(m, L)) return rc;
+    for (int l = 0; l < (int)m->lanes.size(); l++)
+        if (int rc = wait_lane(m, l)) return rc;
     for (Lane& L : m->lanes)
         for (mirt_ctx* c : L.ctx)
             if (int rc = mirt_scene_upload_flat(c, spheres, num_spheres, nodes, num_nodes)) return rc;
     return MIRT_OK;
 }
 
+int mirt_multi_render_frames_async(mirt_multi* m, const mirt_camera* cam, const mirt_frame_desc* fd, int nframes,
+                                   int flags, mirt_rgba8* const* outs)
+try {
+    const char* fn = "mirt_multi_render_frames_async";
+    if (!multi_ok(m, fn)) return MIRT_E_INVALID;
+    if (m->failed) return failed_status(m, fn);
+    if (int rc = check_frame(m, cam, fd, nframes, outs, fn)) return rc;
+    const int li = m->next;
+    if (int rc = wait_lane(m, li)) return rc;
+    m->next = (m->next + 1) % (int)m->lanes.size();
+    Lane& L = m->lanes[li];
+    const int rc = enqueue(m, L, cam, fd, nframes, flags, outs);
+    if (rc && L.pending) mark_partial(m, L);
+    return rc;
+} catch (const std::bad_alloc&) {
+    set_error("mirt_multi_render_frames_async: out of host memory");
+    return MIRT_E_NOMEM;
+}
+
 int mirt_multi_render_frame_async(mirt_multi* m, const mirt_camera* cam, const mirt_frame_desc* fd,
                                   mirt_rgba8* out)
 {
-    if (!multi_ok(m, "mirt_multi_render_frame_async")) return MIRT_E_INVALID;
-    if (int rc = check_frame(cam, fd, out, "mirt_multi_render_frame_async")) return rc;
-    Lane& L = m->lanes[m->next];
-    if (int rc = wait_lane(m, L)) return rc;
-    m->next = (m->next + 1) % (int)m->lanes.size();
-    return enqueue(m, L, cam, fd, out);
+    if (!out) {
+        set_error("mirt_multi_render_frame_async: null output");
+        return MIRT_E_INVALID;
+    }
+    return mirt_multi_render_frames_async(m, cam, fd, 1, 0, &out);
 }
 
 int mirt_multi_render_frame(mirt_multi* m, const mirt_camera* cam, const mirt_frame_desc* fd, mirt_rgba8* out)
 {
     if (!multi_ok(m, "mirt_multi_render_frame")) return MIRT_E_INVALID;
-    if (int rc = check_frame(cam, fd, out, "mirt_multi_render_frame")) return rc;
-    Lane& L = m->lanes[m->next];
-    if (int rc = wait_lane(m, L)) return rc;
-    m->next = (m->next + 1) % (int)m->lanes.size();
-    if (int rc = enqueue(m, L, cam, fd, out)) return rc;
-    return wait_lane(m, L);
+    const int li = m->next;
+    if (int rc = mirt_multi_render_frame_async(m, cam, fd, out)) return rc;
+    return wait_lane(m, li);
 }
 
 int mirt_multi_wait(mirt_multi* m)
 {
     if (!multi_ok(m, "mirt_multi_wait")) return MIRT_E_INVALID;
-    for (Lane& L : m->lanes)
-        if (int rc = wait_lane(m, L)) return rc;
+    for (int l = 0; l < (int)m->lanes.size(); l++)
+        if (int rc = wait_lane(m, l)) return rc;
     return MIRT_OK;
 }
 

@@ -217,6 +217,15 @@ __global__ __launch_bounds__(512) void render_kernel(DevScene sc, FrameConst f, 
     }
 }
 
+// MIRT_OPT_DEBUG_STALL_MS (test hook): one wave that waits `ticks` of the
+// 100 MHz real-time clock, then exits -- a frame that cannot finish within a
+// caller's deadline, bounded so the grid always drains.
+__global__ void stall_kernel(uint64_t ticks)
+{
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
 __global__ void mark_deferred_kernel(FrameConst f, uint32_t* __restrict__ list, uint32_t* __restrict__ count)
 {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1336,6 +1345,7 @@ struct mirt_ctx {
     unsigned long long* d_keys = nullptr;  // chunked brute force: per-ray (t, index) keys
     size_t keys_cap = 0;
     int num_cus = 0;
+    int debug_stall_ms = 0;     // MIRT_OPT_DEBUG_STALL_MS: test hook, each frame starts behind a bounded wait
 };
 
 namespace {
@@ -1762,6 +1772,10 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
     const int bw = c->block_waves;
     const int blocks = (tiles + bw - 1) / bw;
     if (blocks == 0) return MIRT_OK;
+    if (c->debug_stall_ms > 0) {
+        stall_kernel<<<1, 64, 0, s>>>((uint64_t)c->debug_stall_ms * 100000u);
+        HIP_TRY(hipGetLastError());
+    }
     if (timed) {
         HIP_TRY(hipEventRecord(c->ev0, s));
         c->timed_recorded = true;
@@ -2128,7 +2142,7 @@ namespace {
 // accumulation in the ctx's (possibly shared) buffer. *d_display = the slab
 // that holds the display after the last frame.
 int enqueue_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, uint32_t* d_out,
-                  uint32_t** d_display, const char* fn)
+                  uint32_t** d_display, const char* fn, bool independent = false)
 {
     if (!ctx_ok(c, true, fn)) return MIRT_E_NOSCENE;
     if (!cam || !frame_desc_valid(fd)) {
@@ -2149,9 +2163,27 @@ int enqueue_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd
     // a new frame geometry starts a fresh accumulation buffer
     int rc = accum_prepare(c->acc, pixels, c->stream);
     if (rc) return rc;
-    rc = launch_render(c, f, d_out, c->acc->d_acc, c->stream, true, nullptr);
+    // independent fresh frames (mirt_multi's launches of several frames): raw
+    // slabs, then the last one folded as a fresh frame, so the (possibly
+    // shared) accumulation buffer holds what a sequence of fresh frames leaves
+    const bool raw = independent && f.samples > 1 && !f.accumulate;
+    rc = launch_render(c, f, d_out, raw ? nullptr : c->acc->d_acc, c->stream, true, nullptr);
     if (rc) return rc;
     *d_display = d_out + (size_t)(f.samples - 1) * pixels;
+    if (raw) {
+        FrameConst f1 = f;
+        f1.samples = 1;
+        f1.accumulate = 0;
+        AccumShare* chain = accum_chain(c);
+        if (chain && chain->has_fold) HIP_TRY(hipStreamWaitEvent(c->stream, chain->folded, 0));
+        fold_samples_kernel<<<(unsigned)((pixels + 255) / 256), 256, 0, c->stream>>>(f1, *d_display, c->acc->d_acc);
+        HIP_TRY(hipGetLastError());
+        if (chain) {
+            HIP_TRY(hipEventRecord(chain->folded, c->stream));
+            chain->has_fold = true;
+        }
+        HIP_TRY(hipEventRecord(c->done, c->stream));
+    }
     return MIRT_OK;
 }
 
@@ -2175,9 +2207,9 @@ int enqueue_host_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_des
 
 namespace mirt {
 int enqueue_frame_device(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, uint32_t* d_out,
-                         uint32_t** d_display, const char* fn)
+                         uint32_t** d_display, const char* fn, bool independent)
 {
-    return enqueue_frame(c, cam, fd, d_out, d_display, fn);
+    return enqueue_frame(c, cam, fd, d_out, d_display, fn, independent);
 }
 int ctx_device(const mirt_ctx* c) { return c->device; }
 }  // namespace mirt
@@ -2187,12 +2219,16 @@ extern "C" {
 namespace {
 
 // The device-visible address of a page-locked host range (mirt_host_alloc /
-// mirt_host_register memory), or null for pageable memory.
+// mirt_host_register memory), or null for pageable memory -- and for a range
+// that spans separately registered pieces: the device mapping must be ONE
+// contiguous range (the last byte's device address = the first's + bytes - 1),
+// else the kernels' stores would land elsewhere (the copy path takes it).
 uint32_t* host_mapped(const void* p, size_t bytes)
 {
     hipPointerAttribute_t a, b;
     if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeHost || !a.devicePointer ||
-        hipPointerGetAttributes(&b, (const char*)p + bytes - 1) != hipSuccess || b.type != hipMemoryTypeHost) {
+        hipPointerGetAttributes(&b, (const char*)p + bytes - 1) != hipSuccess || b.type != hipMemoryTypeHost ||
+        (const char*)b.devicePointer != (const char*)a.devicePointer + bytes - 1) {
         (void)hipGetLastError();   // a pageable pointer is an error to the query, not to the caller
         return nullptr;
     }
@@ -2740,6 +2776,10 @@ int mirt_set_option(mirt_ctx* c, int option, int value)
         if (value < 0 || value > 2) break;
         c->zero_copy = value;
         return MIRT_OK;
+    case MIRT_OPT_DEBUG_STALL_MS:
+        if (value < 0 || value > 10000) break;
+        c->debug_stall_ms = value;
+        return MIRT_OK;
     case MIRT_OPT_QUEUE_ORDER:
         if (value < 0 || value > 2) break;
         c->queue_order = value;
@@ -2774,6 +2814,7 @@ int mirt_get_option(mirt_ctx* c, int option)
     if (option == MIRT_OPT_QUAD_BATCH) return c->quad_batch;
     if (option == MIRT_OPT_ZERO_COPY) return c->zero_copy;
     if (option == MIRT_OPT_QUEUE_ORDER) return c->queue_order;
+    if (option == MIRT_OPT_DEBUG_STALL_MS) return c->debug_stall_ms;
     if (option == MIRT_OPT_LEAF_BATCH) return leaf_batch(c) ? 1 : 0;  // in effect for the uploaded scene
     set_error("mirt_get_option: bad option %d", option);
     return MIRT_E_INVALID;

@@ -431,17 +431,21 @@ class MultiRenderer:
     """One frame loop over several GPUs from this process (include/mirt_multi.h,
     SURVEY §8(b) mirt_init(num_gpus)): interleaved row blocks per rank, the
     slabs gathered to rank 0 over RCCL (distinct devices) or by device copies
-    ("copy": forced, or a device listed twice -- n shards on one GPU), `lanes`
-    frames in flight. Frames equal Renderer.render_frame's on one GPU."""
+    ("copy": forced, or a device listed twice -- n shards on one GPU), or with
+    host_direct every rank's blocks copied straight into the host frame;
+    `lanes` launches in flight, each of one or more frames. Frames equal
+    Renderer.render_frame's on one GPU."""
 
-    def __init__(self, devices, lanes=1, copy=False):
+    def __init__(self, devices, lanes=1, copy=False, host_direct=False):
         self.L = load()
         devs = (C.c_int * len(devices))(*devices)
         h = C.c_void_p()
-        check(self.L.mirt_multi_create(devs, len(devices), lanes, abi.MULTI_COPY if copy else 0, C.byref(h)),
-              "mirt_multi_create")
+        flags = (abi.MULTI_COPY if copy else 0) | (abi.MULTI_HOST_DIRECT if host_direct else 0)
+        check(self.L.mirt_multi_create(devs, len(devices), lanes, flags, C.byref(h)), "mirt_multi_create")
         self.h = h
         self.devices = list(devices)
+        self.lanes = lanes
+        self.launches = 0   # launch k runs on lane k % lanes (mirt_multi's rotation)
 
     def close(self):
         if self.h:
@@ -465,8 +469,26 @@ class MultiRenderer:
         return self.L.mirt_multi_backend(self.h).decode()
 
     @property
+    def delivery(self):
+        return self.L.mirt_multi_delivery(self.h).decode()
+
+    @property
     def size(self):
         return self.L.mirt_multi_size(self.h)
+
+    @property
+    def failed(self):
+        return self.L.mirt_multi_failed(self.h) == 1
+
+    def ctx(self, lane, rank):
+        """(lane, rank)'s mirt_ctx handle (owned by the multi renderer)."""
+        return self.L.mirt_multi_ctx(self.h, lane, rank)
+
+    def phase_log(self, lane, rank, n):
+        """mirt_phase_log of (lane, rank)'s context: [primary_ms, bounce_ms] of its last n frames."""
+        buf = (C.c_float * (2 * n))()
+        got = check(self.L.mirt_phase_log(self.ctx(lane, rank), buf, n), "mirt_phase_log")
+        return [(buf[2 * i], buf[2 * i + 1]) for i in range(got)]
 
     def upload(self, spheres, bvh):
         spheres = np.ascontiguousarray(spheres, abi.SPHERE)
@@ -477,7 +499,17 @@ class MultiRenderer:
             check(self.L.mirt_multi_scene_upload(self.h, ptr(spheres), len(spheres), bvh), "mirt_multi_scene_upload")
 
     def set_option(self, option, value):
+        """MULTI_OPT_* (timeout, emulation) or a MIRT_OPT_* for every context."""
         check(self.L.mirt_multi_set_option(self.h, option, value), "mirt_multi_set_option")
+
+    def get_option(self, option):
+        return check(self.L.mirt_multi_get_option(self.h, option), "mirt_multi_get_option")
+
+    def emulate(self, world, rank):
+        """Measurement only (one rank): play shard `rank` of a frame split
+        `world` ways (MIRT_MULTI_OPT_EMULATE_*); frames are then incomplete."""
+        self.set_option(abi.MULTI_OPT_EMULATE_WORLD, world)
+        self.set_option(abi.MULTI_OPT_EMULATE_RANK, rank)
 
     def render_frame(self, cam, width, height, depth=5, use_bvh=True, seed=1, sample=0, accumulate=False, frames=1,
                      row_block=8, samples=1, jitter=False):
@@ -486,16 +518,38 @@ class MultiRenderer:
                         jitter)
         out = np.zeros((height, width, 4), np.uint8)
         check(self.L.mirt_multi_render_frame(self.h, C.byref(cam), C.byref(fd), ptr(out)), "mirt_multi_render_frame")
+        self.launches += 1
         return out
+
+    @staticmethod
+    def _host(out, fd):
+        arr = out.array if isinstance(out, HostBuffer) else out
+        if arr.nbytes < fd.width * fd.height * 4 or not arr.flags["C_CONTIGUOUS"]:
+            raise MirtError("mirt_multi: output too small or not contiguous")
+        return arr
 
     def render_frame_async(self, cam, fd, out):
         """Enqueue a whole frame into `out` (HostBuffer or uint8 array of
         height x width x 4) on the next lane; complete after wait()."""
-        arr = out.array if isinstance(out, HostBuffer) else out
-        if arr.nbytes < fd.width * fd.height * 4 or not arr.flags["C_CONTIGUOUS"]:
-            raise MirtError("render_frame_async: output too small")
+        arr = self._host(out, fd)
         check(self.L.mirt_multi_render_frame_async(self.h, C.byref(cam), C.byref(fd), ptr(arr)),
               "mirt_multi_render_frame_async")
+        self.launches += 1
+
+    def render_frames_async(self, cam, fd, outs, nframes=None, full_grid=False):
+        """One launch of len(outs) successive frames (RNG samples fd.sample + j)
+        on the next lane, frame j into outs[j]; outs None: `nframes` frames
+        left on the devices. Complete after wait() (or the lane's next launch)."""
+        n = len(outs) if outs is not None else int(nframes or 1)
+        if outs is not None:
+            arrs = [self._host(o, fd) for o in outs]
+            cp = (C.c_void_p * n)(*[a.ctypes.data for a in arrs])
+        else:
+            cp = None
+        check(self.L.mirt_multi_render_frames_async(self.h, C.byref(cam), C.byref(fd), n,
+                                                    abi.MULTI_FULL_GRID if full_grid else 0, cp),
+              "mirt_multi_render_frames_async")
+        self.launches += 1
 
     def wait(self):
         check(self.L.mirt_multi_wait(self.h), "mirt_multi_wait")

@@ -419,11 +419,15 @@ enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3,
                                        1 (default) for the blocking mirt_render_frame, 2 for
                                        mirt_render_frame_async too, 0 never. Pageable memory:
                                        a copy. */
-       MIRT_OPT_QUEUE_ORDER = 18    /* wavefront: order of a frame's first bounces in the bounce
+       MIRT_OPT_QUEUE_ORDER = 18,   /* wavefront: order of a frame's first bounces in the bounce
                                        queue -- 0 (default) = tile order for the blocking
                                        mirt_render_frame (a frame alone on the chip), grouped by
                                        direction octant per workgroup for frames in flight;
-                                       1 = always grouped; 2 = always tile order. Speed only. */ };
+                                       1 = always grouped; 2 = always tile order. Speed only. */
+       MIRT_OPT_DEBUG_STALL_MS = 19 /* test hook: every frame of this context starts behind a
+                                       kernel that waits this many ms (0..10000, default 0), then
+                                       exits -- a frame that overruns a caller's deadline
+                                       (mirt_multi's MIRT_MULTI_OPT_TIMEOUT_MS) without a hang */ };
 /* Traversal ids keep their first-release values (mirt 0.1: TILE 0, WAVEFRONT 5).
    ABI note: the mirt 0.2 header numbered WAVEFRONT 1; mirt_set_option accepts
    1 as a deprecated alias of MIRT_TRAV_WAVEFRONT (mirt_get_option reads back

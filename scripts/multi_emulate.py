@@ -1,0 +1,87 @@
+"""Per-shard emulation of bench.py's N-GPU timed loop on ONE GPU, through the
+same C-ABI path the N-GPU run takes (include/mirt_multi.h): a one-rank
+mirt_multi with MIRT_MULTI_OPT_EMULATE_WORLD = N / _RANK = k renders shard k
+of every frame with bench.py's schedule at N (lanes, frames per launch, the
+1.5-per-CU bounce grid, the burst's last launches on the full grid), and
+delivers what rank k delivers at N GPUs:
+  gather:      its slabs through RCCL (a self send/recv on the one device) and,
+               as rank 0, the other shards' receives (HBM writes), the
+               de-interleave and every frame's D2H into page-locked memory;
+  host-direct: its own strided copies of its row blocks into the host frames.
+Rank k's time at N GPUs is its time here (xGMI wire time and cross-GPU
+interference aside), so the job's predicted rate is W*H*K / max_k(t_k).
+
+    python scripts/multi_emulate.py --worlds 1,2,4,8 [--delivery gather|host-direct] [--steps 20]
+
+The script raises GPU_MAX_HW_QUEUES to --hw-queues (16, as bench.py's N > 1
+measuring child) before the HIP runtime starts; pass 0 to keep the
+environment's (bench.py's N = 1 leg keeps it).
+"""
+import argparse
+import importlib.util
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+bench = importlib.util.module_from_spec(spec)
+spec.loader.exec_module(bench)
+mirt = bench.mirt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--worlds", default="1,2,4,8")
+    ap.add_argument("--workload", default="1080p_10k", choices=sorted(bench.WORKLOADS))
+    ap.add_argument("--delivery", default="gather", choices=("gather", "host-direct"))
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--rounds", type=int, default=1, help="repeat every shard's measurement (its best round counts)")
+    ap.add_argument("--pipeline", type=int, default=0)
+    ap.add_argument("--batch", type=int, default=0)
+    ap.add_argument("--tail-grid", type=int, default=-1)
+    ap.add_argument("--bounce-blocks", type=int, default=-1)
+    ap.add_argument("--accumulate", action="store_true")
+    ap.add_argument("--opt", action="append", default=[])
+    ap.add_argument("--hw-queues", type=int, default=16)
+    a = ap.parse_args()
+    if a.hw_queues and int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < a.hw_queues:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(a.hw_queues)   # before the first HIP call of this process
+    wl = bench.WORKLOADS[a.workload]
+    bench.WORKLOAD = a.workload
+    bench.W, bench.H, bench.NSPH, bench.KIND, bench.SPP, bench.JITTER = (wl["W"], wl["H"], wl["NSPH"], wl["KIND"],
+                                                                          wl["SPP"], wl["JITTER"])
+    W, H, SPP = bench.W, bench.H, bench.SPP
+    spheres, bvh, _ = bench.make_scene()
+    cam = mirt.default_camera()
+    for world in (int(w) for w in a.worlds.split(",")):
+        lanes, per, tail_n, blocks = bench.schedule(a, world)
+        m = bench.open_multi(1, lanes, a.delivery == "host-direct", spheres, bvh, blocks, a.opt)
+        bufs = bench.host_bufs(lanes, per)
+        timed = bench.plan(a.warmup, a.steps, per)
+        tail = bench.tail_of(timed, tail_n, lanes, blocks)
+        per_rank = []
+        for k in range(world):
+            m.emulate(world, k)
+            best = None
+            for _ in range(a.rounds):
+                el = bench.timed_loop(m, cam, bench.plan(0, a.warmup, per), timed, bufs, bench.DEPTH, a.accumulate,
+                                      tail)
+                best = el if best is None else min(best, el)
+            per_rank.append(best)
+        m.close()
+        bench.close_bufs(bufs)
+        slow = max(per_rank)
+        print(json.dumps({
+            "workload": a.workload, "delivery": a.delivery, "world": world, "steps": a.steps, "warmup": a.warmup,
+            "lanes": lanes, "frames_per_launch": per, "tail_grid": len(tail), "bounce_blocks": blocks,
+            "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+            "rank_ms_per_frame": [round(t / a.steps * 1e3, 4) for t in per_rank],
+            "slowest_rank": per_rank.index(slow),
+            "pred_job_mrays_s": round(W * H * SPP * a.steps / slow / 1e6, 1)}), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

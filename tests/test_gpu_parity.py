@@ -126,14 +126,11 @@ def test_sharded_frames_identical(gpu, mirt, world):
     gpu.upload(s, b)
     cam = mirt.default_camera()
     full = gpu.render_frame(cam, 1920, 1080, depth=5, seed=1)
-    rows = shard.slab_rows(1080, 8, world)
-    slabs = np.zeros((world, rows, 1920, 4), np.uint8)
-    for r in range(world):
-        part = gpu.render_frame(cam, 1920, 1080, depth=5, seed=1, shard=r, num_shards=world)
-        slabs[r, :len(part)] = part
-    st = torch.from_numpy(slabs.view(np.int32).reshape(world, rows, 1920))
-    frame = shard.as_rgba(shard.assemble(st, 1080, 8)).numpy()
+    slabs = [gpu.render_frame(cam, 1920, 1080, depth=5, seed=1, shard=r, num_shards=world)[None]
+             for r in range(world)]
+    frame = shard.assemble_gather(slabs, 1080, 8)[0]
     assert (frame == full).all()
+    assert (shard.assemble_direct(slabs, 1080, 8)[0] == full).all()
 
 
 def test_accumulate_matches_oracle(gpu, mirt, oracle, small):
@@ -221,41 +218,36 @@ def test_weak_scaling_step_identical(gpu, mirt, world):
     cam = mirt.default_camera()
     W, H = 1920, 1080
     full = gpu.render_frame(cam, W, H, depth=5, seed=1, samples=world)
-    rows = shard.slab_rows(H, 8, world)
-    slabs = np.zeros((world, rows, W, 4), np.uint8)
-    for r in range(world):
-        part = gpu.render_frame(cam, W, H, depth=5, seed=1, samples=world, shard=r, num_shards=world)
-        slabs[r, :len(part)] = part
-    st = torch.from_numpy(slabs.view(np.int32).reshape(world, rows, W))
-    frame = shard.as_rgba(shard.assemble(st, H, 8)).numpy()
+    slabs = [gpu.render_frame(cam, W, H, depth=5, seed=1, samples=world, shard=r, num_shards=world)[None]
+             for r in range(world)]
+    frame = shard.assemble_gather(slabs, H, 8)[0]
     assert (frame == full).all()
 
 
 def test_double_buffered_frames_identical(gpu, mirt):
-    """The bench's double buffering (two contexts alternating frames on their
-    own streams, launches overlapping) leaves every frame's bytes unchanged."""
-    from importlib import import_module
-    import torch
-    shard = import_module("cs201_sah-bvh_ray_tracer_amd.shard")
+    """Launches in flight (mirt_multi, two lanes of contexts alternating
+    frames on their own streams, launches overlapping) leave every frame's
+    bytes unchanged."""
     s, b = _scene(mirt, "render", 10000)
     gpu.upload(s, b)
-    r2 = mirt.Renderer(0)
+    cam = mirt.default_camera()
+    W, H = 640, 360
+    bufs = [mirt.HostBuffer((H, W, 4)) for _ in range(5)]
     try:
-        r2.upload(s, b)
-        cam = mirt.default_camera()
-        W, H = 640, 360
-        sf = shard.ShardedFrame(gpu, W, H, 8, renderers=[gpu, r2])
-        outs = []
-        for k in range(5):
-            sf.render_local(cam, sf.desc(depth=5, seed=3, sample=k))
-            with torch.cuda.stream(sf.stream):   # read it on the frame's own stream
-                outs.append(sf.gather().clone())
-        torch.cuda.synchronize()
-        for k, f in enumerate(outs):
-            ref = gpu.render_frame(cam, W, H, depth=5, seed=3, sample=k)
-            assert (shard.as_rgba(f).cpu().numpy() == ref).all(), k
+        with mirt.MultiRenderer([0], lanes=2) as m:
+            m.upload(s, b)
+            for k in range(5):
+                m.render_frames_async(cam, mirt.frame_desc(W, H, depth=5, seed=3, sample=k), [bufs[k]])
+                if k % 2 == 1:
+                    m.wait()
+            m.wait()
+            got = [x.array.copy() for x in bufs]
     finally:
-        r2.close()
+        for x in bufs:
+            x.close()
+    for k in range(5):
+        ref = gpu.render_frame(cam, W, H, depth=5, seed=3, sample=k)
+        assert (got[k] == ref).all(), k
 
 
 def test_async_host_frames_pipelined(gpu, mirt, golden):
@@ -999,41 +991,39 @@ def test_phantom_grazing_rays(gpu, mirt, oracle):
     assert int(want["hit"].sum()) > len(ray) // 4
 
 
-@pytest.mark.parametrize("batch", [1, 4])
-def test_bench_launch_plan_displays(gpu, mirt, batch):
-    """bench.py's timed loop: successive frames of the still-camera display
-    loop, `batch` per launch, launches rotating over four ctxs that share one
-    accumulation buffer (ShardedFrame(share_accum=True)): the display of
-    every frame (its own slab) equals frame k of successive blocking
-    accumulate calls on one ctx."""
-    from importlib import import_module
-    import torch
-    shard = import_module("cs201_sah-bvh_ray_tracer_amd.shard")
+@pytest.mark.parametrize("batch,accumulate,direct", [(1, True, False), (4, True, False), (4, False, False),
+                                                    (4, False, True), (3, True, True)])
+def test_bench_launch_plan_displays(gpu, mirt, batch, accumulate, direct):
+    """bench.py's timed loop through mirt_multi: `batch` successive frames per
+    launch, launches rotating over four lanes (the lanes share one
+    accumulation buffer, each context's bounce pass at the 1.5-per-CU grid
+    mirt_multi sets for lanes > 1, the last launch on the full grid), every
+    frame delivered to its own host buffer (gather or host-direct): each
+    equals frame k of successive blocking calls on one ctx (accumulating:
+    the display main.c:379-408 shows after frame k)."""
     s, b = _scene(mirt, "render", 10000)
     W, H, F = 320, 180, 12
-    rs = [mirt.Renderer(0) for _ in range(4)]
+    cam = mirt.default_camera()
+    bufs = [mirt.HostBuffer((H, W, 4)) for _ in range(F)]
     try:
-        for x in rs:
-            x.upload(s, b)
-            x.set_option(mirt.abi.OPT_BOUNCE_BLOCKS, 384)
-        cam = mirt.default_camera()
-        sf = shard.ShardedFrame(rs[0], W, H, 8, samples=batch, renderers=rs, share_accum=True)
-        shown = []
-        for f0 in range(0, F, batch):
-            sf.render_local(cam, sf.desc(depth=5, seed=1, sample=f0, accumulate=f0 > 0, frames=f0 + 1,
-                                         samples=batch))
-            with torch.cuda.stream(sf.stream):
-                shown.append(sf.gather(every=1).clone())
-        torch.cuda.synchronize()
-        got = [shard.as_rgba(fr).cpu().numpy() for g in shown for fr in g]
-        assert len(got) == F
-        gpu.upload(s, b)
-        for k in range(F):
-            seq = gpu.render_frame(cam, W, H, depth=5, seed=1, sample=k, accumulate=k > 0, frames=k + 1)
-            assert (got[k] == seq).all(), k
+        with mirt.MultiRenderer([0], lanes=4, host_direct=direct) as m:
+            m.upload(s, b)
+            assert m.delivery == ("host-direct" if direct else "gather")
+            for f0 in range(0, F, batch):
+                k = min(batch, F - f0)
+                acc = accumulate and f0 > 0
+                fd = mirt.frame_desc(W, H, depth=5, seed=1, sample=f0, accumulate=acc, frames=f0 + 1 if acc else 1)
+                m.render_frames_async(cam, fd, bufs[f0:f0 + k], full_grid=f0 + k >= F)
+            m.wait()
+            got = [x.array.copy() for x in bufs]
     finally:
-        for x in rs:
+        for x in bufs:
             x.close()
+    gpu.upload(s, b)
+    for k in range(F):
+        acc = accumulate and k > 0
+        seq = gpu.render_frame(cam, W, H, depth=5, seed=1, sample=k, accumulate=acc, frames=k + 1 if acc else 1)
+        assert (got[k] == seq).all(), k
 
 
 @pytest.mark.parametrize("batch", [0, 1])

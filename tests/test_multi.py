@@ -142,3 +142,101 @@ def test_multi_rejects_sharded_descriptor(mirt, scene10k):
         out = np.zeros((36, 64, 4), np.uint8)
         with pytest.raises(mirt.MirtError):
             m.render_frame_async(mirt.default_camera(), fd, out)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices,direct,batch", [([0], False, 4), ([0], True, 4), ([0, 0, 0], False, 3),
+                                                  ([0, 0, 0], True, 4), ([0] * 8, True, 2)])
+def test_multi_batched_launches_equal_one_gpu(gpu, mirt, scene10k, devices, direct, batch):
+    """Launches of several successive fresh frames (bench.py's N >= 4
+    schedule), lanes in flight, the gather (RCCL at n = 1, copy across
+    same-device ranks) or the host-direct delivery (each rank's strided copies
+    into the host frame): frame j of every launch equals one context's
+    blocking frame of that RNG sample; the last launch on the full grid."""
+    s, b = scene10k
+    W, H, F = 333, 187, 9    # ragged: the last 8-row block is short
+    cam = mirt.default_camera()
+    bufs = [mirt.HostBuffer((H, W, 4)) for _ in range(F)]
+    try:
+        with mirt.MultiRenderer(devices, lanes=3, host_direct=direct) as m:
+            m.upload(s, b)
+            for f0 in range(0, F, batch):
+                k = min(batch, F - f0)
+                m.render_frames_async(cam, mirt.frame_desc(W, H, depth=5, seed=4, sample=f0), bufs[f0:f0 + k],
+                                      full_grid=f0 + k >= F)
+            m.wait()
+            got = [x.array.copy() for x in bufs]
+            # a fresh single frame after the batches: the accumulation buffer
+            # holds the last batch's last frame, so an accumulating frame after
+            # it equals the one-context sequence
+            fd = mirt.frame_desc(W, H, depth=5, seed=4, sample=F, accumulate=True, frames=2)
+            m.render_frame_async(cam, fd, bufs[0])
+            m.wait()
+            acc = bufs[0].array.copy()
+    finally:
+        for x in bufs:
+            x.close()
+    gpu.upload(s, b)
+    for j in range(F):
+        assert (got[j] == gpu.render_frame(cam, W, H, depth=5, seed=4, sample=j)).all(), j
+    gpu.render_frame(cam, W, H, depth=5, seed=4, sample=F - 1)
+    assert (acc == gpu.render_frame(cam, W, H, depth=5, seed=4, sample=F, accumulate=True, frames=2)).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 8])
+def test_multi_emulated_shard_rows(gpu, mirt, scene10k, world):
+    """The per-shard emulation (MIRT_MULTI_OPT_EMULATE_*, one GPU playing rank
+    k of a world-way split, host-direct): rank k delivers exactly its own row
+    blocks, and those rows equal the one-GPU frame's."""
+    s, b = scene10k
+    W, H = 320, 180
+    cam = mirt.default_camera()
+    gpu.upload(s, b)
+    full = gpu.render_frame(cam, W, H, depth=5, seed=1)
+    with mirt.MultiRenderer([0], lanes=2, host_direct=True) as m:
+        m.upload(s, b)
+        for k in range(world):
+            m.emulate(world, k)
+            out = np.full((H, W, 4), 7, np.uint8)
+            m.render_frame_async(cam, mirt.frame_desc(W, H, depth=5, seed=1), out)
+            m.wait()
+            mine = (np.arange(H) // 8) % world == k
+            assert (out[mine] == full[mine]).all(), k
+            assert (out[~mine] == 7).all(), k
+        m.emulate(0, 0)
+        assert (m.render_frame(cam, W, H, depth=5, seed=1) == full).all()
+
+
+@pytest.mark.gpu
+def test_multi_timeout_fails_with_status(mirt, scene10k):
+    """A rank whose frame overruns MIRT_MULTI_OPT_TIMEOUT_MS (the test hook
+    MIRT_OPT_DEBUG_STALL_MS puts a bounded 4 s wait before its frames) makes
+    the call return MIRT_E_DEVICE within the deadline + a margin, naming the
+    stuck rank; the object then fails every call, and destroying it does not
+    wait. (Copy mode, two ranks on one GPU: no RCCL kernels are queued behind
+    the stall.)"""
+    import time
+    s, b = scene10k
+    m = mirt.MultiRenderer([0, 0], lanes=1)
+    try:
+        m.upload(s, b)
+        m.set_option(mirt.abi.MULTI_OPT_TIMEOUT_MS, 1000)
+        assert mirt.load().mirt_set_option(m.ctx(0, 1), mirt.abi.OPT_DEBUG_STALL_MS, 4000) == 0
+        t0 = time.monotonic()
+        with pytest.raises(mirt.MirtError, match="stuck rank"):
+            m.render_frame(mirt.default_camera(), 320, 180, depth=5, seed=1)
+        dt = time.monotonic() - t0
+        assert 1.0 <= dt < 3.5, dt
+        assert m.failed
+        with pytest.raises(mirt.MirtError):
+            m.render_frame(mirt.default_camera(), 320, 180, depth=5, seed=1)
+    finally:
+        t1 = time.monotonic()
+        m.close()
+        assert time.monotonic() - t1 < 1.0
+    # the stall ends by itself; the device is usable afterwards
+    time.sleep(3.5)
+    with mirt.Renderer(0) as r:
+        r.upload(s, b)
+        assert r.render_frame(mirt.default_camera(), 64, 36, depth=5, seed=1).shape == (36, 64, 4)

@@ -1,8 +1,10 @@
-"""The N>1 path on CPU: world_size 2 and 3 over gloo. Each rank produces its
-row-block slab (here with the oracle standing in for the GPU kernel -- this
-test covers the shard geometry, the gather and the de-interleave, which are
-the same code bench.py runs over RCCL), rank 0 gathers and assembles, and the
-frame must equal the single-process frame byte for byte."""
+"""The N>1 frame geometry on CPU, over processes: world_size 2 and 3 over
+gloo. Each rank produces its row-block slabs (the oracle standing in for the
+GPU kernels), rank 0 gathers them (gloo here; RCCL ncclSend/ncclRecv in
+csrc/multi.hip) and assembles them with shard.py's restatements of BOTH of
+mirt_multi's deliveries -- deinterleave_kernel (gather to GPU 0) and the
+per-rank strided host copies (host-direct) -- and every frame must equal the
+single-process frame byte for byte."""
 import os
 import socket
 import sys
@@ -44,16 +46,19 @@ def _worker(rank, world, port, result_path, frames=1):
     slab = np.zeros((frames, shard.slab_rows(H, RB, world), W, 4), np.uint8)
     for j in range(frames):
         slab[j, :len(rows)] = o.render(cam, W, H, s, t, depth=5, mode=1, seed=2, sample=j, rows=rows, threads=1)
-    st = torch.from_numpy(slab.view(np.int32).reshape(frames, -1, W))
-    # one frame: a (rows, W) slab; several (bench.py's multi-frame launches): (frames, rows, W)
-    frame = shard.gather_frame(st[0] if frames == 1 else st, H, RB)
+    st = torch.from_numpy(np.ascontiguousarray(slab.view(np.int32).reshape(frames, -1, W)))
+    got_all = [torch.empty_like(st) for _ in range(world)] if rank == 0 else None
+    dist.gather(st, got_all, dst=0)
     if rank == 0:
+        # each shard's real rows (the slabs are padded to shard 0's height)
+        slabs = [g.numpy()[:, :shard.shard_row_count(H, RB, world, r)] for r, g in enumerate(got_all)]
         ok = shape = 1
-        for j in range(frames):
-            full = o.render(cam, W, H, s, t, depth=5, mode=1, seed=2, sample=j, threads=1)
-            got = shard.as_rgba(frame if frames == 1 else frame[j]).numpy()
-            ok &= int((got == full).all())
-            shape &= int(got.shape == full.shape)
+        for assembled in (shard.assemble_gather(slabs, H, RB), shard.assemble_direct(slabs, H, RB)):
+            for j in range(frames):
+                full = o.render(cam, W, H, s, t, depth=5, mode=1, seed=2, sample=j, threads=1)
+                got = shard.as_rgba(assembled[j])
+                ok &= int((got == full).all())
+                shape &= int(got.shape == full.shape)
         np.save(result_path, np.array([ok, shape]))
     o.free(t)
     dist.barrier()
