@@ -33,5 +33,8 @@ int validate_flat(const mirt_node* nd, int nn, int num_spheres, int sphere_lo, c
 int enqueue_frame_device(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, uint32_t* d_out,
                          uint32_t** d_display, const char* fn, bool independent = false);
 int ctx_device(const mirt_ctx* c);
+// [p, p + bytes) is ONE page-locked host range (mirt_host_alloc /
+// mirt_host_register): copies into it are DMA, asynchronous to the host.
+bool host_page_locked(const void* p, size_t bytes);
 
 }  // namespace mirt

@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstring>
 #include <new>
 #include <string>
 #include <thread>
@@ -108,6 +109,17 @@ struct Lane {
     // a launch was (possibly partly) enqueued and not yet waited for: set
     // before the first enqueue, cleared only once every rank's work is done
     bool pending = false;
+    // outputs in pageable memory: a copy into them would block the enqueuing
+    // thread behind the frame (no bounded wait), so the frames land in this
+    // page-locked staging area and are copied out once the lane is waited for
+    uint8_t* stage = nullptr;
+    size_t stage_cap = 0;
+    struct Deferred {
+        void* dst;
+        const void* src;
+        size_t bytes;
+    };
+    std::vector<Deferred> deferred;
 };
 
 }  // namespace
@@ -141,6 +153,7 @@ int failed_status(const mirt_multi* m, const char* fn)
 int fail_multi(mirt_multi* m, const std::string& why)
 {
     m->failed = true;
+    for (Lane& L : m->lanes) L.deferred.clear();
     m->fail_msg = why;
     for (ncclComm_t& c : m->comm)
         if (c) {
@@ -190,6 +203,8 @@ int wait_lane(mirt_multi* m, int li)
         }
     }
     L.pending = false;
+    for (const Lane::Deferred& d : L.deferred) std::memcpy(d.dst, d.src, d.bytes);
+    L.deferred.clear();
     return MIRT_OK;
 }
 
@@ -235,6 +250,28 @@ int enqueue(mirt_multi* m, Lane& L, const mirt_camera* cam, const mirt_frame_des
         int rc = grow(dev0, &L.gathered, &L.gathered_cap, 4 * shard_stride * world + 4);
         if (!rc && world > 1 && rank0_assembles) rc = grow(dev0, &L.frame, &L.frame_cap, 4 * frame_elems * nframes + 4);
         if (rc) return rc;
+    }
+    // where frame j lands: the caller's buffer if it is page-locked, else
+    // the lane's staging area (copied out by wait_lane)
+    std::vector<mirt_rgba8*> dst(nframes, nullptr);
+    L.deferred.clear();
+    if (outs) {
+        const size_t fb = 4 * frame_elems;
+        for (int j = 0; j < nframes; j++) {
+            if (host_page_locked(outs[j], fb)) {
+                dst[j] = outs[j];
+                continue;
+            }
+            if (L.stage_cap < fb * nframes) {
+                if (L.stage) MHIP(hipHostFree(L.stage));
+                L.stage = nullptr;
+                L.stage_cap = 0;
+                MHIP(hipHostMalloc((void**)&L.stage, fb * nframes, hipHostMallocDefault));
+                L.stage_cap = fb * nframes;
+            }
+            dst[j] = (mirt_rgba8*)(L.stage + fb * j);
+            L.deferred.push_back({outs[j], dst[j], fb});
+        }
     }
     L.pending = true;
     // every rank renders its row blocks of all frames: `samples` slabs in the
@@ -318,7 +355,7 @@ int enqueue(mirt_multi* m, Lane& L, const mirt_camera* cam, const mirt_frame_des
             }
             if (outs)
                 for (int j = 0; j < nframes; j++)
-                    MHIP(hipMemcpyAsync(outs[j], frames + (size_t)j * frame_elems, 4 * frame_elems,
+                    MHIP(hipMemcpyAsync(dst[j], frames + (size_t)j * frame_elems, 4 * frame_elems,
                                         hipMemcpyDeviceToHost, s0));
         }
     } else {
@@ -338,7 +375,7 @@ int enqueue(mirt_multi* m, Lane& L, const mirt_camera* cam, const mirt_frame_des
             MHIP(hipSetDevice(m->dev[r]));
             for (int j = 0; j < nframes; j++) {
                 const uint32_t* sj = src[r] + (size_t)j * elems;
-                uint32_t* dj = (uint32_t*)outs[j];
+                uint32_t* dj = (uint32_t*)dst[j];
                 if (nfull > 0)
                     MHIP(hipMemcpy2DAsync(dj + (size_t)s * rb * W, (size_t)world * rb * W * 4, sj, (size_t)rb * W * 4,
                                           (size_t)rb * W * 4, nfull, hipMemcpyDeviceToHost, stream_of(L.ctx[r])));
@@ -500,6 +537,7 @@ void mirt_multi_destroy(mirt_multi* m)
         (void)hipSetDevice(m->dev[0]);
         if (L.gathered) (void)hipFree(L.gathered);
         if (L.frame) (void)hipFree(L.frame);
+        if (L.stage) (void)hipHostFree(L.stage);
     }
     for (ncclComm_t c : m->comm)
         if (c) (void)ncclCommDestroy(c);

@@ -2237,6 +2237,12 @@ uint32_t* host_mapped(const void* p, size_t bytes)
 
 }  // namespace
 
+extern "C++" {
+namespace mirt {
+bool host_page_locked(const void* p, size_t bytes) { return host_mapped(p, bytes) != nullptr; }
+}  // namespace mirt
+}
+
 static int render_frame_blocking(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd, mirt_rgba8* out);
 
 // The blocking call renders one frame with nothing after it on the ctx: its
