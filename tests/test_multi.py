@@ -194,18 +194,23 @@ def test_multi_emulated_shard_rows(gpu, mirt, scene10k, world):
     cam = mirt.default_camera()
     gpu.upload(s, b)
     full = gpu.render_frame(cam, W, H, depth=5, seed=1)
-    with mirt.MultiRenderer([0], lanes=2, host_direct=True) as m:
-        m.upload(s, b)
-        for k in range(world):
-            m.emulate(world, k)
-            out = np.full((H, W, 4), 7, np.uint8)
-            m.render_frame_async(cam, mirt.frame_desc(W, H, depth=5, seed=1), out)
-            m.wait()
-            mine = (np.arange(H) // 8) % world == k
-            assert (out[mine] == full[mine]).all(), k
-            assert (out[~mine] == 7).all(), k
-        m.emulate(0, 0)
-        assert (m.render_frame(cam, W, H, depth=5, seed=1) == full).all()
+    hb = mirt.HostBuffer((H, W, 4))     # page-locked: the strided copies land in it directly
+    try:
+        with mirt.MultiRenderer([0], lanes=2, host_direct=True) as m:
+            m.upload(s, b)
+            for k in range(world):
+                m.emulate(world, k)
+                out = hb.array
+                out[:] = 7
+                m.render_frame_async(cam, mirt.frame_desc(W, H, depth=5, seed=1), hb)
+                m.wait()
+                mine = (np.arange(H) // 8) % world == k
+                assert (out[mine] == full[mine]).all(), k
+                assert (out[~mine] == 7).all(), k
+            m.emulate(0, 0)
+            assert (m.render_frame(cam, W, H, depth=5, seed=1) == full).all()
+    finally:
+        hb.close()
 
 
 @pytest.mark.gpu
