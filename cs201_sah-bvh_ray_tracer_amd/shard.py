@@ -38,11 +38,12 @@ def row_sources(height, row_block, world):
 
 def assemble_gather(slabs, height, row_block):
     """multi.hip deinterleave_kernel, restated: slabs[s] is shard s's
-    (frames, rows_s, W) array (the gathered displays) -> (frames, height, W)."""
+    (frames, rows_s, W, ...) array (the gathered displays) -> (frames,
+    height, W, ...)."""
     world = len(slabs)
     src, pos = row_sources(height, row_block, world)
-    frames, width = slabs[0].shape[0], slabs[0].shape[2]
-    out = np.empty((frames, height, width), slabs[0].dtype)
+    frames = slabs[0].shape[0]
+    out = np.empty((frames, height) + slabs[0].shape[2:], slabs[0].dtype)
     for y in range(height):
         out[:, y] = slabs[src[y]][:, pos[y]]
     return out
@@ -54,8 +55,9 @@ def assemble_direct(slabs, height, row_block):
     pixels, destination pitch world * row_block rows) and the image's short
     last block, if it is s's, after them -> (frames, height, W)."""
     world = len(slabs)
-    frames, width = slabs[0].shape[0], slabs[0].shape[2]
-    out = np.zeros((frames, height, width), slabs[0].dtype)
+    frames = slabs[0].shape[0]
+    out = np.zeros((frames, height) + slabs[0].shape[2:], slabs[0].dtype)
+    width = int(np.prod(slabs[0].shape[2:]))     # elements per image row (pixels x channels)
     blocks = (height + row_block - 1) // row_block
     last = blocks - 1
     flat = out.reshape(frames, -1)
