@@ -514,7 +514,12 @@ def plan(f0, steps, per):
 def run_launches(m, cam, launches, bufs, depth, accumulate=False, tail=(), device_only=False):
     """Enqueue every launch (on lane m.launches % lanes, frame j into
     bufs[lane][j]; device_only: the frames stay on the devices)."""
+    seq = []
     for f0, k in launches:
+        # the display loop's first frame is fresh, a launch of its own
+        # (several frames with accumulate = 0 are successive FRESH frames)
+        seq += [(0, 1), (1, k - 1)] if accumulate and f0 == 0 and k > 1 else [(f0, k)]
+    for f0, k in seq:
         lane = m.launches % m.lanes
         outs = None if device_only else bufs[lane][:k]
         m.render_frames_async(cam, frame_desc_for(f0, k, depth, accumulate), outs, nframes=k, full_grid=f0 in tail)

@@ -1009,8 +1009,12 @@ def test_bench_launch_plan_displays(gpu, mirt, batch, accumulate, direct):
         with mirt.MultiRenderer([0], lanes=4, host_direct=direct) as m:
             m.upload(s, b)
             assert m.delivery == ("host-direct" if direct else "gather")
-            for f0 in range(0, F, batch):
-                k = min(batch, F - f0)
+            # launches of `batch` frames; the display loop's first frame is a
+            # fresh frame of its own (accumulate = 0 with several frames means
+            # successive FRESH frames)
+            starts = ([0] + list(range(1, F, batch))) if accumulate else list(range(0, F, batch))
+            for i, f0 in enumerate(starts):
+                k = (starts[i + 1] if i + 1 < len(starts) else F) - f0
                 acc = accumulate and f0 > 0
                 fd = mirt.frame_desc(W, H, depth=5, seed=1, sample=f0, accumulate=acc, frames=f0 + 1 if acc else 1)
                 m.render_frames_async(cam, fd, bufs[f0:f0 + k], full_grid=f0 + k >= F)
