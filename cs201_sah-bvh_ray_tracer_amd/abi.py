@@ -200,4 +200,4 @@ OPT_QUEUE_ORDER, OPT_DEBUG_STALL_MS = 18, 19
 TRAV_TILE, TRAV_WAVEFRONT = 0, 5
 MULTI_COPY, MULTI_HOST_DIRECT = 1, 2
 MULTI_FULL_GRID = 1
-MULTI_OPT_TIMEOUT_MS, MULTI_OPT_EMULATE_WORLD, MULTI_OPT_EMULATE_RANK = 256, 257, 258
+MULTI_OPT_TIMEOUT_MS, MULTI_OPT_EMULATE_WORLD, MULTI_OPT_EMULATE_RANK, MULTI_OPT_DIRECT_COPY = 256, 257, 258, 259

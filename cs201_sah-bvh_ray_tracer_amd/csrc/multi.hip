@@ -34,20 +34,21 @@ namespace {
 
 constexpr int kMaxShards = 64;  // shards of one frame (ranks, or the emulated world)
 
-// Rows of every shard (kernel argument of deinterleave_kernel).
-struct ShardRows {
+// Where every shard's displays are (kernel argument of deinterleave_kernel):
+// shard s's `nframes` displays at p[s], frame j at + j * rows[s] * width --
+// rank 0's own slabs in place, the other shards' in the gather buffer.
+struct ShardSrc {
+    const uint32_t* p[kMaxShards];
     int rows[kMaxShards];
 };
 
-// The gathered slabs -> the row-major frames. Shard s's `nframes` displays
-// lie at gathered + s * shard_stride, frame j at + j * rows[s] * width. Image
-// row y lies in row block b = y / rb, which shard b % n rendered as its
-// compact row (b / n) * rb + y % rb (host_scene.cpp shard_row_count's
-// geometry). One thread per pixel, rows across blockIdx.y, frames across
-// blockIdx.z: both sides are coalesced row segments.
-__global__ void __launch_bounds__(256) deinterleave_kernel(const uint32_t* __restrict__ gathered,
-                                                           uint32_t* __restrict__ frames, int width, int height,
-                                                           int rb, int n, size_t shard_stride, ShardRows sr)
+// The shards' slabs -> the row-major frames. Image row y lies in row block
+// b = y / rb, which shard b % n rendered as its compact row (b / n) * rb +
+// y % rb (host_scene.cpp shard_row_count's geometry). One thread per pixel,
+// rows across blockIdx.y, frames across blockIdx.z: both sides are coalesced
+// row segments.
+__global__ void __launch_bounds__(256) deinterleave_kernel(ShardSrc src, uint32_t* __restrict__ frames, int width,
+                                                           int height, int rb, int n)
 {
     const int x = blockIdx.x * 256 + threadIdx.x;
     const int y = blockIdx.y;
@@ -56,8 +57,7 @@ __global__ void __launch_bounds__(256) deinterleave_kernel(const uint32_t* __res
     const int b = y / rb;
     const int s = b % n;
     const size_t row = (size_t)(b / n) * rb + y % rb;
-    frames[((size_t)j * height + y) * width + x] =
-        gathered[(size_t)s * shard_stride + ((size_t)j * sr.rows[s] + row) * width + x];
+    frames[((size_t)j * height + y) * width + x] = src.p[s][((size_t)j * src.rows[s] + row) * width + x];
 }
 
 int hip_err(hipError_t e, const char* what)
@@ -134,6 +134,7 @@ struct mirt_multi {
     int next = 0;
     int timeout_ms = 60000;           // MIRT_MULTI_OPT_TIMEOUT_MS (0: unbounded)
     int emu_world = 0, emu_rank = 0;  // MIRT_MULTI_OPT_EMULATE_*: this one rank plays shard emu_rank of emu_world
+    int direct_copy = 0;              // MIRT_MULTI_OPT_DIRECT_COPY: 0 one strided copy per frame, 1 one per row block
     bool failed = false;              // a wait timed out or a device call failed: every call returns fail_msg
     std::string fail_msg;
 };
@@ -235,7 +236,7 @@ int enqueue(mirt_multi* m, Lane& L, const mirt_camera* cam, const mirt_frame_des
     sd.num_shards = world;
     sd.samples = spp * nframes;
     const int rb = sd.row_block;
-    ShardRows sr{};
+    ShardSrc sr{};
     for (int s = 0; s < world; s++) {
         sd.shard = s;
         sr.rows[s] = shard_row_count(&sd);
@@ -244,9 +245,9 @@ int enqueue(mirt_multi* m, Lane& L, const mirt_camera* cam, const mirt_frame_des
     const size_t shard_stride = slab_elems * nframes;           // gathered: shard s's displays
     const size_t frame_elems = (size_t)W * H;
     const int dev0 = m->dev[0];
-    const bool gather = !m->direct || !outs;                    // frames to device 0
+    const bool gather = !m->direct;                             // frames to device 0
     const bool rank0_assembles = gather && (!emu || m->emu_rank == 0);
-    if (gather) {
+    if (gather && world > 1) {
         int rc = grow(dev0, &L.gathered, &L.gathered_cap, 4 * shard_stride * world + 4);
         if (!rc && world > 1 && rank0_assembles) rc = grow(dev0, &L.frame, &L.frame_cap, 4 * frame_elems * nframes + 4);
         if (rc) return rc;
@@ -299,14 +300,18 @@ int enqueue(mirt_multi* m, Lane& L, const mirt_camera* cam, const mirt_frame_des
     }
     hipStream_t s0 = stream_of(L.ctx[0]);
     if (gather) {
-        if (m->rccl) {
-            // one group: every rank (rank 0 included, a self send/recv, so
-            // every slab takes one path) sends its displays to rank 0, which
+        // rank 0's own displays stay where it rendered them; the other
+        // shards' land in the gather buffer
+        sr.p[shard[0]] = src[0];
+        for (int s = 0; s < world; s++)
+            if (s != shard[0]) sr.p[s] = L.gathered + (size_t)s * shard_stride;
+        if (m->rccl && (n > 1 || (emu && m->emu_rank > 0))) {
+            // one group: every other rank sends its displays to rank 0, which
             // receives shard s at gathered + s * shard_stride; each op on the
             // stream that rendered it, so it starts when that rank's frames
-            // are done
+            // are done. (Emulated rank k > 0: its send, as a send to itself.)
             MNCCL(ncclGroupStart());
-            for (int r = 0; r < n; r++) {
+            for (int r = n > 1 ? 1 : 0; r < n; r++) {
                 ncclResult_t e = ncclSend(src[r], cnt[r], ncclUint32, 0, m->comm[r], stream_of(L.ctx[r]));
                 if (e == ncclSuccess)
                     e = ncclRecv(L.gathered + (size_t)shard[r] * shard_stride, cnt[r], ncclUint32, r, m->comm[0], s0);
@@ -316,40 +321,37 @@ int enqueue(mirt_multi* m, Lane& L, const mirt_camera* cam, const mirt_frame_des
                 }
             }
             MNCCL(ncclGroupEnd());
-        } else {
+        } else if (!m->rccl) {
             // copy mode: rank 0's stream waits for each rank's frames, then
             // copies its slabs (peer-to-peer across devices, device-local
             // otherwise)
-            for (int r = 0; r < n; r++) {
-                if (r > 0) {
-                    MHIP(hipSetDevice(m->dev[r]));
-                    MHIP(hipEventRecord(L.rendered[r], stream_of(L.ctx[r])));
-                    MHIP(hipSetDevice(dev0));
-                    MHIP(hipStreamWaitEvent(s0, L.rendered[r], 0));
-                }
+            for (int r = 1; r < n; r++) {
+                MHIP(hipSetDevice(m->dev[r]));
+                MHIP(hipEventRecord(L.rendered[r], stream_of(L.ctx[r])));
                 MHIP(hipSetDevice(dev0));
-                uint32_t* dst = L.gathered + (size_t)shard[r] * shard_stride;
+                MHIP(hipStreamWaitEvent(s0, L.rendered[r], 0));
+                uint32_t* to = L.gathered + (size_t)shard[r] * shard_stride;
                 if (m->dev[r] == dev0)
-                    MHIP(hipMemcpyAsync(dst, src[r], 4 * cnt[r], hipMemcpyDeviceToDevice, s0));
+                    MHIP(hipMemcpyAsync(to, src[r], 4 * cnt[r], hipMemcpyDeviceToDevice, s0));
                 else
-                    MHIP(hipMemcpyPeerAsync(dst, dev0, src[r], m->dev[r], 4 * cnt[r], s0));
+                    MHIP(hipMemcpyPeerAsync(to, dev0, src[r], m->dev[r], 4 * cnt[r], s0));
             }
         }
         MHIP(hipSetDevice(dev0));
         if (emu && m->emu_rank == 0) {
             // emulated rank 0 of a `world`-rank job: the other shards' slabs
-            // arrive too (HBM writes of the receives; the xGMI wire time is
-            // not modelled), copied from this rank's own
+            // arrive too (HBM writes of the receives; the xGMI wire time and
+            // the receive kernels are not modelled), copied from its own
             for (int s = 1; s < world; s++)
                 MHIP(hipMemcpyAsync(L.gathered + (size_t)s * shard_stride, src[0],
                                     4 * std::min(cnt[0], (size_t)sr.rows[s] * W * nframes), hipMemcpyDeviceToDevice,
                                     s0));
         }
         if (rank0_assembles) {
-            const uint32_t* frames = L.gathered;   // one shard: its displays are the frames
+            const uint32_t* frames = src[0];   // one shard: its displays are the frames
             if (world > 1) {
                 const dim3 grid((W + 255) / 256, H, nframes);
-                deinterleave_kernel<<<grid, 256, 0, s0>>>(L.gathered, L.frame, W, H, rb, world, shard_stride, sr);
+                deinterleave_kernel<<<grid, 256, 0, s0>>>(sr, L.frame, W, H, rb, world);
                 MHIP(hipGetLastError());
                 frames = L.frame;
             }
@@ -358,7 +360,7 @@ int enqueue(mirt_multi* m, Lane& L, const mirt_camera* cam, const mirt_frame_des
                     MHIP(hipMemcpyAsync(dst[j], frames + (size_t)j * frame_elems, 4 * frame_elems,
                                         hipMemcpyDeviceToHost, s0));
         }
-    } else {
+    } else if (outs) {
         // host-direct: rank r's row blocks of frame j straight into outs[j]:
         // its full blocks b = s, s + world, ... as one strided copy (rows of
         // rb * W pixels, the destination pitch world * rb rows), the image's
@@ -376,9 +378,12 @@ int enqueue(mirt_multi* m, Lane& L, const mirt_camera* cam, const mirt_frame_des
             for (int j = 0; j < nframes; j++) {
                 const uint32_t* sj = src[r] + (size_t)j * elems;
                 uint32_t* dj = (uint32_t*)dst[j];
-                if (nfull > 0)
+                if (nfull > 0 && m->direct_copy == 0)
                     MHIP(hipMemcpy2DAsync(dj + (size_t)s * rb * W, (size_t)world * rb * W * 4, sj, (size_t)rb * W * 4,
                                           (size_t)rb * W * 4, nfull, hipMemcpyDeviceToHost, stream_of(L.ctx[r])));
+                for (int i = 0; m->direct_copy == 1 && i < nfull; i++)   // one copy per row block
+                    MHIP(hipMemcpyAsync(dj + ((size_t)i * world + s) * rb * W, sj + (size_t)i * rb * W,
+                                        (size_t)rb * W * 4, hipMemcpyDeviceToHost, stream_of(L.ctx[r])));
                 if (has_short)
                     MHIP(hipMemcpyAsync(dj + (size_t)last * rb * W, sj + (size_t)nfull * rb * W,
                                         (size_t)(H - last * rb) * W * 4, hipMemcpyDeviceToHost, stream_of(L.ctx[r])));
@@ -573,6 +578,10 @@ int mirt_multi_set_option(mirt_multi* m, int option, int value)
         m->emu_world = value;
         if (m->emu_rank >= std::max(1, value)) m->emu_rank = 0;
         return MIRT_OK;
+    case MIRT_MULTI_OPT_DIRECT_COPY:
+        if (value < 0 || value > 1) break;
+        m->direct_copy = value;
+        return MIRT_OK;
     case MIRT_MULTI_OPT_EMULATE_RANK:
         if (value < 0 || value >= std::max(1, m->emu_world)) break;
         for (int l = 0; l < (int)m->lanes.size(); l++)
@@ -595,6 +604,7 @@ int mirt_multi_get_option(mirt_multi* m, int option)
     if (option == MIRT_MULTI_OPT_TIMEOUT_MS) return m->timeout_ms;
     if (option == MIRT_MULTI_OPT_EMULATE_WORLD) return m->emu_world;
     if (option == MIRT_MULTI_OPT_EMULATE_RANK) return m->emu_rank;
+    if (option == MIRT_MULTI_OPT_DIRECT_COPY) return m->direct_copy;
     return mirt_get_option(m->lanes[0].ctx[0], option);
 }
 

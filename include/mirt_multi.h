@@ -83,7 +83,9 @@ enum {
                                             render, its send, and as rank 0 also the other shards'
                                             receives, the de-interleave and the frame's D2H; the frames
                                             delivered are NOT complete. 0 or 1 = off (default) */
-    MIRT_MULTI_OPT_EMULATE_RANK = 258
+    MIRT_MULTI_OPT_EMULATE_RANK = 258,
+    MIRT_MULTI_OPT_DIRECT_COPY = 259     /* MIRT_MULTI_HOST_DIRECT: each rank's blocks of a frame as one strided
+                                            copy (hipMemcpy2DAsync, 0, default) or one copy per row block (1) */
 };
 
 /* n ranks on devices[0..n-1] (NULL: devices 0..n-1; n <= 64), `lanes` launches in

@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--accumulate", action="store_true")
     ap.add_argument("--opt", action="append", default=[])
     ap.add_argument("--hw-queues", type=int, default=16)
+    ap.add_argument("--device-only", action="store_true", help="frames left on the devices (no delivery to host)")
+    ap.add_argument("--direct-copy", type=int, default=0, help="MIRT_MULTI_OPT_DIRECT_COPY for host-direct")
     a = ap.parse_args()
     if a.hw_queues and int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < a.hw_queues:
         os.environ["GPU_MAX_HW_QUEUES"] = str(a.hw_queues)   # before the first HIP call of this process
@@ -58,6 +60,7 @@ def main():
     for world in (int(w) for w in a.worlds.split(",")):
         lanes, per, tail_n, blocks = bench.schedule(a, world)
         m = bench.open_multi(1, lanes, a.delivery == "host-direct", spheres, bvh, blocks, a.opt)
+        m.set_option(mirt.abi.MULTI_OPT_DIRECT_COPY, a.direct_copy)
         bufs = bench.host_bufs(lanes, per)
         timed = bench.plan(a.warmup, a.steps, per)
         tail = bench.tail_of(timed, tail_n, lanes, blocks)
@@ -67,14 +70,15 @@ def main():
             best = None
             for _ in range(a.rounds):
                 el = bench.timed_loop(m, cam, bench.plan(0, a.warmup, per), timed, bufs, bench.DEPTH, a.accumulate,
-                                      tail)
+                                      tail, device_only=a.device_only)
                 best = el if best is None else min(best, el)
             per_rank.append(best)
         m.close()
         bench.close_bufs(bufs)
         slow = max(per_rank)
         print(json.dumps({
-            "workload": a.workload, "delivery": a.delivery, "world": world, "steps": a.steps, "warmup": a.warmup,
+            "workload": a.workload, "delivery": "device-only" if a.device_only else a.delivery,
+            "direct_copy": a.direct_copy, "world": world, "steps": a.steps, "warmup": a.warmup,
             "lanes": lanes, "frames_per_launch": per, "tail_grid": len(tail), "bounce_blocks": blocks,
             "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
             "rank_ms_per_frame": [round(t / a.steps * 1e3, 4) for t in per_rank],
