@@ -306,6 +306,14 @@ int enqueue(mirt_multi* m, Lane& L, const mirt_camera* cam, const mirt_frame_des
         for (int s = 0; s < world; s++)
             if (s != shard[0]) sr.p[s] = L.gathered + (size_t)s * shard_stride;
         if (m->rccl && (n > 1 || (emu && m->emu_rank > 0))) {
+            if (m->comm.empty()) {
+                m->comm.assign(n, nullptr);
+                ncclResult_t e = ncclCommInitAll(m->comm.data(), n, m->dev.data());
+                if (e != ncclSuccess) {
+                    m->comm.clear();
+                    return nccl_err(e, "mirt_multi_render_frames_async: ncclCommInitAll");
+                }
+            }
             // one group: every other rank sends its displays to rank 0, which
             // receives shard s at gathered + s * shard_stride; each op on the
             // stream that rendered it, so it starts when that rank's frames
@@ -464,12 +472,10 @@ try {
         return rc;
     };
     if (m->rccl) {
-        m->comm.assign(n, nullptr);
-        ncclResult_t e = ncclCommInitAll(m->comm.data(), n, m->dev.data());
-        if (e != ncclSuccess) {
-            m->comm.clear();
-            return fail(nccl_err(e, "mirt_multi_create: ncclCommInitAll"));
-        }
+        // communicators: at the first launch that exchanges anything (never
+        // for one rank, whose slab is its frame), after the contexts' streams
+        // exist -- RCCL's own streams created first would share the lanes'
+        // hardware queues (GPU_MAX_HW_QUEUES is 4 by default)
     } else {
         // copy mode across distinct devices: direct peer copies where the
         // link allows (the runtime stages them otherwise)
