@@ -1477,7 +1477,7 @@ uint32_t live_node(const mirt_node* nd, uint32_t ci, int ns)
 // reference's trees, whose build partitions the array in place) and the
 // inner depth must leave the packet walk's stack (one entry per level)
 // within 64.
-bool build_pnodes(const mirt_node* nd, int nn, int ns, std::vector<PNode>& pn)
+bool build_pnodes(const mirt_node* nd, int nn, const mirt_sphere* sp, int ns, std::vector<PNode>& pn)
 {
     std::vector<uint32_t> pidx((size_t)nn, kPNone);
     uint32_t np = 1;
@@ -1501,10 +1501,22 @@ bool build_pnodes(const mirt_node* nd, int nn, int ns, std::vector<PNode>& pn)
         if (n.skip & MIRT_NODE_EMPTY) {
             ref = kPNone;  // a 0-sphere leaf: passes, never hits
         } else if (n.sphere >= 0) {
-            if (n.sphere >= ns) {
+            if (n.sphere >= ns || (uint32_t)n.sphere > kPIndex) {
                 ref = kPNone;
             } else {
                 ref = kPLeaf | (uint32_t)n.sphere;
+                // the box is exactly the sphere's (bvh.c:26-35, float, no
+                // contraction: this file is built -ffp-contract=off): store
+                // the sphere, the walk recomputes the box bit for bit
+                const mirt_sphere& q = sp[n.sphere];
+                const float lo[3] = {q.center.x - q.radius, q.center.y - q.radius, q.center.z - q.radius};
+                const float hi[3] = {q.center.x + q.radius, q.center.y + q.radius, q.center.z + q.radius};
+                if (MIRT_PNODE_INLINE && std::memcmp(lo, n.bmin, sizeof lo) == 0 &&
+                    std::memcmp(hi, n.bmax, sizeof hi) == 0) {
+                    const float g[6] = {q.center.x, q.center.y, q.center.z, q.radius, 0.0f, 0.0f};
+                    std::memcpy(slot, g, sizeof g);
+                    ref |= kPInline;
+                }
             }
         }
         (k ? p.ref1 : p.ref0) = ref;
@@ -2059,7 +2071,7 @@ try {
     HIP_TRY(hipMemcpy(c->d_geo, geo.data(), sizeof(float4) * geo.size(), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_color, col.data(), sizeof(uint32_t) * col.size(), hipMemcpyHostToDevice));
     std::vector<PNode> pn;
-    const bool ordered = build_pnodes(nodes, nn, ns, pn);
+    const bool ordered = build_pnodes(nodes, nn, spheres, ns, pn);
     HIP_TRY(hipMalloc((void**)&c->d_pnodes, sizeof(PNode) * pn.size()));
     HIP_TRY(hipMemcpy(c->d_pnodes, pn.data(), sizeof(PNode) * pn.size(), hipMemcpyHostToDevice));
     std::vector<HNode> hn;

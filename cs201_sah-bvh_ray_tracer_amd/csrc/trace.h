@@ -50,6 +50,16 @@ static_assert(sizeof(DNode) == 64, "device node is 64 B");
 // without a stack.
 constexpr uint32_t kPLeaf = 0x80000000u;
 constexpr uint32_t kPNone = 0xffffffffu;
+// MIRT_PNODE_INLINE: a leaf slot whose box is exactly its one sphere's
+// fl(c -+ r) (bvh.c:26-35 create_aabb_from_sphere; every 1-sphere leaf of the
+// reference's builds) holds the SPHERE instead (c.x, c.y, c.z, r) and its ref
+// carries kPInline: the walk recomputes the box with the same roundings and
+// has the sphere without a second dependent load.
+#ifndef MIRT_PNODE_INLINE
+#define MIRT_PNODE_INLINE 1
+#endif
+constexpr uint32_t kPInline = 0x40000000u;
+constexpr uint32_t kPIndex = 0x3fffffffu;
 struct __attribute__((aligned(64))) PNode {
     float c0[6];
     float c1[6];
@@ -816,9 +826,16 @@ __device__ __forceinline__ bool visit_child(const DevScene& sc, const SlabRay& s
     if (ref == kPNone) return false;
     if (ref & kPLeaf) {
         if (COUNT) cnt.nodes++;
-        if (slab_box<FAST>(sr, pr, s0, s1, s2, s3, s4, s5, near)) {
+        const int si = (int)(ref & kPIndex);
+        if (MIRT_PNODE_INLINE && (ref & kPInline)) {
+            // the sphere inline: its box as bvh.c:26-35 computes it
+            if (slab_box<FAST>(sr, pr, s0 - s3, s1 - s3, s2 - s3, s0 + s3, s1 + s3, s2 + s3, near)) {
+                if (COUNT) cnt.spheres++;
+                consider_sphere<FAST>(sc, sp, pr, sr.ox, sr.oy, sr.oz, si, make_float4(s0, s1, s2, s3), best_t,
+                                      best_s);
+            }
+        } else if (slab_box<FAST>(sr, pr, s0, s1, s2, s3, s4, s5, near)) {
             if (COUNT) cnt.spheres++;
-            const int si = (int)(ref & ~kPLeaf);
             consider_sphere<FAST>(sc, sp, pr, sr.ox, sr.oy, sr.oz, si, sc.geo[si], best_t, best_s);
         }
         return false;

@@ -56,7 +56,8 @@ def main():
             b_ms = rl.get("bounce_launch_ms_under_overlap", rl.get("kernel_ms"))
             p_ms = rl.get("primary_launch_ms_under_overlap", rl.get("primary_kernel_ms"))
             res[lib].append((d["value"], b_ms, p_ms, sl["frame_ms"], d["depth1_mrays_s"]))
-            print(json.dumps({"lib": lib, "value": d["value"], "bounce_ms": b_ms,
+            print(json.dumps({"lib": lib, "value": d["value"], "device_resident": d.get("device_resident_mrays_s"),
+                              "bounce_ms": b_ms,
                               "primary_ms": p_ms, "frame_ms": sl["frame_ms"],
                               "serial_bounce_ms": sl.get("bounce_ms"), "serial_primary_ms": sl.get("primary_ms"),
                               "depth1": d["depth1_mrays_s"]}), flush=True)
