@@ -312,7 +312,14 @@ mirt_hit_record mirt_ray_bvh_intersect(mirt_ray ray, mirt_bvh_node* node)
         // the scene bound by the last trace_ray (or this call), if the tree
         // is still the same (pointer and content, read through `node` only:
         // the stored sphere pointer may belong to a freed array)
-        if (!(s.bound && s.root == node && s.tree_fp == tree_fingerprint(node))) {
+        // (and its leaves still point into the bound array: a tree rebuilt
+        // at the same address with the same content over a RELOCATED array
+        // fingerprints the same, but its hit records must point into the
+        // new array -- one leaf, reached through the current tree, tells)
+        const mirt_bvh_node* leaf = node;
+        while (leaf && !leaf->sphere) leaf = leaf->left ? leaf->left : leaf->right;
+        const bool same_array = leaf && leaf->sphere >= s.spheres && leaf->sphere <= s.spheres + s.num_spheres;
+        if (!(s.bound && s.root == node && same_array && s.tree_fp == tree_fingerprint(node))) {
             // a tree seen without its sphere array: the leaves span it, or
             // the array the caller declared (mirt_dropin_scene) holds them
             const mirt_sphere* lo = nullptr;
