@@ -6,6 +6,7 @@
 // an L2-resident tree).
 //   hipcc -O3 --offload-arch=gfx950 scripts/td_probe.hip -o scripts/td_probe
 //   ./scripts/td_probe > profiles/r04_td_probe.json   (one JSON object)
+//   ./scripts/td_probe --mix                          (the walk's access mix, below)
 // Shapes:
 //   lines L (1..64): L lanes of each wave active, each reading its own
 //     64-B node as four dwordx4 (the bounce walk's HNode visit) -> L distinct
@@ -39,8 +40,91 @@ __global__ void __launch_bounds__(256) probe(const uint4* __restrict__ tab, uint
     if (acc == 0x12345678u) out[0] = acc;   // keeps the loads; never true for the table's contents
 }
 
-int main()
+// Round 5: the bounce walk's access MIX, to explain why
+// its TD is 44% busy at 19% of the independent-gather peak. Each lane walks
+// `iters` nodes; a visit is the same four dwordx4 as above, but
+//   dep = 1: the next node index is computed from the loaded data (a chain of
+//            dependent gathers, as a walk's next node comes from its node),
+//   cold:   a fraction cold/256 of the visits go to a 256 MB table (L2 and
+//            MALL misses, as the 13% of the kernel's requests that miss L2),
+//   waves:  occupancy forced down by dynamic LDS (5 per SIMD as the kernel).
+__global__ void __launch_bounds__(256) probe_mix(const uint4* __restrict__ hot, const uint4* __restrict__ cold,
+                                                 uint32_t hot_mask, uint32_t cold_mask, int active, int dep,
+                                                 uint32_t cold256, int iters, uint32_t* __restrict__ out)
 {
+    extern __shared__ uint32_t pad[];
+    const uint32_t lane = threadIdx.x & 63;
+    if ((int)lane >= active) return;
+    uint32_t x = blockIdx.x * 977u + threadIdx.x * 131u + 1u;
+    uint32_t acc = 0;
+    for (int i = 0; i < iters; i++) {
+        const uint32_t h = (x + (uint32_t)i * 7919u) * 2654435761u;
+        const bool is_cold = ((h >> 24) & 0xffu) < cold256;
+        const uint4* p = is_cold ? cold + 4 * ((h >> 4) & cold_mask) : hot + 4 * ((h >> 8) & hot_mask);
+        const uint4 a = p[0], b = p[1], c = p[2], d = p[3];
+        const uint32_t v = (a.x ^ a.y ^ a.z ^ a.w) + (b.x ^ b.y ^ b.z ^ b.w) + (c.x ^ c.y ^ c.z ^ c.w) +
+                           (d.x ^ d.y ^ d.z ^ d.w);
+        acc += v;
+        if (dep) x ^= v;   // the next address depends on this node's data
+    }
+    if (acc == 0x12345678u) out[0] = acc + pad[0];
+}
+
+int mix_main()
+{
+    const uint32_t hot_nodes = 1u << 14, cold_nodes = 1u << 22;   // 1 MB / 256 MB
+    uint4 *hot = nullptr, *cold = nullptr;
+    uint32_t* out = nullptr;
+    if (hipMalloc(&hot, sizeof(uint4) * 4 * hot_nodes) != hipSuccess ||
+        hipMalloc(&cold, sizeof(uint4) * 4 * (size_t)cold_nodes) != hipSuccess || hipMalloc(&out, 4) != hipSuccess)
+        return 1;
+    (void)hipMemset(hot, 0, sizeof(uint4) * 4 * hot_nodes);     // zero data: a dependent chain stays a hash walk
+    (void)hipMemset(cold, 0, sizeof(uint4) * 4 * (size_t)cold_nodes);
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    int cus = 0, clk_khz = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    (void)hipDeviceGetAttribute(&clk_khz, hipDeviceAttributeClockRate, 0);
+    const int blocks = 2048, threads = 256, iters = 256;
+    printf("{\"probe\": \"scripts/td_probe.hip --mix\", \"cus\": %d, \"clock_khz\": %d, \"cases\": [", cus, clk_khz);
+    struct Case { int active, dep, cold256, waves; };
+    const Case cases[] = {{20, 0, 0, 8}, {20, 1, 0, 8}, {20, 1, 0, 5}, {20, 0, 33, 8}, {20, 1, 33, 5}, {20, 1, 33, 8},
+                          {64, 1, 0, 5}, {64, 0, 0, 8}};
+    bool first = true;
+    for (const Case& c : cases) {
+        // dynamic LDS sized so that only c.waves waves (workgroups / 4 x 4 SIMDs) fit a CU's 160 KB
+        const size_t lds = c.waves >= 8 ? 0 : (160 * 1024) / (size_t)c.waves - 256;
+        float best = 1e30f;
+        for (int rep = 0; rep < 3; rep++) {
+            probe_mix<<<blocks, threads, lds>>>(hot, cold, hot_nodes - 1, cold_nodes - 1, c.active, c.dep, c.cold256,
+                                                iters, out);
+            (void)hipEventRecord(e0);
+            probe_mix<<<blocks, threads, lds>>>(hot, cold, hot_nodes - 1, cold_nodes - 1, c.active, c.dep, c.cold256,
+                                                iters, out);
+            (void)hipEventRecord(e1);
+            (void)hipEventSynchronize(e1);
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, e0, e1);
+            if (ms < best) best = ms;
+        }
+        const double inst = (double)blocks * (threads / 64) * iters * 4;
+        printf("%s\n  {\"active_lanes\": %d, \"dependent\": %d, \"cold_frac\": %.3f, \"waves_per_simd\": %d, "
+               "\"lds_bytes\": %zu, \"ms\": %.4f, \"wave_load_instructions\": %.0f, \"ginst_per_s\": %.3f}",
+               first ? "" : ",", c.active, c.dep, c.cold256 / 256.0, c.waves, lds, best, inst,
+               inst / (best * 1e-3) / 1e9);
+        first = false;
+    }
+    printf("\n]}\n");
+    (void)hipFree(hot);
+    (void)hipFree(cold);
+    (void)hipFree(out);
+    return 0;
+}
+
+int main(int argc, char** argv)
+{
+    if (argc > 1 && argv[1][0] == '-' && argv[1][1] == '-' && argv[1][2] == 'm') return mix_main();
     const uint32_t nodes = 1u << 14;  // 16k x 64 B = 1 MB: L2-resident (the 10k scene's four-wide tree: 0.7 MB)
     uint4* tab = nullptr;
     uint32_t* out = nullptr;
