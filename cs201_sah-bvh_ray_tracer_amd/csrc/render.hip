@@ -638,6 +638,75 @@ __device__ __forceinline__ void solo_chain(const DevScene& sc, const FrameConst&
     }
 }
 
+// Continuation queue (lone frames: the blocking call; MIRT_OPT_CONT_QUEUE).
+// Once a frame's first-bounce queue is dry, its remaining chains sit in the
+// waves that drew them, and the waves that finished early would leave the
+// chip while the last chains are walked one lane (or one quad) per ray. With
+// the queue on, waves that run out of chains stay and WAIT, and a wave that
+// still holds several chains hands a chain that goes on to its next level to
+// them (never more than are waiting) as a 64-B record; a waiting wave takes
+// one record and walks that chain with all 16 of its quads (solo_chain), so
+// the tail's chains get the whole chip instead of a lane each. Termination:
+// every wave counts itself a possible pusher until its own chains are done;
+// a waiting wave leaves once no pusher is left and the queue is empty (a
+// pusher's records are published before it stops being one, so none is
+// orphaned). Every wait is bounded (kContSpinTicks of the 100 MHz clock): a
+// wait that runs out sets the error word and gives up (a wrong frame, never
+// a hung grid).
+struct ContRec {                    // one chain at the start of a bounce level
+    float ox, oy, oz, dx, dy, dz;
+    uint32_t pixel, k, base0, level;
+    uint32_t col[6];                // colour stack rows 0 .. level - 2 (levels 1 .. level - 1)
+};
+static_assert(sizeof(ContRec) == 64, "continuation record is 64 B");
+struct ContQ {
+    uint32_t* ctl;    // kCq* words, each in its own 128-B line
+    ContRec* rec;     // cap records (a ring)
+    uint32_t* flag;   // per record slot: 0 free, else the epoch of the record published there
+    uint32_t cap;     // records: the launch's lanes (chains alive after the queue is dry <= lanes)
+};
+constexpr uint32_t kCqHead = 0, kCqTail = 32, kCqPushers = 64, kCqWaiters = 96, kCqError = 128;
+constexpr size_t kCqCtlBytes = 4 * 160;
+constexpr uint64_t kContSpinTicks = 2000000;   // 20 ms of the 100 MHz real-time clock
+
+__device__ __forceinline__ uint32_t cq_load(const uint32_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Pushes the waiting waves would take at once: waiters - records queued.
+__device__ __forceinline__ uint32_t cq_room(const ContQ& q)
+{
+    const uint32_t w = cq_load(q.ctl + kCqWaiters), h = cq_load(q.ctl + kCqHead), t = cq_load(q.ctl + kCqTail);
+    const uint32_t queued = h - t;
+    return w > queued ? w - queued : 0u;
+}
+
+// One lane publishes its chain (ray of level `level`, colours at cs[(l) * cstride]).
+__device__ __forceinline__ void cq_push(const ContQ& q, const Ray& ray, uint32_t pixel, uint32_t k, uint32_t base0,
+                                        int level, const uint32_t* cs, int cstride)
+{
+    const uint32_t idx = atomicAdd(q.ctl + kCqHead, 1u);
+    const uint32_t slot = idx % q.cap, epoch = idx / q.cap + 1u;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (cq_load(q.flag + slot) != 0u) {     // the ring slot's previous record is still being read
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kContSpinTicks) {
+            atomicOr(q.ctl + kCqError, 1u);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    ContRec r;
+    r.ox = ray.ox; r.oy = ray.oy; r.oz = ray.oz; r.dx = ray.dx; r.dy = ray.dy; r.dz = ray.dz;
+    r.pixel = pixel; r.k = k; r.base0 = base0; r.level = (uint32_t)level;
+#pragma unroll
+    for (int l = 0; l < 6; l++) r.col[l] = l < level - 1 ? cs[l * cstride] : 0u;
+    uint4* d = (uint4*)(q.rec + slot);
+    const uint4* v = (const uint4*)&r;
+    d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
+    __hip_atomic_store(q.flag + slot, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Persistent bounce pass: each lane owns one pixel's chain of bounces,
 // refilled from the primary pass's queue. WALK 2 (default) ends with a QUAD
 // DRAIN: once the queue is dry and at most 16 of
@@ -653,12 +722,14 @@ __device__ __forceinline__ void solo_chain(const DevScene& sc, const FrameConst&
 #define MIRT_BOUNCE_WAVES 5
 #endif
 #define MIRT_BOUNCE_ATTR __attribute__((amdgpu_waves_per_eu(MIRT_BOUNCE_WAVES)))
-template <bool FAST, int WALK, bool DIAG = false>
+template <bool FAST, int WALK, bool DIAG = false, bool CQ = false>
 __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
                                                      float* __restrict__ acc, const BounceRec* __restrict__ queue,
                                                      uint32_t* __restrict__ qctl, int threshold, int quad_drain,
-                                                     uint64_t* __restrict__ diag = nullptr)
+                                                     uint64_t* __restrict__ diag = nullptr, ContQ cq = ContQ{})
 {
+    static_assert(!CQ || ((WALK == 2 || WALK == 4) && !DIAG), "the continuation queue rides on the quad drain");
+    if (CQ && (threadIdx.x & 63) == 0) atomicAdd(cq.ctl + kCqPushers, 1u);   // this wave may push
     uint64_t dg_it = 0, dg_lanes = 0, dg_it_x = 0, dg_lanes_x = 0, dg_tx = 0, dg_qit = 0, dg_tq = 0;
     const uint64_t dg_t0 = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
     uint32_t dg_steps = 0, dg_chain = 0, dg_walk_max = 0, dg_chain_max = 0;
@@ -702,6 +773,7 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
     uint32_t pixel = 0, k = 0, base0 = 0;
     int level = 0, best_s = -1;
     float best_t = INFINITY;
+    bool cont = false;   // CQ: this lane's chain just started its next level after the queue ran dry
     for (;;) {
         // refill lanes that own no chain (one atomic per wave, tile order
         // kept), from the next segment while the current one is dry
@@ -783,12 +855,30 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                 best_t = INFINITY;
                 best_s = -1;
                 pr = prune_off();
+                cont = CQ && exhausted;
             } else {
                 has = false;
                 if (DIAG) {
                     dg_chain_max = max(dg_chain_max, dg_chain);
                     dg_chain = 0;
                 }
+            }
+        }
+        if constexpr (CQ) {
+            // chains starting a new level after the queue ran dry: as many as
+            // waves are waiting go to them (the wave keeps at least one)
+            const uint64_t cm = __ballot(cont);
+            if (cm) {
+                const int lead = __builtin_ctzll(cm);
+                uint32_t room = 0;
+                if ((int)(threadIdx.x & 63) == lead) room = cq_room(cq);
+                room = min((uint32_t)__builtin_amdgcn_readlane((int)room, lead),
+                           (uint32_t)__popcll(__ballot(has)) - 1u);
+                if (cont && lanes_below(cm) < room) {
+                    cq_push(cq, ray, pixel, k, base0, level, cs, cstride);
+                    has = false;
+                }
+                cont = false;
             }
         }
     }
@@ -839,6 +929,7 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                 if (has && qw.cur != kPNone)
                     quad_step<FAST, kWideStride, kWideStack>(sc, sr, sp, pr, qw, qstk, best_t, best_s,
                                                              (lds_uint4*)hcache, hc_n);
+                bool qcont = false;
                 if (has && qw.cur == kPNone) {
                     if (shade_level(sc, f, ray, best_t, best_s, level, k, chain_key(f, pixel), qcs, kWideStride, base0, pixel, out,
                                     acc, (lane & 3) == 0)) {
@@ -848,12 +939,101 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                         best_t = INFINITY;
                         best_s = -1;
                         pr = prune_off();
+                        qcont = CQ;
                     } else {
                         has = false;
                     }
                 }
+                if constexpr (CQ) {
+                    // quads whose ray starts its next level hand it to waiting
+                    // waves (quad-uniform decision; the wave keeps one ray)
+                    const uint64_t cm = __ballot(qcont && (lane & 3) == 0);
+                    if (cm) {
+                        const int lead = __builtin_ctzll(cm);
+                        uint32_t room = 0;
+                        if ((int)lane == lead) room = cq_room(cq);
+                        room = min((uint32_t)__builtin_amdgcn_readlane((int)room, lead),
+                                   (uint32_t)__popcll(__ballot(has && (lane & 3) == 0)) - 1u);
+                        const uint32_t qb = lane & ~3u;
+                        const uint32_t qrank = (uint32_t)__popcll(qb ? cm & ((1ull << qb) - 1) : 0ull);
+                        if (qcont && qrank < room) {
+                            if ((lane & 3) == 0) cq_push(cq, ray, pixel, k, base0, level, qcs, kWideStride);
+                            has = false;
+                            qw.cur = kPNone;
+                        }
+                    }
+                }
             }
         }
+    }
+    if constexpr (CQ) {
+        // this wave's own chains are done: no more pushes from it; wait for
+        // records while any wave may still push, walking each with the whole wave
+        const uint32_t lane = threadIdx.x & 63;
+        uint32_t* wst = wstack + (threadIdx.x & ~63u);
+        uint32_t* wcs = cstack + (threadIdx.x & ~63u);
+        if (lane == 0) {
+            __hip_atomic_fetch_add(cq.ctl + kCqWaiters, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(cq.ctl + kCqPushers, ~0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            constexpr uint32_t kNone = ~0u, kExit = ~1u;
+            uint32_t got = kNone;
+            if (lane == 0) {
+                const uint32_t t = cq_load(cq.ctl + kCqTail), h = cq_load(cq.ctl + kCqHead);
+                if (t < h) {
+                    if (atomicCAS(cq.ctl + kCqTail, t, t + 1u) == t) got = t;
+                } else if (cq_load(cq.ctl + kCqPushers) == 0u &&
+                           cq_load(cq.ctl + kCqTail) >= cq_load(cq.ctl + kCqHead)) {
+                    got = kExit;
+                } else if (__builtin_amdgcn_s_memrealtime() - t0 > 25 * kContSpinTicks) {
+                    atomicOr(cq.ctl + kCqError, 2u);   // no pusher ever finished: give up
+                    got = kExit;
+                }
+            }
+            got = (uint32_t)__builtin_amdgcn_readfirstlane((int)got);
+            if (got == kExit) break;
+            if (got == kNone) {
+                __builtin_amdgcn_s_sleep(8);
+                continue;
+            }
+            const uint32_t slot = got % cq.cap, epoch = got / cq.cap + 1u;
+            uint32_t ok = 1;
+            if (lane == 0) {
+                const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
+                __hip_atomic_fetch_add(cq.ctl + kCqWaiters, ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                while (cq_load(cq.flag + slot) != epoch) {
+                    if (__builtin_amdgcn_s_memrealtime() - w0 > kContSpinTicks) {
+                        atomicOr(cq.ctl + kCqError, 4u);
+                        ok = 0;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            ok = (uint32_t)__builtin_amdgcn_readfirstlane((int)ok);
+            if (!ok) break;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            const uint32_t word = lane < 16 ? ((const uint32_t*)(cq.rec + slot))[lane] : 0u;
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) __hip_atomic_store(cq.flag + slot, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            auto wd = [&](int i) { return (uint32_t)__builtin_amdgcn_readlane((int)word, i); };
+            const Ray cr{__uint_as_float(wd(0)), __uint_as_float(wd(1)), __uint_as_float(wd(2)),
+                         __uint_as_float(wd(3)), __uint_as_float(wd(4)), __uint_as_float(wd(5))};
+            const int clevel = (int)wd(9);
+            // the colour stack rows into column 0 (this wave's columns are free)
+            const uint32_t colw = (uint32_t)__shfl((int)word, min(10 + (int)lane, 63));
+            if (lane < 6 && (int)lane < clevel - 1) wcs[lane * kWideStride] = colw;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            solo_chain<FAST>(sc, f, 0, cr, INFINITY, -1, prune_off(), QuadWalk{sc.wide_root, 0u, 0u}, clevel, wd(7),
+                             wd(6), wd(8), 0u, wst, wcs, out, acc, (lds_uint4*)hcache, hc_n);
+            if (lane == 0) __hip_atomic_fetch_add(cq.ctl + kCqWaiters, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            t0 = __builtin_amdgcn_s_memrealtime();
+        }
+        if (lane == 0) __hip_atomic_fetch_add(cq.ctl + kCqWaiters, ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (DIAG) {
         for (int o = 32; o; o >>= 1) {
@@ -1274,6 +1454,10 @@ struct AccumShare {
 #define MIRT_LEAF_BATCH_DEFAULT 2
 #endif
 
+#ifndef MIRT_CONT_QUEUE_DEFAULT
+#define MIRT_CONT_QUEUE_DEFAULT 1
+#endif
+
 struct mirt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -1346,6 +1530,9 @@ struct mirt_ctx {
     size_t keys_cap = 0;
     int num_cus = 0;
     int debug_stall_ms = 0;     // MIRT_OPT_DEBUG_STALL_MS: test hook, each frame starts behind a bounded wait
+    int cont_queue = MIRT_CONT_QUEUE_DEFAULT;  // MIRT_OPT_CONT_QUEUE: 0 off, 1 lone frames, 2 every frame
+    void* d_cq = nullptr;       // continuation queue: control words, records, slot flags
+    size_t cq_bytes = 0;
 };
 
 namespace {
@@ -1876,7 +2063,25 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
             primary_kernel<false, false><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl, octant_queue(c));
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ph1[ps], s));
-        if (d_bdiag && sc.wide)
+        // the continuation queue for a frame alone on the chip
+        const bool cq_on = sc.wide && c->fast_slab && c->quad_drain && !d_bdiag &&
+                           (c->cont_queue == 2 || (c->cont_queue == 1 && c->lone_frame));
+        ContQ cq{};
+        if (cq_on) {
+            cq.cap = (uint32_t)bblocks * 256u;
+            const size_t need = kCqCtlBytes + sizeof(ContRec) * cq.cap + 4 * (size_t)cq.cap;
+            if (int rc2 = ensure(&c->d_cq, &c->cq_bytes, need)) return rc2;
+            cq.ctl = (uint32_t*)c->d_cq;
+            cq.rec = (ContRec*)((char*)c->d_cq + kCqCtlBytes);
+            cq.flag = (uint32_t*)((char*)cq.rec + sizeof(ContRec) * cq.cap);
+            HIP_TRY(hipMemsetAsync(cq.ctl, 0, kCqCtlBytes, s));
+            HIP_TRY(hipMemsetAsync(cq.flag, 0, 4 * (size_t)cq.cap, s));
+        }
+        if (cq_on && leaf_batch(c))
+            bounce_kernel<true, 4, false, true><<<bblocks, 256, blds, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, nullptr, cq);
+        else if (cq_on)
+            bounce_kernel<true, 2, false, true><<<bblocks, 256, blds, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, nullptr, cq);
+        else if (d_bdiag && sc.wide)
             bounce_kernel<true, 2, true><<<bblocks, 256, blds, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, d_bdiag);
         else if (d_bdiag)
             bounce_kernel<true, 0, true><<<bblocks, 256, blds, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, d_bdiag);
@@ -2004,7 +2209,7 @@ void mirt_destroy(mirt_ctx* c)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     accum_release(c->acc);
     for (void* p : {(void*)c->d_nodes, (void*)c->d_nodes32, (void*)c->d_geo, (void*)c->d_color, (void*)c->d_out,
-                    c->d_in, c->d_res, (void*)c->d_counts, (void*)c->d_defer, c->d_queue, (void*)c->d_keys, (void*)c->d_pnodes,
+                    c->d_in, c->d_res, (void*)c->d_counts, (void*)c->d_defer, c->d_queue, c->d_cq, (void*)c->d_keys, (void*)c->d_pnodes,
                     (void*)c->d_hnodes, (void*)c->d_haux, (void*)c->d_leaves, (void*)c->d_ndepth,
                     (void*)c->d_overlay})
         if (p) (void)hipFree(p);
@@ -2794,6 +2999,10 @@ int mirt_set_option(mirt_ctx* c, int option, int value)
         if (value < 0 || value > 2) break;
         c->zero_copy = value;
         return MIRT_OK;
+    case MIRT_OPT_CONT_QUEUE:
+        if (value < 0 || value > 2) break;
+        c->cont_queue = value;
+        return MIRT_OK;
     case MIRT_OPT_DEBUG_STALL_MS:
         if (value < 0 || value > 10000) break;
         c->debug_stall_ms = value;
@@ -2833,6 +3042,7 @@ int mirt_get_option(mirt_ctx* c, int option)
     if (option == MIRT_OPT_ZERO_COPY) return c->zero_copy;
     if (option == MIRT_OPT_QUEUE_ORDER) return c->queue_order;
     if (option == MIRT_OPT_DEBUG_STALL_MS) return c->debug_stall_ms;
+    if (option == MIRT_OPT_CONT_QUEUE) return c->cont_queue;
     if (option == MIRT_OPT_LEAF_BATCH) return leaf_batch(c) ? 1 : 0;  // in effect for the uploaded scene
     set_error("mirt_get_option: bad option %d", option);
     return MIRT_E_INVALID;

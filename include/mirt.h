@@ -424,10 +424,16 @@ enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3,
                                        mirt_render_frame (a frame alone on the chip), grouped by
                                        direction octant per workgroup for frames in flight;
                                        1 = always grouped; 2 = always tile order. Speed only. */
-       MIRT_OPT_DEBUG_STALL_MS = 19 /* test hook: every frame of this context starts behind a
+       MIRT_OPT_DEBUG_STALL_MS = 19, /* test hook: every frame of this context starts behind a
                                        kernel that waits this many ms (0..10000, default 0), then
                                        exits -- a frame that overruns a caller's deadline
-                                       (mirt_multi's MIRT_MULTI_OPT_TIMEOUT_MS) without a hang */ };
+                                       (mirt_multi's MIRT_MULTI_OPT_TIMEOUT_MS) without a hang */
+       MIRT_OPT_CONT_QUEUE = 20     /* wavefront, four-wide bounce walk: once a frame's bounce queue is
+                                       dry, waves out of chains wait and take chains starting their
+                                       next level from waves that still hold several, walking each
+                                       with the whole wave -- 1 (default) for a frame alone on the
+                                       chip (the blocking mirt_render_frame), 2 for every frame, 0
+                                       never. Speed only. */ };
 /* Traversal ids keep their first-release values (mirt 0.1: TILE 0, WAVEFRONT 5).
    ABI note: the mirt 0.2 header numbered WAVEFRONT 1; mirt_set_option accepts
    1 as a deprecated alias of MIRT_TRAV_WAVEFRONT (mirt_get_option reads back
