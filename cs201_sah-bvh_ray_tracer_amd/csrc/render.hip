@@ -668,6 +668,11 @@ struct ContQ {
 constexpr uint32_t kCqHead = 0, kCqTail = 32, kCqPushers = 64, kCqWaiters = 96, kCqError = 128;
 constexpr size_t kCqCtlBytes = 4 * 160;
 constexpr uint64_t kContSpinTicks = 2000000;   // 20 ms of the 100 MHz real-time clock
+// pushes from waves still walking one chain per lane (1), or only from waves
+// in the quad drain (0)
+#ifndef MIRT_CQ_LANE_PUSH
+#define MIRT_CQ_LANE_PUSH 1
+#endif
 
 __device__ __forceinline__ uint32_t cq_load(const uint32_t* p)
 {
@@ -864,7 +869,7 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                 }
             }
         }
-        if constexpr (CQ) {
+        if constexpr (CQ && MIRT_CQ_LANE_PUSH) {
             // chains starting a new level after the queue ran dry: as many as
             // waves are waiting go to them (the wave keeps at least one)
             const uint64_t cm = __ballot(cont);
