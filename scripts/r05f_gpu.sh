@@ -16,6 +16,7 @@ step() {
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
     return $rc
 }
+step ptr_probe 120 python scripts/ptr_query_probe.py
 step pytest_cq 400 python -u -m pytest tests/test_cont_queue.py -m gpu -x -v --timeout 200 --timeout-method thread || exit 1
 step cq_ab 400 python scripts/cq_ab.py --rounds 3
 grep '"best_ms"' $OUT/cq_ab.log
