@@ -10,6 +10,8 @@
 #include <cmath>
 #include <cstdint>
 #include <algorithm>
+#include <map>
+#include <mutex>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -2461,7 +2463,33 @@ uint32_t* host_mapped(const void* p, size_t bytes)
 
 extern "C++" {
 namespace mirt {
-bool host_page_locked(const void* p, size_t bytes) { return host_mapped(p, bytes) != nullptr; }
+// Page-locked ranges this library handed out or registered (mirt_host_alloc /
+// mirt_host_register): checked without a HIP call, which the frame loops of
+// mirt_multi make for every output of every launch.
+static std::mutex g_pin_mu;
+static std::map<uintptr_t, size_t> g_pinned;   // start -> bytes
+void pinned_add(const void* p, size_t bytes)
+{
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    g_pinned[(uintptr_t)p] = bytes;
+}
+void pinned_remove(const void* p)
+{
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    g_pinned.erase((uintptr_t)p);
+}
+bool host_page_locked(const void* p, size_t bytes)
+{
+    {
+        std::lock_guard<std::mutex> lk(g_pin_mu);
+        auto it = g_pinned.upper_bound((uintptr_t)p);
+        if (it != g_pinned.begin()) {
+            --it;
+            if ((uintptr_t)p + bytes <= it->first + it->second) return true;
+        }
+    }
+    return host_mapped(p, bytes) != nullptr;   // pinned by other means (e.g. the caller's hipHostMalloc)
+}
 }  // namespace mirt
 }
 
@@ -2525,12 +2553,15 @@ int mirt_host_alloc(size_t bytes, void** out)
     if (!out) return MIRT_E_INVALID;
     *out = nullptr;
     HIP_TRY(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+    mirt::pinned_add(*out, bytes ? bytes : 1);
     return MIRT_OK;
 }
 
 void mirt_host_free(void* p)
 {
-    if (p) (void)hipHostFree(p);
+    if (!p) return;
+    mirt::pinned_remove(p);
+    (void)hipHostFree(p);
 }
 
 int mirt_host_register(void* p, size_t bytes)
@@ -2540,6 +2571,7 @@ int mirt_host_register(void* p, size_t bytes)
         return MIRT_E_INVALID;
     }
     HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterDefault));
+    mirt::pinned_add(p, bytes);
     return MIRT_OK;
 }
 
@@ -2549,6 +2581,7 @@ int mirt_host_unregister(void* p)
         set_error("mirt_host_unregister: null pointer");
         return MIRT_E_INVALID;
     }
+    mirt::pinned_remove(p);
     HIP_TRY(hipHostUnregister(p));
     return MIRT_OK;
 }
