@@ -11,11 +11,16 @@ Every N runs the C-ABI multi-GPU renderer of include/mirt_multi.h -- the
 path a C caller of main.c's loop uses -- in ONE process:
 mirt_multi_create over devices 0..N-1 (RCCL communicators from
 ncclCommInitAll), the scene replicated, `pipeline` lanes of per-GPU contexts
-keeping launches in flight, and every frame gathered and delivered into
-page-locked host memory. A step is ONE fresh frame (main.c:358-374) split N
-ways by interleaved 8-row blocks ("scaling": "strong"); value = W*H*spp*K /
-the timed region (mirt_multi_wait + wall clock on both sides: every frame of
-the K steps has reached host memory when the clock stops).
+keeping launches in flight, and every frame delivered into page-locked host
+memory. A step is ONE fresh frame (main.c:358-374) split N ways by
+interleaved 8-row blocks ("scaling": "strong"); value = W*H*spp*K / the timed
+region (mirt_multi_wait + wall clock on both sides: every frame of the K
+steps has reached host memory when the clock stops). Delivery (--delivery
+auto): at N = 1 the GPU's slab is the frame (one D2H); at N > 1 every GPU
+copies its row blocks into the host frame over its own link (host-direct),
+and the RCCL gather to GPU 0 is measured beside it, to host memory
+(`value_gather`) and left on GPU 0 (`device_resident_mrays_s`) -- one host
+link cannot carry the frame rate of 8 GPUs at 1080p.
 
 Processes. N = 1 measures in this process. N > 1: this process never
 touches a GPU; it starts ONE fresh child (`--measure-child`) with
@@ -590,22 +595,32 @@ def tail_of(launches, tail, lanes, blocks):
     return {f0 for f0, _ in launches[-tail:]}
 
 
+def last_delivered(m, bufs, launches):
+    """The last frame a timed loop delivered (host copy)."""
+    f0, k = launches[-1]
+    return bufs[(m.launches - 1) % m.lanes][k - 1].array.copy(), (f0 + k - 1) * SPP
+
+
 def measure(args):
-    """The GPU measurement over args.gpus devices in THIS process."""
+    """The GPU measurement over args.gpus devices in THIS process. The
+    headline delivers every frame to page-locked host memory (SURVEY §8(d)
+    t_frame): at N = 1 the rank's slab is the frame (one D2H); at N > 1 by
+    default every GPU copies its row blocks into the host frame (host-direct),
+    and the RCCL gather to GPU 0 is measured beside it -- with the frames
+    then copied to the host (value_gather) and left on GPU 0
+    (device_resident_mrays_s)."""
     n = args.gpus
+    delivery = args.delivery if args.delivery != "auto" else ("gather" if n == 1 else "host-direct")
     lanes, per, tail_n, blocks = schedule(args, n)
     spheres, bvh, build_s = make_scene()
     cam = mirt.default_camera()
-    m = open_multi(n, lanes, args.delivery == "host-direct", spheres, bvh, blocks, args.opt)
+    m = open_multi(n, lanes, delivery == "host-direct", spheres, bvh, blocks, args.opt)
     bufs = host_bufs(lanes, per)
     warm = plan(0, args.warmup, per)
     timed_launches = plan(args.warmup, args.steps, per)
     tail = tail_of(timed_launches, tail_n, lanes, blocks)
     elapsed = timed_loop(m, cam, warm, timed_launches, bufs, DEPTH, args.accumulate, tail)
-    # the last frame delivered must be the frame one context renders alone
-    last_f0, last_k = timed_launches[-1]
-    last_lane = (m.launches - 1) % lanes
-    last_frame = bufs[last_lane][last_k - 1].array.copy()
+    last_frame, last_sample = last_delivered(m, bufs, timed_launches)
     # the passes of rank 0's timed launches (HIP events on each launch's own
     # stream, under the overlap of the lanes in flight)
     phases = []
@@ -614,34 +629,45 @@ def measure(args):
         if k_lane:
             phases += m.phase_log(lane, 0, min(k_lane, 64))
     primary_ms, bounce_ms = (float(v) for v in np.mean(np.array(phases), axis=0)) if phases else (0.0, 0.0)
-    # the same loop with the frames left on the devices (no D2H)
-    el_dev = timed_loop(m, cam, plan(0, 2, per), plan(args.warmup, args.steps, per), bufs, DEPTH, args.accumulate,
-                        tail, device_only=True)
     # depth 1 (camera rays and their shading only), frames to host memory
     el_d1 = timed_loop(m, cam, plan(0, 2, per), plan(args.warmup, args.steps, per), bufs, 1, False, tail)
+    # the same loop with the frames left on the device(s): N = 1 in the
+    # rank's slabs; N > 1 gathered on GPU 0 over RCCL (below)
+    el_dev = None
+    if n == 1:
+        el_dev = timed_loop(m, cam, plan(0, 2, per), plan(args.warmup, args.steps, per), bufs, DEPTH,
+                            args.accumulate, tail, device_only=True)
     m.close()
     close_bufs(bufs)
-    # the last delivered frame against one context rendering the same frame
+    # the other delivery at N > 1: the RCCL gather to GPU 0, to host memory
+    # and device-resident (a second renderer, same schedule)
+    other, other_frame = None, None
+    if n > 1 and not args.no_other:
+        od = "gather" if delivery == "host-direct" else "host-direct"
+        m2 = open_multi(n, lanes, od == "host-direct", spheres, bvh, blocks, args.opt)
+        bufs2 = host_bufs(lanes, per)
+        tl2 = plan(args.warmup, args.steps, per)
+        el2 = timed_loop(m2, cam, plan(0, args.warmup, per), tl2, bufs2, DEPTH, args.accumulate, tail)
+        other_frame = last_delivered(m2, bufs2, tl2)
+        other = {"delivery": od, "mrays_s": round(W * H * SPP * args.steps / el2 / 1e6, 3),
+                 "ms_per_step": round(el2 / args.steps * 1e3, 4)}
+        if od == "gather":
+            el_dev = timed_loop(m2, cam, plan(0, 2, per), plan(args.warmup, args.steps, per), bufs2, DEPTH,
+                                args.accumulate, tail, device_only=True)
+        m2.close()
+        close_bufs(bufs2)
+    # the last delivered frame(s) against one context rendering the same frame
     # alone (the N-GPU frame must equal the one-GPU frame byte for byte)
     same = None
     if not args.accumulate:
         with mirt.Renderer(0) as r1:
             r1.upload(spheres, bvh)
-            one = r1.render_frame(cam, W, H, depth=DEPTH, seed=SEED, sample=(last_f0 + last_k - 1) * SPP,
-                                  samples=SPP, jitter=JITTER)
-        same = frame_sha(one) == frame_sha(last_frame)
-    # the other delivery at N > 1 (a second renderer, same schedule)
-    other = None
-    if n > 1 and not args.no_other:
-        od = "gather" if args.delivery == "host-direct" else "host-direct"
-        m2 = open_multi(n, lanes, od == "host-direct", spheres, bvh, blocks, args.opt)
-        bufs2 = host_bufs(lanes, per)
-        el2 = timed_loop(m2, cam, plan(0, args.warmup, per), plan(args.warmup, args.steps, per), bufs2, DEPTH,
-                         args.accumulate, tail)
-        other = {"delivery": od, "mrays_s": round(W * H * SPP * args.steps / el2 / 1e6, 3),
-                 "ms_per_step": round(el2 / args.steps * 1e3, 4)}
-        m2.close()
-        close_bufs(bufs2)
+            one = r1.render_frame(cam, W, H, depth=DEPTH, seed=SEED, sample=last_sample, samples=SPP, jitter=JITTER)
+            same = frame_sha(one) == frame_sha(last_frame)
+            if other_frame is not None:
+                one2 = r1.render_frame(cam, W, H, depth=DEPTH, seed=SEED, sample=other_frame[1], samples=SPP,
+                                       jitter=JITTER)
+                other["last_frame_equals_one_context"] = frame_sha(one2) == frame_sha(other_frame[0])
 
     value = W * H * SPP * args.steps / elapsed / 1e6
     line = {
@@ -663,18 +689,20 @@ def measure(args):
                    "launches": len(timed_launches), "pipeline": lanes, "bounce_blocks": blocks,
                    "tail_grid": len(tail), "bvh_nodes": len(bvh), "row_block": ROW_BLOCK,
                    "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
-                   "delivery": args.delivery,
+                   "delivery": delivery,
                    "step": ("1 frame of the still-camera display loop (main.c:379-408), lanes sharing one "
                             "accumulation buffer" if args.accumulate else "1 fresh frame (main.c:358-374)")
                            + f", {SPP} sample(s), {per} frame(s) per launch, launches rotating over {lanes} lanes, "
                              "every frame delivered to page-locked host memory",
                    "parallelism": (f"row-block shard x{n}, one process: mirt_multi over ncclCommInitAll, "
-                                   + ("RCCL gather to GPU 0 + D2H" if args.delivery == "gather"
-                                      else "per-GPU strided D2H into the host frame"))},
+                                   + ("one D2H per frame" if n == 1 else "RCCL gather to GPU 0 + D2H"
+                                      if delivery == "gather" else "per-GPU strided D2H into the host frame"))},
         "timing": "one process drives all GPUs (include/mirt_multi.h); the timed region is bracketed by "
                   "mirt_multi_wait on both sides, so it ends when every frame is in host memory on every lane",
-        "device_resident_mrays_s": round(W * H * SPP * args.steps / el_dev / 1e6, 3),
-        "device_resident_note": "the same launches with the frames left on the devices (gathered on GPU 0; no D2H)",
+        "device_resident_mrays_s": round(W * H * SPP * args.steps / el_dev / 1e6, 3) if el_dev else None,
+        "device_resident_note": ("the same launches with the frames left in device memory (no D2H)" if n == 1 else
+                                 "the same launches with every frame gathered on GPU 0 over RCCL and "
+                                 "de-interleaved there (no D2H)"),
         "depth1_mrays_s": round(W * H * SPP * args.steps / el_d1 / 1e6, 3),
         "bvh_build_s": round(build_s, 4),
         "frame_sha_last": frame_sha(last_frame),
@@ -815,9 +843,11 @@ def main():
     ap.add_argument("--no-host", action="store_true", help="skip the blocking-call leg (child process)")
     ap.add_argument("--no-other", action="store_true", help="N > 1: skip the other delivery's leg")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="1080p_10k")
-    ap.add_argument("--delivery", choices=("gather", "host-direct"), default="gather",
+    ap.add_argument("--delivery", choices=("auto", "gather", "host-direct"), default="auto",
                     help="gather: RCCL gather of the slabs to GPU 0, de-interleave, one D2H per frame (SURVEY "
-                         "8(e)); host-direct: every GPU copies its row blocks straight into the host frame")
+                         "8(e)); host-direct: every GPU copies its row blocks straight into the host frame; "
+                         "auto: gather at N = 1 (no exchange: the slab is the frame), host-direct at N > 1 (one "
+                         "host link cannot carry the frame rate of 8 GPUs: DESIGN §7)")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="lanes of contexts keeping launches in flight (0 = 4 at N = 1, 8 at N > 1)")
     ap.add_argument("--bounce-blocks", type=int, default=-1,
