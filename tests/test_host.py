@@ -343,3 +343,21 @@ def test_phantom_leaves_are_covered(mirt, kind, n, start, end, depth):
     tested = set(nd["sphere"][leaf & ~empty].tolist())
     pointed = set(nd["sphere"][empty].tolist())
     assert pointed - tested <= {start + ns}, sorted(pointed - tested)[:5]
+
+
+@pytest.mark.parametrize("H,rb,world", [(1080, 8, 1), (1080, 8, 8), (45, 8, 3), (90, 8, 7), (13, 4, 5),
+                                        (187, 8, 8), (7, 8, 3)])
+def test_delivery_index_math_restated(H, rb, world):
+    """shard.py's restatements of multi.hip's two deliveries (the gather's
+    deinterleave_kernel and host-direct's strided copies, short last block
+    included) rebuild a frame from its shards' compact slabs."""
+    from importlib import import_module
+    shard = import_module("cs201_sah-bvh_ray_tracer_amd.shard")
+    rng = np.random.default_rng(H * 31 + world)
+    full = rng.integers(0, 1 << 31, size=(2, H, 11), dtype=np.int64)
+    src, _ = shard.row_sources(H, rb, world)
+    slabs = [full[:, [y for y in range(H) if src[y] == s]] for s in range(world)]
+    for s in range(world):
+        assert slabs[s].shape[1] == shard.shard_row_count(H, rb, world, s)
+    assert (shard.assemble_gather(slabs, H, rb) == full).all()
+    assert (shard.assemble_direct(slabs, H, rb) == full).all()
