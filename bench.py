@@ -541,6 +541,18 @@ def timed_loop(m, cam, warm, timed_launches, bufs, depth, accumulate=False, tail
     return time.perf_counter() - t0
 
 
+def prime(m, cam, bufs, per):
+    """Untimed, before the warm-up steps: two launches per lane through every
+    page-locked buffer and two without a delivery. A process's first frame
+    loop into host memory ran ~9 ms slower than the same loop repeated
+    (profiles/r05f/n1_sweep.log: 4 lanes, K = 20, 1,635 -> 2,558 Mrays/s;
+    device-only 2,557 -> 2,658), a one-off start-up cost of the copy path,
+    not part of the steady frame loop the metric describes."""
+    run_launches(m, cam, plan(0, 2 * m.lanes * per, per), bufs, DEPTH)
+    run_launches(m, cam, plan(0, 2 * m.lanes * per, per), bufs, DEPTH, device_only=True)
+    m.wait()
+
+
 def make_scene():
     spheres = (mirt.create_random_spheres(NSPH, SEED) if KIND == "render"
                else mirt.create_benchmark_spheres(NSPH, SEED))
@@ -616,6 +628,7 @@ def measure(args):
     cam = mirt.default_camera()
     m = open_multi(n, lanes, delivery == "host-direct", spheres, bvh, blocks, args.opt)
     bufs = host_bufs(lanes, per)
+    prime(m, cam, bufs, per)
     warm = plan(0, args.warmup, per)
     timed_launches = plan(args.warmup, args.steps, per)
     tail = tail_of(timed_launches, tail_n, lanes, blocks)
@@ -646,6 +659,7 @@ def measure(args):
         od = "gather" if delivery == "host-direct" else "host-direct"
         m2 = open_multi(n, lanes, od == "host-direct", spheres, bvh, blocks, args.opt)
         bufs2 = host_bufs(lanes, per)
+        prime(m2, cam, bufs2, per)
         tl2 = plan(args.warmup, args.steps, per)
         el2 = timed_loop(m2, cam, plan(0, args.warmup, per), tl2, bufs2, DEPTH, args.accumulate, tail)
         other_frame = last_delivered(m2, bufs2, tl2)

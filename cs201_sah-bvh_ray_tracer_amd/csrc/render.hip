@@ -666,6 +666,7 @@ struct ContQ {
     ContRec* rec;     // cap records (a ring)
     uint32_t* flag;   // per record slot: 0 free, else the epoch of the record published there
     uint32_t cap;     // records: the launch's lanes (chains alive after the queue is dry <= lanes)
+    uint32_t consumers;  // workgroups whose first wave waits for records (the others leave when done)
 };
 constexpr uint32_t kCqHead = 0, kCqTail = 32, kCqPushers = 64, kCqWaiters = 96, kCqError = 128;
 constexpr size_t kCqCtlBytes = 4 * 160;
@@ -979,12 +980,16 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
         const uint32_t lane = threadIdx.x & 63;
         uint32_t* wst = wstack + (threadIdx.x & ~63u);
         uint32_t* wcs = cstack + (threadIdx.x & ~63u);
+        // one waiting wave per consumer workgroup (about one per CU): enough
+        // to take the tail's chains, few enough that their polling does not
+        // crowd the L2 lines every wave's walk goes through
+        const bool consumer = blockIdx.x < cq.consumers && threadIdx.x < 64;
         if (lane == 0) {
-            __hip_atomic_fetch_add(cq.ctl + kCqWaiters, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (consumer) __hip_atomic_fetch_add(cq.ctl + kCqWaiters, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_fetch_add(cq.ctl + kCqPushers, ~0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
         uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        for (;;) {
+        for (; consumer;) {
             constexpr uint32_t kNone = ~0u, kExit = ~1u;
             uint32_t got = kNone;
             if (lane == 0) {
@@ -1002,7 +1007,7 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
             got = (uint32_t)__builtin_amdgcn_readfirstlane((int)got);
             if (got == kExit) break;
             if (got == kNone) {
-                __builtin_amdgcn_s_sleep(8);
+                __builtin_amdgcn_s_sleep(32);
                 continue;
             }
             const uint32_t slot = got % cq.cap, epoch = got / cq.cap + 1u;
@@ -1040,7 +1045,8 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
             if (lane == 0) __hip_atomic_fetch_add(cq.ctl + kCqWaiters, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             t0 = __builtin_amdgcn_s_memrealtime();
         }
-        if (lane == 0) __hip_atomic_fetch_add(cq.ctl + kCqWaiters, ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (consumer && lane == 0)
+            __hip_atomic_fetch_add(cq.ctl + kCqWaiters, ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (DIAG) {
         for (int o = 32; o; o >>= 1) {
@@ -2076,6 +2082,7 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
         ContQ cq{};
         if (cq_on) {
             cq.cap = (uint32_t)bblocks * 256u;
+            cq.consumers = (uint32_t)std::max(1, c->num_cus);
             const size_t need = kCqCtlBytes + sizeof(ContRec) * cq.cap + 4 * (size_t)cq.cap;
             if (int rc2 = ensure(&c->d_cq, &c->cq_bytes, need)) return rc2;
             cq.ctl = (uint32_t*)c->d_cq;

@@ -55,8 +55,11 @@ constexpr uint32_t kPNone = 0xffffffffu;
 // reference's builds) holds the SPHERE instead (c.x, c.y, c.z, r) and its ref
 // carries kPInline: the walk recomputes the box with the same roundings and
 // has the sphere without a second dependent load.
+// Measured round 5: no faster -- the recomputed box's VALU costs
+// what the saved scalar load did (the sphere load mostly hits the scalar
+// cache or overlaps); off by default, kept as a build switch.
 #ifndef MIRT_PNODE_INLINE
-#define MIRT_PNODE_INLINE 1
+#define MIRT_PNODE_INLINE 0
 #endif
 constexpr uint32_t kPInline = 0x40000000u;
 constexpr uint32_t kPIndex = 0x3fffffffu;

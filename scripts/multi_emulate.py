@@ -37,7 +37,7 @@ def main():
     ap.add_argument("--delivery", default="gather", choices=("gather", "host-direct"))
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--rounds", type=int, default=1, help="repeat every shard's measurement (its best round counts)")
+    ap.add_argument("--rounds", type=int, default=2, help="repeat every shard's measurement (its best round counts)")
     ap.add_argument("--pipeline", type=int, default=0)
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--tail-grid", type=int, default=-1)
@@ -62,6 +62,7 @@ def main():
         m = bench.open_multi(1, lanes, a.delivery == "host-direct", spheres, bvh, blocks, a.opt)
         m.set_option(mirt.abi.MULTI_OPT_DIRECT_COPY, a.direct_copy)
         bufs = bench.host_bufs(lanes, per)
+        bench.prime(m, cam, bufs, per)
         timed = bench.plan(a.warmup, a.steps, per)
         tail = bench.tail_of(timed, tail_n, lanes, blocks)
         per_rank = []
