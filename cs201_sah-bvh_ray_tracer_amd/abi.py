@@ -160,6 +160,7 @@ SIGNATURES = [
     ("mirt_last_phase_ms", I, [P, C.POINTER(C.c_float)]),
     ("mirt_phase_log", I, [P, C.POINTER(C.c_float), I]),
     ("mirt_bounce_stats", I, [P, P, P, P, I]),
+    ("mirt_cont_queue_stats", I, [P, P, I]),
     ("mirt_set_option", I, [P, I, I]),
     ("mirt_get_option", I, [P, I]),
     # include/mirt_dropin.h: the per-ray surface

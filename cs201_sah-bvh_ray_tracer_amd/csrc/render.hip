@@ -3003,6 +3003,21 @@ int mirt_phase_log(mirt_ctx* c, float* out, int max)
     return n;
 }
 
+// Diagnostics of the last frame that used the continuation queue: {records
+// pushed, records taken, pushers left, waiters left, error bits}.
+int mirt_cont_queue_stats(mirt_ctx* c, uint32_t* out, int n)
+{
+    if (!ctx_ok(c, false, "mirt_cont_queue_stats") || !out || n <= 0) return MIRT_E_INVALID;
+    if (!c->d_cq) return 0;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    uint32_t w[kCqCtlBytes / 4];
+    HIP_TRY(hipMemcpy(w, c->d_cq, kCqCtlBytes, hipMemcpyDeviceToHost));
+    const uint32_t v[5] = {w[kCqHead], w[kCqTail], w[kCqPushers], w[kCqWaiters], w[kCqError]};
+    const int k = std::min(n, 5);
+    std::memcpy(out, v, sizeof(uint32_t) * k);
+    return k;
+}
+
 int mirt_set_option(mirt_ctx* c, int option, int value)
 {
     if (!c) return MIRT_E_INVALID;

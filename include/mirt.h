@@ -440,6 +440,10 @@ enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3,
    5), to be dropped in 1.0. The retired ids 2-4 (chunked / DFS-only schedules
    of mirt 0.1) and the retired option ids 8, 10, 12, 13 return MIRT_E_INVALID. */
 enum { MIRT_TRAV_TILE = 0, MIRT_TRAV_WAVEFRONT = 5, MIRT_TRAV_WAVEFRONT_V02 = 1 /* deprecated alias */ };
+/* Diagnostics of the last frame run with MIRT_OPT_CONT_QUEUE: up to n words of
+   {records pushed, records taken, pushers left, waiters left, error bits};
+   returns the words written (0: no such frame yet). Waits for the ctx. */
+int mirt_cont_queue_stats(mirt_ctx *ctx, uint32_t *out, int n);
 int mirt_set_option(mirt_ctx *ctx, int option, int value);
 int mirt_get_option(mirt_ctx *ctx, int option);
 

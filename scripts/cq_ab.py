@@ -6,12 +6,15 @@ the queue-off frame (and, at 10k, the reference's golden).
     python scripts/cq_ab.py [--spheres 10000,100000] [--rounds 3]
 """
 import argparse
+import ctypes
 import hashlib
 import importlib
 import json
 import os
 import sys
 import time
+
+import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -51,11 +54,14 @@ def main():
                     ph.append(r.last_phase_ms())
                     same = same and bool((hb.array == ref).all())
                 ms = sorted(dts)[len(dts) // 2] * 1e3
+                st = np.zeros(5, np.uint32)
+                k = m.load().mirt_cont_queue_stats(r.h, st.ctypes.data_as(ctypes.c_void_p), 5)
                 ph.sort(key=lambda p: p[1])
                 res.setdefault(cq, []).append(ms)
                 print(json.dumps({"spheres": n, "round": rnd, "cont_queue": cq, "blocking_ms": round(ms, 4),
                                   "primary_ms": round(ph[len(ph) // 2][0], 4), "bounce_ms": round(ph[len(ph) // 2][1], 4),
-                                  "equal_to_queue_off": same}), flush=True)
+                                  "equal_to_queue_off": same,
+                                  "cq_stats": st[:max(k, 0)].tolist() if cq else None}), flush=True)
         key = f"{W}x{H}_render{n}_d5_m1_b1_s1_c0_step1"
         g = gold.get(key, {}).get("sha")
         print(json.dumps({"spheres": n, "best_ms": {k: round(min(v), 4) for k, v in res.items()},

@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--opt", action="append", default=[])
     ap.add_argument("--hw-queues", type=int, default=16)
     ap.add_argument("--device-only", action="store_true", help="frames left on the devices (no delivery to host)")
+    ap.add_argument("--sweep", default="", help="LANES:BATCH:TAIL[,...] schedules to emulate instead of the bench's")
     ap.add_argument("--direct-copy", type=int, default=0, help="MIRT_MULTI_OPT_DIRECT_COPY for host-direct")
     a = ap.parse_args()
     if a.hw_queues and int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < a.hw_queues:
@@ -57,7 +58,10 @@ def main():
     W, H, SPP = bench.W, bench.H, bench.SPP
     spheres, bvh, _ = bench.make_scene()
     cam = mirt.default_camera()
-    for world in (int(w) for w in a.worlds.split(",")):
+    combos = [tuple(int(v) for v in c.split(":")) for c in a.sweep.split(",")] if a.sweep else [None]
+    for world, combo in ((int(w), c) for w in a.worlds.split(",") for c in combos):
+        if combo:
+            a.pipeline, a.batch, a.tail_grid = combo
         lanes, per, tail_n, blocks = bench.schedule(a, world)
         m = bench.open_multi(1, lanes, a.delivery == "host-direct", spheres, bvh, blocks, a.opt)
         m.set_option(mirt.abi.MULTI_OPT_DIRECT_COPY, a.direct_copy)
