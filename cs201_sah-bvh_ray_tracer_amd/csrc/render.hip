@@ -677,9 +677,24 @@ constexpr uint64_t kContSpinTicks = 2000000;   // 20 ms of the 100 MHz real-time
 #define MIRT_CQ_LANE_PUSH 1
 #endif
 
+// Cross-XCD traffic without cache maintenance: the eight XCDs' L2s are not
+// coherent with each other, and an acquire / release at agent scope costs an
+// L2 invalidate / write-back (buffer_inv / buffer_wbl2 sc1) that throws away
+// every wave's cached tree nodes -- so every word of the queue is read and
+// written with RELAXED agent-scope atomics (sc0 sc1: they bypass the caches),
+// and ordering comes from waiting for this wave's own memory operations to
+// complete (a workgroup-scope fence: s_waitcnt, nothing flushed).
 __device__ __forceinline__ uint32_t cq_load(const uint32_t* p)
 {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void cq_store(uint32_t* p, uint32_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void cq_complete()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // this wave's loads / stores done
 }
 
 // Pushes the waiting waves would take at once: waiters - records queued.
@@ -704,15 +719,22 @@ __device__ __forceinline__ void cq_push(const ContQ& q, const Ray& ray, uint32_t
         }
         __builtin_amdgcn_s_sleep(2);
     }
-    ContRec r;
-    r.ox = ray.ox; r.oy = ray.oy; r.oz = ray.oz; r.dx = ray.dx; r.dy = ray.dy; r.dz = ray.dz;
-    r.pixel = pixel; r.k = k; r.base0 = base0; r.level = (uint32_t)level;
+    uint32_t* d = (uint32_t*)(q.rec + slot);
+    cq_store(d + 0, __float_as_uint(ray.ox));
+    cq_store(d + 1, __float_as_uint(ray.oy));
+    cq_store(d + 2, __float_as_uint(ray.oz));
+    cq_store(d + 3, __float_as_uint(ray.dx));
+    cq_store(d + 4, __float_as_uint(ray.dy));
+    cq_store(d + 5, __float_as_uint(ray.dz));
+    cq_store(d + 6, pixel);
+    cq_store(d + 7, k);
+    cq_store(d + 8, base0);
+    cq_store(d + 9, (uint32_t)level);
 #pragma unroll
-    for (int l = 0; l < 6; l++) r.col[l] = l < level - 1 ? cs[l * cstride] : 0u;
-    uint4* d = (uint4*)(q.rec + slot);
-    const uint4* v = (const uint4*)&r;
-    d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
-    __hip_atomic_store(q.flag + slot, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    for (int l = 0; l < 6; l++)
+        if (l < level - 1) cq_store(d + 10 + l, cs[l * cstride]);
+    cq_complete();                              // the record is in memory before its flag
+    cq_store(q.flag + slot, epoch);
 }
 
 // Persistent bounce pass: each lane owns one pixel's chain of bounces,
@@ -985,8 +1007,9 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
         // crowd the L2 lines every wave's walk goes through
         const bool consumer = blockIdx.x < cq.consumers && threadIdx.x < 64;
         if (lane == 0) {
-            if (consumer) __hip_atomic_fetch_add(cq.ctl + kCqWaiters, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(cq.ctl + kCqPushers, ~0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            if (consumer) atomicAdd(cq.ctl + kCqWaiters, 1u);
+            cq_complete();                          // this wave's pushes are published first
+            atomicAdd(cq.ctl + kCqPushers, ~0u);
         }
         uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         for (; consumer;) {
@@ -1014,7 +1037,7 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
             uint32_t ok = 1;
             if (lane == 0) {
                 const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
-                __hip_atomic_fetch_add(cq.ctl + kCqWaiters, ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                atomicAdd(cq.ctl + kCqWaiters, ~0u);
                 while (cq_load(cq.flag + slot) != epoch) {
                     if (__builtin_amdgcn_s_memrealtime() - w0 > kContSpinTicks) {
                         atomicOr(cq.ctl + kCqError, 4u);
@@ -1026,10 +1049,10 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
             }
             ok = (uint32_t)__builtin_amdgcn_readfirstlane((int)ok);
             if (!ok) break;
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            const uint32_t word = lane < 16 ? ((const uint32_t*)(cq.rec + slot))[lane] : 0u;
+            const uint32_t word = lane < 16 ? cq_load((const uint32_t*)(cq.rec + slot) + lane) : 0u;
+            cq_complete();                          // the record is read before its slot is freed
             __builtin_amdgcn_wave_barrier();
-            if (lane == 0) __hip_atomic_store(cq.flag + slot, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) cq_store(cq.flag + slot, 0u);
             auto wd = [&](int i) { return (uint32_t)__builtin_amdgcn_readlane((int)word, i); };
             const Ray cr{__uint_as_float(wd(0)), __uint_as_float(wd(1)), __uint_as_float(wd(2)),
                          __uint_as_float(wd(3)), __uint_as_float(wd(4)), __uint_as_float(wd(5))};
@@ -1042,11 +1065,10 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             solo_chain<FAST>(sc, f, 0, cr, INFINITY, -1, prune_off(), QuadWalk{sc.wide_root, 0u, 0u}, clevel, wd(7),
                              wd(6), wd(8), 0u, wst, wcs, out, acc, (lds_uint4*)hcache, hc_n);
-            if (lane == 0) __hip_atomic_fetch_add(cq.ctl + kCqWaiters, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) atomicAdd(cq.ctl + kCqWaiters, 1u);
             t0 = __builtin_amdgcn_s_memrealtime();
         }
-        if (consumer && lane == 0)
-            __hip_atomic_fetch_add(cq.ctl + kCqWaiters, ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (consumer && lane == 0) atomicAdd(cq.ctl + kCqWaiters, ~0u);
     }
     if (DIAG) {
         for (int o = 32; o; o >>= 1) {
