@@ -676,6 +676,11 @@ constexpr uint64_t kContSpinTicks = 2000000;   // 20 ms of the 100 MHz real-time
 #ifndef MIRT_CQ_LANE_PUSH
 #define MIRT_CQ_LANE_PUSH 1
 #endif
+// A/B of the queue's costs (0 = the queue): 1 no pushes (no room reads),
+// 2 room reads but no pushes, 3 no waiting waves and no pushes
+#ifndef MIRT_CQ_VARIANT
+#define MIRT_CQ_VARIANT 0
+#endif
 
 // Cross-XCD traffic without cache maintenance: the eight XCDs' L2s are not
 // coherent with each other, and an acquire / release at agent scope costs an
@@ -700,6 +705,8 @@ __device__ __forceinline__ void cq_complete()
 // Pushes the waiting waves would take at once: waiters - records queued.
 __device__ __forceinline__ uint32_t cq_room(const ContQ& q)
 {
+    if (MIRT_CQ_VARIANT == 1 || MIRT_CQ_VARIANT == 3) return 0u;
+    if (MIRT_CQ_VARIANT == 2) return cq_load(q.ctl + kCqWaiters) + cq_load(q.ctl + kCqHead) + cq_load(q.ctl + kCqTail) == 0xffffffffu ? 1u : 0u;
     const uint32_t w = cq_load(q.ctl + kCqWaiters), h = cq_load(q.ctl + kCqHead), t = cq_load(q.ctl + kCqTail);
     const uint32_t queued = h - t;
     return w > queued ? w - queued : 0u;
@@ -1005,7 +1012,7 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
         // one waiting wave per consumer workgroup (about one per CU): enough
         // to take the tail's chains, few enough that their polling does not
         // crowd the L2 lines every wave's walk goes through
-        const bool consumer = blockIdx.x < cq.consumers && threadIdx.x < 64;
+        const bool consumer = MIRT_CQ_VARIANT != 3 && blockIdx.x < cq.consumers && threadIdx.x < 64;
         if (lane == 0) {
             if (consumer) atomicAdd(cq.ctl + kCqWaiters, 1u);
             cq_complete();                          // this wave's pushes are published first
