@@ -1496,8 +1496,10 @@ struct AccumShare {
 #define MIRT_LEAF_BATCH_DEFAULT 2
 #endif
 
+// Measured: the blocking call 1.22 -> 3.07 ms with the
+// queue (waiting waves alone +0.3 ms, the hand-overs +1.5 ms): off by default
 #ifndef MIRT_CONT_QUEUE_DEFAULT
-#define MIRT_CONT_QUEUE_DEFAULT 1
+#define MIRT_CONT_QUEUE_DEFAULT 0
 #endif
 
 struct mirt_ctx {

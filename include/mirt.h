@@ -431,9 +431,9 @@ enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3,
        MIRT_OPT_CONT_QUEUE = 20     /* wavefront, four-wide bounce walk: once a frame's bounce queue is
                                        dry, waves out of chains wait and take chains starting their
                                        next level from waves that still hold several, walking each
-                                       with the whole wave -- 1 (default) for a frame alone on the
-                                       chip (the blocking mirt_render_frame), 2 for every frame, 0
-                                       never. Speed only. */ };
+                                       with the whole wave -- 1 for a frame alone on the chip (the
+                                       blocking mirt_render_frame), 2 for every frame, 0 (default)
+                                       never: measured slower. Speed only. */ };
 /* Traversal ids keep their first-release values (mirt 0.1: TILE 0, WAVEFRONT 5).
    ABI note: the mirt 0.2 header numbered WAVEFRONT 1; mirt_set_option accepts
    1 as a deprecated alias of MIRT_TRAV_WAVEFRONT (mirt_get_option reads back
