@@ -116,12 +116,12 @@ HW_QUEUES_SINGLE = 0
 # 4K/1M 0% / 0%: within the rounds' spread at the metric's config, so the
 # bench keeps one launch plan for the whole burst (0).
 TAIL_GRID = 0
-# at N > 1 a rank's launch is 1/N of a frame per frame carried, and the
-# burst's drain is a larger share of the timed region: the last 2 of the 5
-# launches (K = 20, 4 frames each) on the full grid -- the one-frame split at
-# N = 8 emulated per shard (scripts/shard_times.py --tail-grid, copy stream,
-# 16 queues; profiles/r04g/): 15.4-15.6 -> 16.4 Grays/s (1 launch: 16.1)
-TAIL_GRID_MULTI = 2
+# at N > 1 a rank's launch is 1/N of a frame per frame carried. Round 4's
+# Python ranks gained from the burst's last 2 launches on the full grid
+# (profiles/r04g/); through mirt_multi (round 5, the per-shard emulation,
+# host-direct, best of three per shard, profiles/r05k/) it loses: the last
+# 0 / 1 / 2 launches on the full grid 15.51 / 14.91 / 14.82 Grays/s at N = 8
+TAIL_GRID_MULTI = 0
 KERNEL = "bounce_kernel<true, 2, false>"   # dominant kernel of the default (wavefront, four-wide) schedule
 # the PMC-derived bound of the timed launch shape, per workload
 # (scripts/pmc_bench.sh over this script's own command + scripts/pmc_summary.py);
@@ -527,7 +527,14 @@ def run_launches(m, cam, launches, bufs, depth, accumulate=False, tail=(), devic
     for f0, k in seq:
         lane = m.launches % m.lanes
         outs = None if device_only else bufs[lane][:k]
+        t0 = time.perf_counter()
         m.render_frames_async(cam, frame_desc_for(f0, k, depth, accumulate), outs, nframes=k, full_grid=f0 in tail)
+        ENQUEUE.append(time.perf_counter() - t0)
+
+
+# host time of each render_frames_async call of the last loop (the enqueue of
+# every rank's launch; at N GPUs one host thread issues N ranks' work)
+ENQUEUE = []
 
 
 def timed_loop(m, cam, warm, timed_launches, bufs, depth, accumulate=False, tail=(), device_only=False):
@@ -535,6 +542,7 @@ def timed_loop(m, cam, warm, timed_launches, bufs, depth, accumulate=False, tail
     both sides (every frame delivered when the clock stops); seconds."""
     run_launches(m, cam, warm, bufs, depth, accumulate, (), device_only)
     m.wait()
+    ENQUEUE.clear()
     t0 = time.perf_counter()
     run_launches(m, cam, timed_launches, bufs, depth, accumulate, tail, device_only)
     m.wait()
@@ -633,6 +641,7 @@ def measure(args):
     timed_launches = plan(args.warmup, args.steps, per)
     tail = tail_of(timed_launches, tail_n, lanes, blocks)
     elapsed = timed_loop(m, cam, warm, timed_launches, bufs, DEPTH, args.accumulate, tail)
+    enqueue_ms = [round(float(np.median(ENQUEUE)) * 1e3, 4), round(float(np.max(ENQUEUE)) * 1e3, 4)]
     last_frame, last_sample = last_delivered(m, bufs, timed_launches)
     # the passes of rank 0's timed launches (HIP events on each launch's own
     # stream, under the overlap of the lanes in flight)
@@ -723,6 +732,10 @@ def measure(args):
         "last_frame_equals_one_context": same,
         "phases_under_overlap_ms": {"primary": round(primary_ms, 4), "bounce": round(bounce_ms, 4),
                                     "launches": len(phases)},
+        "host_enqueue_ms_per_launch": {"median": enqueue_ms[0], "max": enqueue_ms[1],
+                                       "note": "host time of one mirt_multi_render_frames_async (every rank's "
+                                               "launch issued from this one thread; includes waiting for the "
+                                               "lane's previous launch)"},
     }
     if other:
         line["value_" + other["delivery"].replace("-", "_")] = other["mrays_s"]

@@ -69,7 +69,7 @@ def main():
         bench.prime(m, cam, bufs, per)
         timed = bench.plan(a.warmup, a.steps, per)
         tail = bench.tail_of(timed, tail_n, lanes, blocks)
-        per_rank = []
+        per_rank, enq = [], []
         for k in range(world):
             m.emulate(world, k)
             best = None
@@ -77,6 +77,7 @@ def main():
                 el = bench.timed_loop(m, cam, bench.plan(0, a.warmup, per), timed, bufs, bench.DEPTH, a.accumulate,
                                       tail, device_only=a.device_only)
                 best = el if best is None else min(best, el)
+                enq += bench.ENQUEUE
             per_rank.append(best)
         m.close()
         bench.close_bufs(bufs)
@@ -88,6 +89,7 @@ def main():
             "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
             "rank_ms_per_frame": [round(t / a.steps * 1e3, 4) for t in per_rank],
             "slowest_rank": per_rank.index(slow),
+            "enqueue_ms_per_launch_median": round(sorted(enq)[len(enq) // 2] * 1e3, 4) if enq else None,
             "pred_job_mrays_s": round(W * H * SPP * a.steps / slow / 1e6, 1)}), flush=True)
     return 0
 
