@@ -18,7 +18,12 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <memory>
+#include <mutex>
 #include <cstring>
 #include <new>
 #include <string>
@@ -96,6 +101,18 @@ int grow(int dev, uint32_t** p, size_t* cap, size_t bytes)
     return MIRT_OK;
 }
 
+// What one launch asks of every rank (set by the caller's thread before the
+// ranks issue it; read-only while they do).
+struct Launch {
+    mirt_camera cam;
+    mirt_frame_desc sd;             // shard geometry of the frame (num_shards = world), samples = spp * nframes
+    int nframes = 1, flags = 0, world = 1, W = 0, H = 0, rb = 8;
+    bool emu = false, gather = false, rank0_assembles = false, deliver = false;
+    ShardSrc sr{};                  // rows of every shard (p[] filled by rank 0)
+    size_t shard_stride = 0, frame_elems = 0;
+    std::vector<mirt_rgba8*> dst;   // frame j's host destination (page-locked: the caller's or the staging)
+};
+
 // One launch in flight: a context per rank, the gather buffer and the frames
 // on rank 0, the copy-mode events and each rank's completion event.
 struct Lane {
@@ -120,6 +137,29 @@ struct Lane {
         size_t bytes;
     };
     std::vector<Deferred> deferred;
+    Launch job;
+    // the ranks' issue of the current launch (rank threads): ranks done issuing,
+    // and copy mode's hand-over of each rank's slabs to rank 0
+    std::unique_ptr<std::atomic<int>> issued{new std::atomic<int>(0)};
+    std::vector<std::unique_ptr<std::atomic<uint64_t>>> slabs_ready;   // launch number whose `rendered[r]` is recorded
+    std::vector<uint32_t*> src;       // rank r's first display slab of the current launch
+    uint64_t seq = 0;                 // launch number on this lane
+    std::unique_ptr<std::mutex> err_mu{new std::mutex};
+    int err = MIRT_OK;                // first issue error of the current launch
+    std::string err_msg;
+};
+
+// One host thread per rank (n > 1): the caller's thread prepares a launch and
+// hands it to every rank's thread, which issues that rank's part on its own
+// device -- so N GPUs are fed by N threads, not one, and rank r's first
+// launch does not wait behind ranks 0 .. r - 1's (one host
+// thread calls; inside, one stream per GPU).
+struct RankThread {
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<int> q;                // lanes to issue, in launch order
+    bool stop = false;
 };
 
 }  // namespace
@@ -131,6 +171,7 @@ struct mirt_multi {
     bool direct = false;              // MIRT_MULTI_HOST_DIRECT
     std::vector<ncclComm_t> comm;
     std::vector<Lane> lanes;
+    std::vector<std::unique_ptr<RankThread>> workers;   // n > 1
     int next = 0;
     int timeout_ms = 60000;           // MIRT_MULTI_OPT_TIMEOUT_MS (0: unbounded)
     int emu_world = 0, emu_rank = 0;  // MIRT_MULTI_OPT_EMULATE_*: this one rank plays shard emu_rank of emu_world
@@ -165,8 +206,10 @@ int fail_multi(mirt_multi* m, const std::string& why)
     return MIRT_E_DEVICE;
 }
 
-// Wait for lane `li`'s launch on every rank, polling each rank's completion
-// event against the deadline (no unbounded hipStreamSynchronize).
+// Wait for lane `li`'s launch on every rank: every rank thread has issued
+// it, then each rank's completion event, polled against the deadline (no
+// unbounded hipStreamSynchronize). An issue error is returned once the work
+// that did reach the streams has finished.
 int wait_lane(mirt_multi* m, int li)
 {
     if (m->failed) return failed_status(m, "mirt_multi");
@@ -174,6 +217,19 @@ int wait_lane(mirt_multi* m, int li)
     if (!L.pending) return MIRT_OK;
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
+    auto over = [&]() {
+        return m->timeout_ms > 0 && std::chrono::duration<double, std::milli>(clk::now() - t0).count() > m->timeout_ms;
+    };
+    for (long polls = 0; L.issued->load(std::memory_order_acquire) < m->n; polls++) {
+        if (over())
+            return fail_multi(m, "lane " + std::to_string(li) + ": the rank threads did not issue the launch within " +
+                                     std::to_string(m->timeout_ms) + " ms (MIRT_MULTI_OPT_TIMEOUT_MS); communicators "
+                                     "aborted, the object is unusable");
+        if (polls < 2000)
+            std::this_thread::yield();
+        else
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
     for (int r = 0; r < m->n; r++) {
         for (long polls = 0;; polls++) {
             const hipError_t e = hipEventQuery(L.done[r]);
@@ -183,8 +239,7 @@ int wait_lane(mirt_multi* m, int li)
                 return fail_multi(m, std::string("rank ") + std::to_string(r) + " (device " +
                                          std::to_string(m->dev[r]) + "): " + hipGetErrorString(e));
             }
-            const double ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
-            if (m->timeout_ms > 0 && ms > m->timeout_ms) {
+            if (over()) {
                 std::string stuck;
                 for (int q = r; q < m->n; q++)
                     if (hipEventQuery(L.done[q]) == hipErrorNotReady)
@@ -204,63 +259,76 @@ int wait_lane(mirt_multi* m, int li)
         }
     }
     L.pending = false;
+    if (L.err) {
+        const int rc = L.err;
+        set_error("%s", L.err_msg.c_str());
+        L.err = MIRT_OK;
+        L.deferred.clear();
+        return rc;
+    }
     for (const Lane::Deferred& d : L.deferred) std::memcpy(d.dst, d.src, d.bytes);
     L.deferred.clear();
     return MIRT_OK;
 }
 
-// After a failed enqueue: whatever part of the launch reached the streams is
-// covered by the completion events, so the lane's next wait sees it.
-void mark_partial(mirt_multi* m, Lane& L)
+int communicators(mirt_multi* m)
 {
-    for (int r = 0; r < m->n; r++) {
-        (void)hipSetDevice(m->dev[r]);
-        (void)hipEventRecord(L.done[r], stream_of(L.ctx[r]));
+    if (!m->comm.empty()) return MIRT_OK;
+    m->comm.assign(m->n, nullptr);
+    const ncclResult_t e = ncclCommInitAll(m->comm.data(), m->n, m->dev.data());
+    if (e != ncclSuccess) {
+        m->comm.clear();
+        return nccl_err(e, "mirt_multi: ncclCommInitAll");
     }
-    (void)hipGetLastError();
+    return MIRT_OK;
 }
 
-// Launch on lane L: `nframes` frames (RNG samples fd->sample + j) on every
-// rank, then the gather / host delivery into outs[j] (outs null: the frames
-// stay on the devices).
-int enqueue(mirt_multi* m, Lane& L, const mirt_camera* cam, const mirt_frame_desc* fd, int nframes, int flags,
+// The caller's part of a launch on lane L: the geometry, rank 0's buffers,
+// where every frame lands. Then the ranks issue it (issue_rank).
+int prepare(mirt_multi* m, Lane& L, const mirt_camera* cam, const mirt_frame_desc* fd, int nframes, int flags,
             mirt_rgba8* const* outs)
 {
-    const int n = m->n;
-    const bool emu = m->emu_world > 1;
-    const int world = emu ? m->emu_world : n;   // shards of the frame
+    Launch& J = L.job;
+    J.cam = *cam;
+    J.nframes = nframes;
+    J.flags = flags;
+    J.emu = m->emu_world > 1;
+    J.world = J.emu ? m->emu_world : m->n;   // shards of the frame
+    J.W = fd->width;
+    J.H = fd->height;
     const int spp = std::max(1, fd->samples);
-    const int W = fd->width, H = fd->height;
-    mirt_frame_desc sd = *fd;
-    sd.row_block = fd->row_block > 0 ? fd->row_block : 8;
-    sd.num_shards = world;
-    sd.samples = spp * nframes;
-    const int rb = sd.row_block;
-    ShardSrc sr{};
-    for (int s = 0; s < world; s++) {
-        sd.shard = s;
-        sr.rows[s] = shard_row_count(&sd);
+    J.sd = *fd;
+    J.sd.row_block = fd->row_block > 0 ? fd->row_block : 8;
+    J.sd.num_shards = J.world;
+    J.sd.samples = spp * nframes;
+    J.rb = J.sd.row_block;
+    J.sr = ShardSrc{};
+    mirt_frame_desc g = J.sd;
+    for (int s = 0; s < J.world; s++) {
+        g.shard = s;
+        J.sr.rows[s] = shard_row_count(&g);
     }
-    const size_t slab_elems = (size_t)sr.rows[0] * W;          // shard 0 holds the most rows
-    const size_t shard_stride = slab_elems * nframes;           // gathered: shard s's displays
-    const size_t frame_elems = (size_t)W * H;
-    const int dev0 = m->dev[0];
-    const bool gather = !m->direct;                             // frames to device 0
-    const bool rank0_assembles = gather && (!emu || m->emu_rank == 0);
-    if (gather && world > 1) {
-        int rc = grow(dev0, &L.gathered, &L.gathered_cap, 4 * shard_stride * world + 4);
-        if (!rc && world > 1 && rank0_assembles) rc = grow(dev0, &L.frame, &L.frame_cap, 4 * frame_elems * nframes + 4);
+    J.shard_stride = (size_t)J.sr.rows[0] * J.W * nframes;   // shard 0 holds the most rows
+    J.frame_elems = (size_t)J.W * J.H;
+    J.gather = !m->direct;                                     // frames to device 0
+    J.rank0_assembles = J.gather && (!J.emu || m->emu_rank == 0);
+    J.deliver = outs != nullptr;
+    if (J.gather && J.world > 1) {
+        int rc = grow(m->dev[0], &L.gathered, &L.gathered_cap, 4 * J.shard_stride * J.world + 4);
+        if (!rc && J.rank0_assembles) rc = grow(m->dev[0], &L.frame, &L.frame_cap, 4 * J.frame_elems * nframes + 4);
         if (rc) return rc;
     }
+    if (m->rccl && J.gather && (m->n > 1 || (J.emu && m->emu_rank > 0)))
+        if (int rc = communicators(m)) return rc;
     // where frame j lands: the caller's buffer if it is page-locked, else
     // the lane's staging area (copied out by wait_lane)
-    std::vector<mirt_rgba8*> dst(nframes, nullptr);
+    J.dst.assign(nframes, nullptr);
     L.deferred.clear();
     if (outs) {
-        const size_t fb = 4 * frame_elems;
+        const size_t fb = 4 * J.frame_elems;
         for (int j = 0; j < nframes; j++) {
             if (host_page_locked(outs[j], fb)) {
-                dst[j] = outs[j];
+                J.dst[j] = outs[j];
                 continue;
             }
             if (L.stage_cap < fb * nframes) {
@@ -270,137 +338,211 @@ int enqueue(mirt_multi* m, Lane& L, const mirt_camera* cam, const mirt_frame_des
                 MHIP(hipHostMalloc((void**)&L.stage, fb * nframes, hipHostMallocDefault));
                 L.stage_cap = fb * nframes;
             }
-            dst[j] = (mirt_rgba8*)(L.stage + fb * j);
-            L.deferred.push_back({outs[j], dst[j], fb});
+            J.dst[j] = (mirt_rgba8*)(L.stage + fb * j);
+            L.deferred.push_back({outs[j], J.dst[j], fb});
         }
     }
-    L.pending = true;
-    // every rank renders its row blocks of all frames: `samples` slabs in the
-    // ctx's own buffer, frame j's display in slab (j + 1) * spp - 1 (one frame
-    // of several samples: its last slab)
-    std::vector<uint32_t*> src(n, nullptr);
-    std::vector<size_t> cnt(n, 0);
-    std::vector<int> shard(n, 0);
-    for (int r = 0; r < n; r++) {
-        shard[r] = emu ? m->emu_rank : r;
-        sd.shard = shard[r];
-        const size_t elems = (size_t)sr.rows[shard[r]] * W;
-        int keep = 0;
-        if (flags & MIRT_MULTI_FULL_GRID) {
-            keep = mirt_get_option(L.ctx[r], MIRT_OPT_BOUNCE_BLOCKS);
-            (void)mirt_set_option(L.ctx[r], MIRT_OPT_BOUNCE_BLOCKS, 0);
-        }
-        uint32_t* disp = nullptr;
-        int rc = enqueue_frame_device(L.ctx[r], cam, &sd, nullptr, &disp, "mirt_multi_render_frames_async",
-                                      nframes > 1);
-        if (flags & MIRT_MULTI_FULL_GRID) (void)mirt_set_option(L.ctx[r], MIRT_OPT_BOUNCE_BLOCKS, keep);
-        if (rc) return rc;
-        src[r] = disp - (size_t)(nframes - 1) * elems;   // spp == 1 when nframes > 1: slab j = frame j
-        cnt[r] = elems * nframes;
+    return MIRT_OK;
+}
+
+// Rank r's part of lane L's current launch, on its own device and stream:
+// its row blocks of every frame, then its share of the delivery, then the
+// completion event. Called by rank r's thread (or, for one rank, the
+// caller's).
+int issue_rank_body(mirt_multi* m, Lane& L, int r)
+{
+    const Launch& J = L.job;
+    const int n = m->n;
+    const int s = J.emu ? m->emu_rank : r;    // the shard rank r renders
+    const size_t elems = (size_t)J.sr.rows[s] * J.W;
+    mirt_frame_desc sd = J.sd;
+    sd.shard = s;
+    mirt_ctx* c = L.ctx[r];
+    hipStream_t st = stream_of(c);
+    int keep = 0;
+    if (J.flags & MIRT_MULTI_FULL_GRID) {
+        keep = mirt_get_option(c, MIRT_OPT_BOUNCE_BLOCKS);
+        (void)mirt_set_option(c, MIRT_OPT_BOUNCE_BLOCKS, 0);
     }
-    hipStream_t s0 = stream_of(L.ctx[0]);
-    if (gather) {
-        // rank 0's own displays stay where it rendered them; the other
-        // shards' land in the gather buffer
-        sr.p[shard[0]] = src[0];
-        for (int s = 0; s < world; s++)
-            if (s != shard[0]) sr.p[s] = L.gathered + (size_t)s * shard_stride;
-        if (m->rccl && (n > 1 || (emu && m->emu_rank > 0))) {
-            if (m->comm.empty()) {
-                m->comm.assign(n, nullptr);
-                ncclResult_t e = ncclCommInitAll(m->comm.data(), n, m->dev.data());
-                if (e != ncclSuccess) {
-                    m->comm.clear();
-                    return nccl_err(e, "mirt_multi_render_frames_async: ncclCommInitAll");
+    uint32_t* disp = nullptr;
+    int rc = enqueue_frame_device(c, &J.cam, &sd, nullptr, &disp, "mirt_multi_render_frames_async", J.nframes > 1);
+    if (J.flags & MIRT_MULTI_FULL_GRID) (void)mirt_set_option(c, MIRT_OPT_BOUNCE_BLOCKS, keep);
+    if (rc) return rc;
+    uint32_t* src = disp - (size_t)(J.nframes - 1) * elems;   // spp == 1 when nframes > 1: slab j = frame j
+    const size_t cnt = elems * J.nframes;
+    L.src[r] = src;
+    MHIP(hipSetDevice(m->dev[r]));
+    if (J.gather) {
+        // slabs that travel: every rank's but rank 0's own (read in place);
+        // an emulated rank k > 0 sends its own to itself
+        const bool exchange = n > 1 || (J.emu && m->emu_rank > 0);
+        if (!m->rccl && r > 0) {
+            // copy mode: rank 0's stream copies this rank's slabs once they are done
+            MHIP(hipEventRecord(L.rendered[r], st));
+            L.slabs_ready[r]->store(L.seq, std::memory_order_release);
+        } else if (m->rccl && exchange && r > 0) {
+            // RCCL: this rank's displays to rank 0, on the stream that rendered them
+            MNCCL(ncclSend(src, cnt, ncclUint32, 0, m->comm[r], st));
+        }
+        if (r == 0) {
+            ShardSrc sr = J.sr;
+            // rank 0's own displays stay where it rendered them; the other
+            // shards' land in the gather buffer
+            sr.p[s] = src;
+            for (int q = 0; q < J.world; q++)
+                if (q != s) sr.p[q] = L.gathered + (size_t)q * J.shard_stride;
+            if (m->rccl && exchange) {
+                // one group: rank 0 receives shard q at gathered + q * stride
+                // (emulated rank k > 0: its send, as a send to itself)
+                MNCCL(ncclGroupStart());
+                ncclResult_t e = ncclSuccess;
+                if (n == 1) {
+                    e = ncclSend(src, cnt, ncclUint32, 0, m->comm[0], st);
+                    if (e == ncclSuccess) e = ncclRecv(L.gathered + (size_t)s * J.shard_stride, cnt, ncclUint32, 0,
+                                                       m->comm[0], st);
                 }
-            }
-            // one group: every other rank sends its displays to rank 0, which
-            // receives shard s at gathered + s * shard_stride; each op on the
-            // stream that rendered it, so it starts when that rank's frames
-            // are done. (Emulated rank k > 0: its send, as a send to itself.)
-            MNCCL(ncclGroupStart());
-            for (int r = n > 1 ? 1 : 0; r < n; r++) {
-                ncclResult_t e = ncclSend(src[r], cnt[r], ncclUint32, 0, m->comm[r], stream_of(L.ctx[r]));
-                if (e == ncclSuccess)
-                    e = ncclRecv(L.gathered + (size_t)shard[r] * shard_stride, cnt[r], ncclUint32, r, m->comm[0], s0);
+                for (int q = 1; q < n && e == ncclSuccess; q++)
+                    e = ncclRecv(L.gathered + (size_t)q * J.shard_stride, (size_t)J.sr.rows[q] * J.W * J.nframes,
+                                 ncclUint32, q, m->comm[0], st);
                 if (e != ncclSuccess) {
                     (void)ncclGroupEnd();
                     return nccl_err(e, "mirt_multi_render_frames_async: ncclSend/ncclRecv");
                 }
+                MNCCL(ncclGroupEnd());
+            } else if (!m->rccl) {
+                // copy mode: wait for each rank's slabs, then copy them
+                // (peer-to-peer across devices, device-local otherwise)
+                using clk = std::chrono::steady_clock;
+                const auto t0 = clk::now();
+                for (int q = 1; q < n; q++) {
+                    while (L.slabs_ready[q]->load(std::memory_order_acquire) != L.seq) {
+                        if (m->timeout_ms > 0 &&
+                            std::chrono::duration<double, std::milli>(clk::now() - t0).count() > m->timeout_ms) {
+                            set_error("mirt_multi: rank %d never handed its slabs over", q);
+                            return MIRT_E_DEVICE;
+                        }
+                        std::this_thread::yield();
+                    }
+                    MHIP(hipStreamWaitEvent(st, L.rendered[q], 0));
+                    uint32_t* to = L.gathered + (size_t)q * J.shard_stride;
+                    const size_t cq = (size_t)J.sr.rows[q] * J.W * J.nframes;
+                    if (m->dev[q] == m->dev[0])
+                        MHIP(hipMemcpyAsync(to, L.src[q], 4 * cq, hipMemcpyDeviceToDevice, st));
+                    else
+                        MHIP(hipMemcpyPeerAsync(to, m->dev[0], L.src[q], m->dev[q], 4 * cq, st));
+                }
             }
-            MNCCL(ncclGroupEnd());
-        } else if (!m->rccl) {
-            // copy mode: rank 0's stream waits for each rank's frames, then
-            // copies its slabs (peer-to-peer across devices, device-local
-            // otherwise)
-            for (int r = 1; r < n; r++) {
-                MHIP(hipSetDevice(m->dev[r]));
-                MHIP(hipEventRecord(L.rendered[r], stream_of(L.ctx[r])));
-                MHIP(hipSetDevice(dev0));
-                MHIP(hipStreamWaitEvent(s0, L.rendered[r], 0));
-                uint32_t* to = L.gathered + (size_t)shard[r] * shard_stride;
-                if (m->dev[r] == dev0)
-                    MHIP(hipMemcpyAsync(to, src[r], 4 * cnt[r], hipMemcpyDeviceToDevice, s0));
-                else
-                    MHIP(hipMemcpyPeerAsync(to, dev0, src[r], m->dev[r], 4 * cnt[r], s0));
+            if (J.emu && m->emu_rank == 0) {
+                // emulated rank 0 of a `world`-rank job: the other shards' slabs
+                // arrive too (HBM writes of the receives; the xGMI wire time and
+                // the receive kernels are not modelled), copied from its own
+                for (int q = 1; q < J.world; q++)
+                    MHIP(hipMemcpyAsync(L.gathered + (size_t)q * J.shard_stride, src,
+                                        4 * std::min(cnt, (size_t)J.sr.rows[q] * J.W * J.nframes),
+                                        hipMemcpyDeviceToDevice, st));
+            }
+            if (J.rank0_assembles) {
+                const uint32_t* frames = src;   // one shard: its displays are the frames
+                if (J.world > 1) {
+                    const dim3 grid((J.W + 255) / 256, J.H, J.nframes);
+                    deinterleave_kernel<<<grid, 256, 0, st>>>(sr, L.frame, J.W, J.H, J.rb, J.world);
+                    MHIP(hipGetLastError());
+                    frames = L.frame;
+                }
+                if (J.deliver)
+                    for (int j = 0; j < J.nframes; j++)
+                        MHIP(hipMemcpyAsync(J.dst[j], frames + (size_t)j * J.frame_elems, 4 * J.frame_elems,
+                                            hipMemcpyDeviceToHost, st));
             }
         }
-        MHIP(hipSetDevice(dev0));
-        if (emu && m->emu_rank == 0) {
-            // emulated rank 0 of a `world`-rank job: the other shards' slabs
-            // arrive too (HBM writes of the receives; the xGMI wire time and
-            // the receive kernels are not modelled), copied from its own
-            for (int s = 1; s < world; s++)
-                MHIP(hipMemcpyAsync(L.gathered + (size_t)s * shard_stride, src[0],
-                                    4 * std::min(cnt[0], (size_t)sr.rows[s] * W * nframes), hipMemcpyDeviceToDevice,
-                                    s0));
-        }
-        if (rank0_assembles) {
-            const uint32_t* frames = src[0];   // one shard: its displays are the frames
-            if (world > 1) {
-                const dim3 grid((W + 255) / 256, H, nframes);
-                deinterleave_kernel<<<grid, 256, 0, s0>>>(sr, L.frame, W, H, rb, world);
-                MHIP(hipGetLastError());
-                frames = L.frame;
-            }
-            if (outs)
-                for (int j = 0; j < nframes; j++)
-                    MHIP(hipMemcpyAsync(dst[j], frames + (size_t)j * frame_elems, 4 * frame_elems,
-                                        hipMemcpyDeviceToHost, s0));
-        }
-    } else if (outs) {
-        // host-direct: rank r's row blocks of frame j straight into outs[j]:
-        // its full blocks b = s, s + world, ... as one strided copy (rows of
-        // rb * W pixels, the destination pitch world * rb rows), the image's
-        // short last block (if it is this shard's) after it
+    } else if (J.deliver) {
+        // host-direct: this rank's row blocks of frame j straight into its
+        // host frame: its full blocks b = s, s + world, ... as one strided
+        // copy (rows of rb * W pixels, the destination pitch world * rb
+        // rows), the image's short last block (if it is this shard's) after it
+        const int W = J.W, H = J.H, rb = J.rb, world = J.world;
         const int blocks = (H + rb - 1) / rb;
         const int last = blocks - 1;
-        const bool short_last = H % rb != 0;
-        for (int r = 0; r < n; r++) {
-            const int s = shard[r];
-            const int nb = s < blocks ? (last - s) / world + 1 : 0;     // this shard's blocks
-            const bool has_short = short_last && nb > 0 && last % world == s;
-            const int nfull = nb - (has_short ? 1 : 0);
-            const size_t elems = (size_t)sr.rows[s] * W;
-            MHIP(hipSetDevice(m->dev[r]));
-            for (int j = 0; j < nframes; j++) {
-                const uint32_t* sj = src[r] + (size_t)j * elems;
-                uint32_t* dj = (uint32_t*)dst[j];
-                if (nfull > 0 && m->direct_copy == 0)
-                    MHIP(hipMemcpy2DAsync(dj + (size_t)s * rb * W, (size_t)world * rb * W * 4, sj, (size_t)rb * W * 4,
-                                          (size_t)rb * W * 4, nfull, hipMemcpyDeviceToHost, stream_of(L.ctx[r])));
-                for (int i = 0; m->direct_copy == 1 && i < nfull; i++)   // one copy per row block
-                    MHIP(hipMemcpyAsync(dj + ((size_t)i * world + s) * rb * W, sj + (size_t)i * rb * W,
-                                        (size_t)rb * W * 4, hipMemcpyDeviceToHost, stream_of(L.ctx[r])));
-                if (has_short)
-                    MHIP(hipMemcpyAsync(dj + (size_t)last * rb * W, sj + (size_t)nfull * rb * W,
-                                        (size_t)(H - last * rb) * W * 4, hipMemcpyDeviceToHost, stream_of(L.ctx[r])));
-            }
+        const int nb = s < blocks ? (last - s) / world + 1 : 0;     // this shard's blocks
+        const bool has_short = H % rb != 0 && nb > 0 && last % world == s;
+        const int nfull = nb - (has_short ? 1 : 0);
+        for (int j = 0; j < J.nframes; j++) {
+            const uint32_t* sj = src + (size_t)j * elems;
+            uint32_t* dj = (uint32_t*)J.dst[j];
+            if (nfull > 0 && m->direct_copy == 0)
+                MHIP(hipMemcpy2DAsync(dj + (size_t)s * rb * W, (size_t)world * rb * W * 4, sj, (size_t)rb * W * 4,
+                                      (size_t)rb * W * 4, nfull, hipMemcpyDeviceToHost, st));
+            for (int i = 0; m->direct_copy == 1 && i < nfull; i++)   // one copy per row block
+                MHIP(hipMemcpyAsync(dj + ((size_t)i * world + s) * rb * W, sj + (size_t)i * rb * W,
+                                    (size_t)rb * W * 4, hipMemcpyDeviceToHost, st));
+            if (has_short)
+                MHIP(hipMemcpyAsync(dj + (size_t)last * rb * W, sj + (size_t)nfull * rb * W,
+                                    (size_t)(H - last * rb) * W * 4, hipMemcpyDeviceToHost, st));
         }
     }
-    for (int r = 0; r < n; r++) {
-        MHIP(hipSetDevice(m->dev[r]));
-        MHIP(hipEventRecord(L.done[r], stream_of(L.ctx[r])));
+    MHIP(hipEventRecord(L.done[r], st));
+    return MIRT_OK;
+}
+
+// issue_rank_body with its outcome recorded on the lane: the first error
+// (with its message, which lives in this thread's error slot) and, on an
+// error, the completion event over whatever did reach the stream.
+void issue_rank(mirt_multi* m, Lane& L, int r)
+{
+    const int rc = issue_rank_body(m, L, r);
+    if (rc) {
+        (void)hipSetDevice(m->dev[r]);
+        (void)hipEventRecord(L.done[r], stream_of(L.ctx[r]));
+        (void)hipGetLastError();
+        if (!m->rccl && r > 0) L.slabs_ready[r]->store(L.seq, std::memory_order_release);   // rank 0 must not wait
+        std::lock_guard<std::mutex> lk(*L.err_mu);
+        if (!L.err) {
+            L.err = rc;
+            L.err_msg = mirt_last_error();
+        }
+    }
+    L.issued->fetch_add(1, std::memory_order_acq_rel);
+}
+
+void rank_thread_main(mirt_multi* m, int r)
+{
+    RankThread& w = *m->workers[r];
+    (void)hipSetDevice(m->dev[r]);
+    for (;;) {
+        int li;
+        {
+            std::unique_lock<std::mutex> lk(w.mu);
+            w.cv.wait(lk, [&] { return w.stop || !w.q.empty(); });
+            if (w.q.empty()) return;   // stop, nothing left
+            li = w.q.front();
+            w.q.pop_front();
+        }
+        issue_rank(m, m->lanes[li], r);
+    }
+}
+
+// Launch on lane li: prepared here, issued by every rank (its own thread
+// when n > 1).
+int enqueue(mirt_multi* m, int li, const mirt_camera* cam, const mirt_frame_desc* fd, int nframes, int flags,
+            mirt_rgba8* const* outs)
+{
+    Lane& L = m->lanes[li];
+    if (int rc = prepare(m, L, cam, fd, nframes, flags, outs)) return rc;
+    L.seq++;
+    L.err = MIRT_OK;
+    L.issued->store(0, std::memory_order_relaxed);
+    L.pending = true;
+    if (m->workers.empty()) {
+        for (int r = m->n - 1; r >= 0; r--) issue_rank(m, L, r);
+        return MIRT_OK;
+    }
+    for (int r = 0; r < m->n; r++) {
+        RankThread& w = *m->workers[r];
+        {
+            std::lock_guard<std::mutex> lk(w.mu);
+            w.q.push_back(li);
+        }
+        w.cv.notify_one();
     }
     return MIRT_OK;
 }
@@ -495,6 +637,8 @@ try {
         L.ctx.assign(n, nullptr);
         L.rendered.assign(n, nullptr);
         L.done.assign(n, nullptr);
+        L.src.assign(n, nullptr);
+        for (int r = 0; r < n; r++) L.slabs_ready.emplace_back(new std::atomic<uint64_t>(0));
         for (int r = 0; r < n; r++) {
             int rc = mirt_create(m->dev[r], &L.ctx[r]);
             if (rc) return fail(rc);
@@ -520,10 +664,19 @@ try {
             }
         }
     }
+    // one issuing thread per rank (n > 1)
+    if (n > 1)
+        for (int r = 0; r < n; r++) {
+            m->workers.emplace_back(new RankThread());
+            m->workers.back()->th = std::thread(rank_thread_main, m, r);
+        }
     *out = m;
     return MIRT_OK;
 } catch (const std::bad_alloc&) {
     set_error("mirt_multi_create: out of host memory");
+    return MIRT_E_NOMEM;
+} catch (const std::system_error&) {
+    set_error("mirt_multi_create: could not start the rank threads");
     return MIRT_E_NOMEM;
 }
 
@@ -531,13 +684,25 @@ void mirt_multi_destroy(mirt_multi* m)
 {
     if (!m) return;
     for (int l = 0; l < (int)m->lanes.size() && !m->failed; l++) (void)wait_lane(m, l);
+    for (auto& w : m->workers) {
+        {
+            std::lock_guard<std::mutex> lk(w->mu);
+            w->stop = true;
+        }
+        w->cv.notify_one();
+    }
     if (m->failed) {
-        // work may still be queued on a stuck device: freeing its buffers or
-        // destroying its streams would wait for it, so they are left to the
-        // process's exit (the communicators were aborted when it failed)
-        delete m;
+        // work may still be queued on a stuck device, and a rank thread may be
+        // inside a call that waits for it: freeing the buffers, destroying the
+        // streams or joining that thread would wait too, so they are left to
+        // the process's exit (the communicators were aborted when it failed)
+        // (the object itself stays allocated: a detached rank thread may
+        // still touch its lane and its queue)
+        for (auto& w : m->workers) w->th.detach();
         return;
     }
+    for (auto& w : m->workers) w->th.join();
+    m->workers.clear();
     for (Lane& L : m->lanes) {
         for (int r = 0; r < (int)L.ctx.size(); r++) {
             (void)hipSetDevice(m->dev[r]);
@@ -571,6 +736,11 @@ int mirt_multi_set_option(mirt_multi* m, int option, int value)
 {
     if (!multi_ok(m, "mirt_multi_set_option")) return MIRT_E_INVALID;
     if (m->failed) return failed_status(m, "mirt_multi_set_option");
+    // the rank threads read the options and the contexts while they issue a
+    // launch: change them only with no launch in flight
+    if (option != MIRT_MULTI_OPT_TIMEOUT_MS)
+        for (int l = 0; l < (int)m->lanes.size(); l++)
+            if (int rc = wait_lane(m, l)) return rc;
     switch (option) {
     case MIRT_MULTI_OPT_TIMEOUT_MS:
         if (value < 0) break;
@@ -579,8 +749,6 @@ int mirt_multi_set_option(mirt_multi* m, int option, int value)
     case MIRT_MULTI_OPT_EMULATE_WORLD:
         // launches in flight would mix shard geometries: only between frames
         if (value < 0 || value > kMaxShards || (value > 1 && m->n != 1)) break;
-        for (int l = 0; l < (int)m->lanes.size(); l++)
-            if (int rc = wait_lane(m, l)) return rc;
         m->emu_world = value;
         if (m->emu_rank >= std::max(1, value)) m->emu_rank = 0;
         return MIRT_OK;
@@ -590,8 +758,6 @@ int mirt_multi_set_option(mirt_multi* m, int option, int value)
         return MIRT_OK;
     case MIRT_MULTI_OPT_EMULATE_RANK:
         if (value < 0 || value >= std::max(1, m->emu_world)) break;
-        for (int l = 0; l < (int)m->lanes.size(); l++)
-            if (int rc = wait_lane(m, l)) return rc;
         m->emu_rank = value;
         return MIRT_OK;
     default:
@@ -647,10 +813,9 @@ try {
     const int li = m->next;
     if (int rc = wait_lane(m, li)) return rc;
     m->next = (m->next + 1) % (int)m->lanes.size();
-    Lane& L = m->lanes[li];
-    const int rc = enqueue(m, L, cam, fd, nframes, flags, outs);
-    if (rc && L.pending) mark_partial(m, L);
-    return rc;
+    // an error here (before any rank issued) leaves the lane as it was; the
+    // ranks' own issue errors come back from the lane's wait
+    return enqueue(m, li, cam, fd, nframes, flags, outs);
 } catch (const std::bad_alloc&) {
     set_error("mirt_multi_render_frames_async: out of host memory");
     return MIRT_E_NOMEM;
