@@ -119,7 +119,7 @@ TAIL_GRID = 0
 # at N > 1 a rank's launch is 1/N of a frame per frame carried. Round 4's
 # Python ranks gained from the burst's last 2 launches on the full grid
 # (profiles/r04g/); through mirt_multi (round 5, the per-shard emulation,
-# host-direct, best of three per shard, profiles/r05k/) it loses: the last
+# host-direct, best of three per shard, profiles/r05_logs/r05k/) it loses: the last
 # 0 / 1 / 2 launches on the full grid 15.51 / 14.91 / 14.82 Grays/s at N = 8
 TAIL_GRID_MULTI = 0
 KERNEL = "bounce_kernel<true, 2, false>"   # dominant kernel of the default (wavefront, four-wide) schedule
@@ -553,7 +553,7 @@ def prime(m, cam, bufs, per):
     """Untimed, before the warm-up steps: two launches per lane through every
     page-locked buffer and two without a delivery. A process's first frame
     loop into host memory ran ~9 ms slower than the same loop repeated
-    (profiles/r05f/n1_sweep.log: 4 lanes, K = 20, 1,635 -> 2,558 Mrays/s;
+    (profiles/r05_logs/r05f/n1_sweep.log: 4 lanes, K = 20, 1,635 -> 2,558 Mrays/s;
     device-only 2,557 -> 2,658), a one-off start-up cost of the copy path,
     not part of the steady frame loop the metric describes."""
     run_launches(m, cam, plan(0, 2 * m.lanes * per, per), bufs, DEPTH)

@@ -6,7 +6,8 @@ rate)), the figure that tells whether dependent chains and L2 misses hold the
 data-return unit longer per instruction, as the bounce kernel's 44% TD at 19%
 of the independent-gather peak suggests.
 
-    python scripts/td_mix_summary.py gpurun_out/r05e --json profiles/r05_td_mix.json
+    python scripts/td_mix_summary.py gpurun_out/r05n --json profiles/r05_td_mix.json
+    (or the committed copy: profiles/r05_logs/r05n)
 """
 import argparse
 import collections
@@ -24,6 +25,14 @@ def dispatches(root):
         for f in fs:
             if f.endswith("counter_collection.csv"):
                 rows += list(csv.DictReader(open(os.path.join(dp, f))))
+    return per_dispatch(rows)
+
+
+def dispatches_file(path):
+    return per_dispatch(list(csv.DictReader(open(path)))) if os.path.exists(path) else []
+
+
+def per_dispatch(rows):
     per = collections.defaultdict(dict)
     for r in rows:
         if "probe_mix" not in r["Kernel_Name"]:
@@ -40,7 +49,9 @@ def main():
     txt = open(os.path.join(a.out, "mix.json")).read()
     probe = json.loads(txt[txt.index("{"):])
     cases = probe["cases"]
-    passes = [dispatches(os.path.join(a.out, f"pmc.{i}")) for i in range(1, 5)]
+    # gpurun_out/<tag>/pmc.i/ (rocprofv3 -d) or the committed copy pmc.i.counter_collection.csv
+    passes = [dispatches(os.path.join(a.out, f"pmc.{i}")) if os.path.isdir(os.path.join(a.out, f"pmc.{i}"))
+              else dispatches_file(os.path.join(a.out, f"pmc.{i}.counter_collection.csv")) for i in range(1, 5)]
     for p_i, d in enumerate(passes):
         per_case = len(d) // len(cases) if d else 0
         for i, c in enumerate(cases):
@@ -61,7 +72,9 @@ def main():
             if "TCC_HIT_sum" in timed[0]:
                 h, mi = med("TCC_HIT_sum"), med("TCC_MISS_sum")
                 c["l2_hit"] = round(h / max(h + mi, 1.0), 4)
-    base = next((c for c in cases if c["dependent"] == 0 and c["cold_frac"] == 0 and c["active_lanes"] == 20), None)
+    base = next((c for c in cases if c["dependent"] == 0 and c["cold_frac"] == 0 and c["active_lanes"] == 20
+                 and not c.get("valu_fma_per_visit") and not c.get("lds_reads_per_visit")
+                 and not c.get("dword_loads_per_visit")), None)
     for c in cases:
         if base and "td_busy" in c:
             rel = c["ginst_per_s"] / base["ginst_per_s"]

@@ -50,24 +50,33 @@ __global__ void __launch_bounds__(256) probe(const uint4* __restrict__ tab, uint
 //   waves:  occupancy forced down by dynamic LDS (5 per SIMD as the kernel).
 __global__ void __launch_bounds__(256) probe_mix(const uint4* __restrict__ hot, const uint4* __restrict__ cold,
                                                  uint32_t hot_mask, uint32_t cold_mask, int active, int dep,
-                                                 uint32_t cold256, int iters, uint32_t* __restrict__ out)
+                                                 uint32_t cold256, int valu, int ldsr, int narrow, int iters,
+                                                 uint32_t* __restrict__ out)
 {
-    extern __shared__ uint32_t pad[];
+    extern __shared__ uint4 pad[];
     const uint32_t lane = threadIdx.x & 63;
     if ((int)lane >= active) return;
     uint32_t x = blockIdx.x * 977u + threadIdx.x * 131u + 1u;
     uint32_t acc = 0;
+    float f = (float)lane;
+    const uint32_t* hot32 = reinterpret_cast<const uint32_t*>(hot);
     for (int i = 0; i < iters; i++) {
         const uint32_t h = (x + (uint32_t)i * 7919u) * 2654435761u;
         const bool is_cold = ((h >> 24) & 0xffu) < cold256;
         const uint4* p = is_cold ? cold + 4 * ((h >> 4) & cold_mask) : hot + 4 * ((h >> 8) & hot_mask);
         const uint4 a = p[0], b = p[1], c = p[2], d = p[3];
-        const uint32_t v = (a.x ^ a.y ^ a.z ^ a.w) + (b.x ^ b.y ^ b.z ^ b.w) + (c.x ^ c.y ^ c.z ^ c.w) +
-                           (d.x ^ d.y ^ d.z ^ d.w);
+        uint32_t v = (a.x ^ a.y ^ a.z ^ a.w) + (b.x ^ b.y ^ b.z ^ b.w) + (c.x ^ c.y ^ c.z ^ c.w) +
+                     (d.x ^ d.y ^ d.z ^ d.w);
+        for (int k = 0; k < narrow; k++) v += hot32[(h >> (3 + k)) & (hot_mask * 16u + 15u)];   // dword gathers
+        for (int k = 0; k < ldsr; k++) {   // LDS-resident node reads (the walk's top levels)
+            const uint4 q = pad[(h >> (2 * k + 5)) & 1023u];
+            acc += q.x ^ q.w;
+        }
+        for (int k = 0; k < valu; k++) f = __builtin_fmaf(f, 1.0001f, (float)(v + k));   // slab-test ALU work
         acc += v;
         if (dep) x ^= v;   // the next address depends on this node's data
     }
-    if (acc == 0x12345678u) out[0] = acc + pad[0];
+    if (acc == 0x12345678u || f == 1.2345f) out[0] = acc;
 }
 
 int mix_main()
@@ -88,30 +97,36 @@ int mix_main()
     (void)hipDeviceGetAttribute(&clk_khz, hipDeviceAttributeClockRate, 0);
     const int blocks = 2048, threads = 256, iters = 256;
     printf("{\"probe\": \"scripts/td_probe.hip --mix\", \"cus\": %d, \"clock_khz\": %d, \"cases\": [", cus, clk_khz);
-    struct Case { int active, dep, cold256, waves; };
-    const Case cases[] = {{20, 0, 0, 8}, {20, 1, 0, 8}, {20, 1, 0, 5}, {20, 0, 33, 8}, {20, 1, 33, 5}, {20, 1, 33, 8},
-                          {64, 1, 0, 5}, {64, 0, 0, 8}};
+    struct Case { int active, dep, cold256, waves, valu, ldsr, narrow; };
+    const Case cases[] = {{20, 0, 0, 8, 0, 0, 0},  {20, 1, 0, 8, 0, 0, 0},  {20, 1, 0, 5, 0, 0, 0},
+                          {20, 0, 33, 8, 0, 0, 0}, {20, 1, 33, 5, 0, 0, 0}, {20, 1, 33, 8, 0, 0, 0},
+                          {64, 1, 0, 5, 0, 0, 0},  {64, 0, 0, 8, 0, 0, 0},
+                          // round 5, session n: the walk's other work beside its gathers
+                          {20, 1, 33, 5, 48, 0, 0}, {20, 1, 33, 5, 0, 4, 0}, {20, 1, 33, 5, 0, 0, 2},
+                          {20, 1, 33, 5, 48, 4, 2}, {20, 0, 0, 8, 48, 0, 0}, {20, 0, 0, 5, 0, 4, 0}};
     bool first = true;
     for (const Case& c : cases) {
         // dynamic LDS sized so that only c.waves waves (workgroups / 4 x 4 SIMDs) fit a CU's 160 KB
-        const size_t lds = c.waves >= 8 ? 0 : (160 * 1024) / (size_t)c.waves - 256;
+        size_t lds = c.waves >= 8 ? 0 : (160 * 1024) / (size_t)c.waves - 256;
+        if (c.ldsr && lds < 16384) lds = 16384;   // the reads' 1024 x 16 B
         float best = 1e30f;
         for (int rep = 0; rep < 3; rep++) {
             probe_mix<<<blocks, threads, lds>>>(hot, cold, hot_nodes - 1, cold_nodes - 1, c.active, c.dep, c.cold256,
-                                                iters, out);
+                                                c.valu, c.ldsr, c.narrow, iters, out);
             (void)hipEventRecord(e0);
             probe_mix<<<blocks, threads, lds>>>(hot, cold, hot_nodes - 1, cold_nodes - 1, c.active, c.dep, c.cold256,
-                                                iters, out);
+                                                c.valu, c.ldsr, c.narrow, iters, out);
             (void)hipEventRecord(e1);
             (void)hipEventSynchronize(e1);
             float ms = 0;
             (void)hipEventElapsedTime(&ms, e0, e1);
             if (ms < best) best = ms;
         }
-        const double inst = (double)blocks * (threads / 64) * iters * 4;
+        const double inst = (double)blocks * (threads / 64) * iters * (4 + c.narrow);
         printf("%s\n  {\"active_lanes\": %d, \"dependent\": %d, \"cold_frac\": %.3f, \"waves_per_simd\": %d, "
+               "\"valu_fma_per_visit\": %d, \"lds_reads_per_visit\": %d, \"dword_loads_per_visit\": %d, "
                "\"lds_bytes\": %zu, \"ms\": %.4f, \"wave_load_instructions\": %.0f, \"ginst_per_s\": %.3f}",
-               first ? "" : ",", c.active, c.dep, c.cold256 / 256.0, c.waves, lds, best, inst,
+               first ? "" : ",", c.active, c.dep, c.cold256 / 256.0, c.waves, c.valu, c.ldsr, c.narrow, lds, best, inst,
                inst / (best * 1e-3) / 1e9);
         first = false;
     }
