@@ -69,6 +69,9 @@ def main():
             if "SQ_INSTS_VMEM_RD" in timed[0]:
                 c["tcp_accesses_per_instruction"] = round(med("TCP_TOTAL_CACHE_ACCESSES_sum") / med("SQ_INSTS_VMEM_RD"), 3)
                 c["wait_any_per_wave_cycle"] = round(med("SQ_WAIT_ANY") / med("SQ_WAVE_CYCLES"), 4)
+                if "SQ_INSTS_VALU" in timed[0]:
+                    c["valu_per_vmem_rd"] = round(med("SQ_INSTS_VALU") / med("SQ_INSTS_VMEM_RD"), 2)
+                    c["lds_per_vmem_rd"] = round(med("SQ_INSTS_LDS") / med("SQ_INSTS_VMEM_RD"), 3)
             if "TCC_HIT_sum" in timed[0]:
                 h, mi = med("TCC_HIT_sum"), med("TCC_MISS_sum")
                 c["l2_hit"] = round(h / max(h + mi, 1.0), 4)

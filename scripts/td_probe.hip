@@ -95,20 +95,26 @@ int mix_main()
     int cus = 0, clk_khz = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
     (void)hipDeviceGetAttribute(&clk_khz, hipDeviceAttributeClockRate, 0);
-    const int blocks = 2048, threads = 256, iters = 256;
+    const int threads = 256;
     printf("{\"probe\": \"scripts/td_probe.hip --mix\", \"cus\": %d, \"clock_khz\": %d, \"cases\": [", cus, clk_khz);
-    struct Case { int active, dep, cold256, waves, valu, ldsr, narrow; };
+    struct Case { int active, dep, cold256, waves, valu, ldsr, narrow, blocks = 2048, iters = 256; };
     const Case cases[] = {{20, 0, 0, 8, 0, 0, 0},  {20, 1, 0, 8, 0, 0, 0},  {20, 1, 0, 5, 0, 0, 0},
                           {20, 0, 33, 8, 0, 0, 0}, {20, 1, 33, 5, 0, 0, 0}, {20, 1, 33, 8, 0, 0, 0},
                           {64, 1, 0, 5, 0, 0, 0},  {64, 0, 0, 8, 0, 0, 0},
                           // round 5, session n: the walk's other work beside its gathers
                           {20, 1, 33, 5, 48, 0, 0}, {20, 1, 33, 5, 0, 4, 0}, {20, 1, 33, 5, 0, 0, 2},
-                          {20, 1, 33, 5, 48, 4, 2}, {20, 0, 0, 8, 48, 0, 0}, {20, 0, 0, 5, 0, 4, 0}};
+                          {20, 1, 33, 5, 48, 4, 2}, {20, 0, 0, 8, 48, 0, 0}, {20, 0, 0, 5, 0, 4, 0},
+                          // the bounce kernel's own mix per visit (counter pass of the 1080p/10k timed
+                          // launch: 50.7 VALU and 1 LDS instruction per vector load) at its occupancy
+                          // in one launch (384 workgroups of 256 = 1.5 waves per SIMD), then fuller
+                          {20, 1, 33, 8, 200, 4, 0, 384, 1024}, {20, 1, 33, 8, 200, 4, 0, 768, 512},
+                          {20, 1, 33, 5, 200, 4, 0, 2048, 256}, {20, 1, 33, 8, 200, 0, 0, 384, 1024}};
     bool first = true;
     for (const Case& c : cases) {
         // dynamic LDS sized so that only c.waves waves (workgroups / 4 x 4 SIMDs) fit a CU's 160 KB
         size_t lds = c.waves >= 8 ? 0 : (160 * 1024) / (size_t)c.waves - 256;
         if (c.ldsr && lds < 16384) lds = 16384;   // the reads' 1024 x 16 B
+        const int blocks = c.blocks, iters = c.iters;
         float best = 1e30f;
         for (int rep = 0; rep < 3; rep++) {
             probe_mix<<<blocks, threads, lds>>>(hot, cold, hot_nodes - 1, cold_nodes - 1, c.active, c.dep, c.cold256,
@@ -125,8 +131,10 @@ int mix_main()
         const double inst = (double)blocks * (threads / 64) * iters * (4 + c.narrow);
         printf("%s\n  {\"active_lanes\": %d, \"dependent\": %d, \"cold_frac\": %.3f, \"waves_per_simd\": %d, "
                "\"valu_fma_per_visit\": %d, \"lds_reads_per_visit\": %d, \"dword_loads_per_visit\": %d, "
+               "\"workgroups\": %d, \"visits_per_lane\": %d, "
                "\"lds_bytes\": %zu, \"ms\": %.4f, \"wave_load_instructions\": %.0f, \"ginst_per_s\": %.3f}",
-               first ? "" : ",", c.active, c.dep, c.cold256 / 256.0, c.waves, c.valu, c.ldsr, c.narrow, lds, best, inst,
+               first ? "" : ",", c.active, c.dep, c.cold256 / 256.0, c.waves, c.valu, c.ldsr, c.narrow, blocks, iters,
+               lds, best, inst,
                inst / (best * 1e-3) / 1e9);
         first = false;
     }
