@@ -32,8 +32,9 @@ ranks hold no GPU work and join rank 0 only at a gloo barrier at the end.
 
 The schedule: `pipeline` lanes (4 at N = 1, 8 at N > 1), each
 context's bounce pass at 1.5 persistent workgroups per CU, `batch` frames
-per launch (1 at N <= 2, 4 at N >= 4), the burst's last `tail_grid`
-launches on the full grid at N > 1 (mirt_multi's MIRT_MULTI_FULL_GRID).
+per launch (1 at N <= 2, 4 at N >= 4); `--tail-grid T` puts the burst's
+last T launches on the full grid (MIRT_MULTI_FULL_GRID; 0 by default: it
+lost through mirt_multi in round 5's emulation).
 
 Also in the line: `device_resident_mrays_s` (the same loop with the frames
 left in device 0's HBM: the previous rounds' headline), depth 1, the
