@@ -335,7 +335,7 @@ int prepare(mirt_multi* m, Lane& L, const mirt_camera* cam, const mirt_frame_des
                 if (L.stage) MHIP(hipHostFree(L.stage));
                 L.stage = nullptr;
                 L.stage_cap = 0;
-                MHIP(hipHostMalloc((void**)&L.stage, fb * nframes, hipHostMallocDefault));
+                MHIP(hipHostMalloc((void**)&L.stage, fb * nframes, hipHostMallocPortable));
                 L.stage_cap = fb * nframes;
             }
             J.dst[j] = (mirt_rgba8*)(L.stage + fb * j);

@@ -2590,7 +2590,7 @@ int mirt_host_alloc(size_t bytes, void** out)
 {
     if (!out) return MIRT_E_INVALID;
     *out = nullptr;
-    HIP_TRY(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocPortable));   // pinned for every device (mirt_multi host-direct)
     mirt::pinned_add(*out, bytes ? bytes : 1);
     return MIRT_OK;
 }
@@ -2608,7 +2608,7 @@ int mirt_host_register(void* p, size_t bytes)
         set_error("mirt_host_register: invalid arguments");
         return MIRT_E_INVALID;
     }
-    HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterDefault));
+    HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterPortable));
     mirt::pinned_add(p, bytes);
     return MIRT_OK;
 }

@@ -851,6 +851,95 @@ __device__ __forceinline__ bool visit_child(const DevScene& sc, const SlabRay& s
     return slab_box<FAST>(sr, pr, s0, s1, s2, s3, s4, s5, near);
 }
 
+// MIRT_PACKET_PREFETCH (round 5): the packet walk's next
+// data requested through the VECTOR memory path at the start of each step,
+// while the step's box tests run. One global_load_dword per step, lanes
+// [16k, 16k + 16) loading target k's 64 B: k = 0 / 1 the node's two children
+// (an inner child's PNode, a leaf child's sphere), k = 2 the PNode on top of
+// the packet's stack (the target of a pop). Whatever the step decides --
+// descend into either child, pop, or gate a leaf -- its data is then in
+// flight already, so a step waits for ONE load issued before its tests
+// instead of a chain of scalar loads (node, then the leaf's sphere, then the
+// next node) each behind its own s_waitcnt; the values reach the scalar unit
+// by v_readlane. The vector path is nearly idle in this kernel (TD 9% busy).
+// Measured (profiles/r05_logs/r05p/): byte-identical, but the
+// packet launch alone 0.328 -> 0.452 ms at 8 waves per SIMD (13 VGPRs and 19
+// SGPRs spilled) and 0.455 at 7 (no VGPR spills): a vector round trip plus
+// the v_readlane chain is longer than the scalar loads it replaces, which
+// mostly hit the scalar cache. Off by default, kept as a build switch.
+#ifndef MIRT_PACKET_PREFETCH
+#define MIRT_PACKET_PREFETCH 0
+#endif
+
+__device__ __forceinline__ uint32_t readlane_u(uint32_t v, uint32_t l)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
+
+__device__ __forceinline__ PNodeV pnode_from_lanes(uint32_t v, uint32_t b)
+{
+    PNodeV n;
+    n.a0 = __uint_as_float(readlane_u(v, b + 0));
+    n.a1 = __uint_as_float(readlane_u(v, b + 1));
+    n.a2 = __uint_as_float(readlane_u(v, b + 2));
+    n.a3 = __uint_as_float(readlane_u(v, b + 3));
+    n.a4 = __uint_as_float(readlane_u(v, b + 4));
+    n.a5 = __uint_as_float(readlane_u(v, b + 5));
+    n.b0 = __uint_as_float(readlane_u(v, b + 6));
+    n.b1 = __uint_as_float(readlane_u(v, b + 7));
+    n.b2 = __uint_as_float(readlane_u(v, b + 8));
+    n.b3 = __uint_as_float(readlane_u(v, b + 9));
+    n.b4 = __uint_as_float(readlane_u(v, b + 10));
+    n.b5 = __uint_as_float(readlane_u(v, b + 11));
+    n.r0 = readlane_u(v, b + 12);
+    n.r1 = readlane_u(v, b + 13);
+    n.flat = readlane_u(v, b + 14);
+    n.end = readlane_u(v, b + 15);
+    return n;
+}
+
+// The dword lane `w` (0..15) of a prefetch target loads: an inner child's
+// PNode word w, a leaf child's sphere word w & 3, nothing useful for kPNone
+// (a valid address all the same).
+__device__ __forceinline__ const uint32_t* prefetch_word(const DevScene& sc, uint32_t ref, uint32_t w)
+{
+    if (ref == kPNone) return (const uint32_t*)sc.pnodes + w;
+    if (ref & kPLeaf) return (const uint32_t*)(sc.geo + (ref & kPIndex)) + (w & 3u);
+    return (const uint32_t*)(sc.pnodes + ref) + w;
+}
+
+// visit_child with the leaf's sphere taken from the prefetch register
+// (lanes b .. b + 3) instead of a load of its own.
+template <bool FAST, bool COUNT>
+__device__ __forceinline__ bool visit_child_pf(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
+                                               uint32_t ref, float s0, float s1, float s2, float s3, float s4,
+                                               float s5, uint32_t pf, uint32_t b, float& near, float& best_t,
+                                               int& best_s, Counters& cnt)
+{
+    if (ref == kPNone) return false;
+    if (ref & kPLeaf) {
+        if (COUNT) cnt.nodes++;
+        const int si = (int)(ref & kPIndex);
+        if (MIRT_PNODE_INLINE && (ref & kPInline)) {
+            if (slab_box<FAST>(sr, pr, s0 - s3, s1 - s3, s2 - s3, s0 + s3, s1 + s3, s2 + s3, near)) {
+                if (COUNT) cnt.spheres++;
+                consider_sphere<FAST>(sc, sp, pr, sr.ox, sr.oy, sr.oz, si, make_float4(s0, s1, s2, s3), best_t,
+                                      best_s);
+            }
+        } else if (slab_box<FAST>(sr, pr, s0, s1, s2, s3, s4, s5, near)) {
+            if (COUNT) cnt.spheres++;
+            const float4 g = make_float4(__uint_as_float(readlane_u(pf, b)), __uint_as_float(readlane_u(pf, b + 1)),
+                                         __uint_as_float(readlane_u(pf, b + 2)),
+                                         __uint_as_float(readlane_u(pf, b + 3)));
+            consider_sphere<FAST>(sc, sp, pr, sr.ox, sr.oy, sr.oz, si, g, best_t, best_s);
+        }
+        return false;
+    }
+    if (COUNT) cnt.nodes++;
+    if (FAST) return slab_cons(sr, pr, s0, s1, s2, s3, s4, s5, near);
+    return slab_box<FAST>(sr, pr, s0, s1, s2, s3, s4, s5, near);
+}
+
 // Ordered closest hit of a wave of rays walked as one packet (camera rays),
 // over PNodes with scalar loads. `mask` holds the lanes that passed every
 // box on the path to the current node, so a lane tests a child only when
@@ -875,6 +964,67 @@ __device__ __forceinline__ void closest_packet_ordered(const DevScene& sc, const
     uint32_t cur = 0;
     uint32_t top = 0;
     uint32_t st_node = 0, st_lo = 0, st_hi = 0;
+#if MIRT_PACKET_PREFETCH
+    (void)cur;
+    // the current node lives in lanes [cb, cb + 16) of the VGPR `nv` (one
+    // register instead of 16 SGPRs); its words are read where they are used
+    uint32_t nv = *((const uint32_t*)sc.pnodes + (lane & 15u));
+    uint32_t cb = 0;
+    const uint32_t seg = lane >> 4, w = lane & 15u;
+    while (mask) {
+        if (COUNT) cnt.steps++;
+        const uint32_t r0 = readlane_u(nv, cb + 12), r1 = readlane_u(nv, cb + 13);
+        // this step's possible next data: both children, and the stack's top
+        const uint32_t pop_node = top > 0 ? readlane_u(st_node, top - 1) : kPNone;
+        const uint32_t tgt = seg == 0 ? r0 : (seg == 1 ? r1 : pop_node);
+        uint32_t pf = 0;
+        if (seg < 3) pf = *prefetch_word(sc, tgt, w);
+        const bool in = (mask >> lane) & 1;
+        float e0 = 0.0f, e1 = 0.0f;
+        bool h0 = false, h1 = false;
+        if (in) {
+            h0 = visit_child_pf<FAST, COUNT>(sc, sr, sp, pr, r0, __uint_as_float(readlane_u(nv, cb + 0)),
+                                             __uint_as_float(readlane_u(nv, cb + 1)),
+                                             __uint_as_float(readlane_u(nv, cb + 2)),
+                                             __uint_as_float(readlane_u(nv, cb + 3)),
+                                             __uint_as_float(readlane_u(nv, cb + 4)),
+                                             __uint_as_float(readlane_u(nv, cb + 5)), pf, 0u, e0, best_t, best_s, cnt);
+            h1 = visit_child_pf<FAST, COUNT>(sc, sr, sp, pr, r1, __uint_as_float(readlane_u(nv, cb + 6)),
+                                             __uint_as_float(readlane_u(nv, cb + 7)),
+                                             __uint_as_float(readlane_u(nv, cb + 8)),
+                                             __uint_as_float(readlane_u(nv, cb + 9)),
+                                             __uint_as_float(readlane_u(nv, cb + 10)),
+                                             __uint_as_float(readlane_u(nv, cb + 11)), pf, 16u, e1, best_t, best_s,
+                                             cnt);
+        }
+        const uint64_t m0 = __ballot(h0), m1 = __ballot(h1);
+        if (m0 && m1) {
+            const uint64_t both = m0 & m1;
+            const uint64_t v = __ballot(((both >> lane) & 1) && e1 < e0);
+            const bool swap = 2 * __popcll(v) > __popcll(both);
+            const uint32_t second = swap ? r0 : r1;
+            const uint64_t sm = swap ? m0 : m1;
+            if (lane == top) {
+                st_node = second;
+                st_lo = (uint32_t)sm;
+                st_hi = (uint32_t)(sm >> 32);
+            }
+            top++;
+            mask = swap ? m1 : m0;
+            cb = swap ? 16u : 0u;
+        } else if (m0 | m1) {
+            mask = m0 | m1;
+            cb = m0 ? 0u : 16u;
+        } else if (top > 0) {
+            top--;
+            mask = ((uint64_t)readlane_u(st_hi, top) << 32) | (uint64_t)readlane_u(st_lo, top);
+            cb = 32u;
+        } else {
+            break;
+        }
+        nv = pf;
+    }
+#else
     while (mask) {
         if (COUNT) cnt.steps++;
         const PNodeV nd = load_pnode_uniform(sc.pnodes, cur);
@@ -915,6 +1065,7 @@ __device__ __forceinline__ void closest_packet_ordered(const DevScene& sc, const
             break;
         }
     }
+#endif
 }
 
 // Per-lane DFS walk (any tree, the reference order): `cur` is the next flat

@@ -13,7 +13,7 @@ while [ $# -ge 2 ]; do
     rm -rf "$obj"; mkdir -p "$obj"
     common="-O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function $flags"
     for f in host_scene bvh_build bvh_cache dropin; do
-        /opt/rocm/bin/hipcc $common -c "$CSRC/$f.cpp" -o "$obj/$f.o" &
+        /opt/rocm/bin/hipcc $common --offload-arch=gfx950 -c "$CSRC/$f.cpp" -o "$obj/$f.o" &
     done
     for f in render multi; do
         /opt/rocm/bin/hipcc $common --offload-arch=gfx950 -c "$CSRC/$f.hip" -o "$obj/$f.o" &
