@@ -1083,6 +1083,9 @@ struct DfsWalk {
 #ifndef MIRT_WIDE_STACK
 #define MIRT_WIDE_STACK 20
 #endif
+#ifndef MIRT_EXTRA_NODE_LOAD
+#define MIRT_EXTRA_NODE_LOAD 0
+#endif
 constexpr int kWideStack = MIRT_WIDE_STACK;
 constexpr int kWideStride = 256;  // threads per workgroup of the bounce kernel
 struct WideWalk {
@@ -1210,6 +1213,19 @@ __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay
             s1 = p[1];
             s2 = p[2];
             s3 = p[3];
+#if MIRT_EXTRA_NODE_LOAD
+            // sensitivity probe (pricing a three-load node format):
+            // one more load instruction per visit, 1 = a word of the same
+            // node, 2 = a word of the neighbouring HNode (another 64-B line)
+            {
+                uint32_t z;   // an offset of 0 the compiler cannot see, so the load is not merged
+                asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+                const uint32_t* xp =
+                    (const uint32_t*)(sc.hnodes + (MIRT_EXTRA_NODE_LOAD == 2 ? (w.cur ^ 1u) : w.cur)) + z;
+                const uint32_t x = *xp;
+                asm volatile("" ::"v"(x));
+            }
+#endif
         }
         auto test = [&](const uint4& q, float& e) {
             if (COUNT && q.w != kPNone) cnt.nodes++;
