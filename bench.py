@@ -123,6 +123,10 @@ TAIL_GRID = 0
 # host-direct, best of three per shard, profiles/r05_logs/r05k/) it loses: the last
 # 0 / 1 / 2 launches on the full grid 15.51 / 14.91 / 14.82 Grays/s at N = 8
 TAIL_GRID_MULTI = 0
+# MIRT_MULTI_QUEUE_AHEAD: each context takes its next launch behind the
+# current one on its stream (own slabs, copies on a copy stream), so no
+# context idles through its frame's D2H and the host's turnaround
+QUEUE_AHEAD, QUEUE_AHEAD_MULTI = False, False
 KERNEL = "bounce_kernel<true, 2, false>"   # dominant kernel of the default (wavefront, four-wide) schedule
 # the PMC-derived bound of the timed launch shape, per workload
 # (scripts/pmc_bench.sh over this script's own command + scripts/pmc_summary.py);
@@ -629,8 +633,8 @@ def make_scene():
     return spheres, bvh, time.perf_counter() - t0
 
 
-def open_multi(n, lanes, host_direct, spheres, bvh, blocks, opts, timeout_ms=120000):
-    m = mirt.MultiRenderer(list(range(n)), lanes=lanes, host_direct=host_direct)
+def open_multi(n, lanes, host_direct, spheres, bvh, blocks, opts, timeout_ms=120000, ahead=False):
+    m = mirt.MultiRenderer(list(range(n)), lanes=lanes, host_direct=host_direct, queue_ahead=ahead)
     m.set_option(mirt.abi.MULTI_OPT_TIMEOUT_MS, timeout_ms)
     m.upload(spheres, bvh)
     if blocks >= 0:
@@ -655,6 +659,11 @@ def frames_per_launch(args, n):
     if SPP > 1 and not args.accumulate:
         return 1             # one fresh frame of SPP samples per launch (the fold restarts per launch)
     return args.batch if args.batch > 0 else DEFAULT_BATCH.get(n, 1 if n <= 2 else 4)
+
+
+def queue_ahead(args, n):
+    """MIRT_MULTI_QUEUE_AHEAD for the timed loop (two launch slots per context)."""
+    return bool(args.queue_ahead) if args.queue_ahead >= 0 else (QUEUE_AHEAD if n == 1 else QUEUE_AHEAD_MULTI)
 
 
 def schedule(args, n):
@@ -694,8 +703,9 @@ def measure(args):
     lanes, per, tail_n, blocks = schedule(args, n)
     spheres, bvh, build_s = make_scene()
     cam = mirt.default_camera()
-    m = open_multi(n, lanes, delivery == "host-direct", spheres, bvh, blocks, args.opt)
-    bufs = host_bufs(lanes, per)
+    ahead = queue_ahead(args, n)
+    m = open_multi(n, lanes, delivery == "host-direct", spheres, bvh, blocks, args.opt, ahead=ahead)
+    bufs = host_bufs(m.lanes, per)
     prime(m, cam, bufs, per)
     warm = plan(0, args.warmup, per)
     timed_launches = plan(args.warmup, args.steps, per)
@@ -706,8 +716,8 @@ def measure(args):
     # the passes of rank 0's timed launches (HIP events on each launch's own
     # stream, under the overlap of the lanes in flight)
     phases = []
-    for lane in range(lanes):
-        k_lane = sum(1 for i in range(len(warm), len(warm) + len(timed_launches)) if i % lanes == lane)
+    for lane in range(lanes):   # the context sets (with queue-ahead two launch slots share one)
+        k_lane = sum(1 for i in range(len(warm), len(warm) + len(timed_launches)) if i % m.lanes % lanes == lane)
         if k_lane:
             phases += m.phase_log(lane, 0, min(k_lane, 64))
     primary_ms, bounce_ms = (float(v) for v in np.mean(np.array(phases), axis=0)) if phases else (0.0, 0.0)
@@ -741,8 +751,9 @@ def measure(args):
         other = {"delivery": od}
         m2 = bufs2 = None
         try:
-            m2 = open_multi(n, lanes, od == "host-direct", spheres, bvh, blocks, args.opt, timeout_ms=60000)
-            bufs2 = host_bufs(lanes, per)
+            m2 = open_multi(n, lanes, od == "host-direct", spheres, bvh, blocks, args.opt, timeout_ms=60000,
+                            ahead=ahead)
+            bufs2 = host_bufs(m2.lanes, per)
             prime(m2, cam, bufs2, per)
             tl2 = plan(args.warmup, args.steps, per)
             el2 = timed_loop(m2, cam, plan(0, args.warmup, per), tl2, bufs2, DEPTH, args.accumulate, tail)
@@ -784,7 +795,8 @@ def measure(args):
         "config": {"workload": WORKLOADS[WORKLOAD]["desc"], "name": WORKLOAD,
                    "width": W, "height": H, "spheres": NSPH, "scene": KIND, "max_depth": DEPTH, "spp": SPP,
                    "jitter": JITTER, "frames_per_step": 1, "frames_per_launch": per,
-                   "launches": len(timed_launches), "pipeline": lanes, "bounce_blocks": blocks,
+                   "launches": len(timed_launches), "pipeline": lanes, "queue_ahead": ahead,
+                   "bounce_blocks": blocks,
                    "tail_grid": len(tail), "bvh_nodes": len(bvh), "row_block": ROW_BLOCK,
                    "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                    "delivery": delivery,
@@ -957,6 +969,8 @@ def main():
                          "BB_PER_CU (1.5 unless stated) per CU with lanes > 1, else 0 (occupancy x CUs)")
     ap.add_argument("--batch", type=int, default=0,
                     help="frames per launch (0 = DEFAULT_BATCH[N])")
+    ap.add_argument("--queue-ahead", type=int, default=-1,
+                    help="1: two launch slots per context (MIRT_MULTI_QUEUE_AHEAD), 0: one; default per N")
     ap.add_argument("--tail-grid", type=int, default=-1,
                     help="the last N launches of the timed burst take the full persistent bounce grid; -1 = "
                          "TAIL_GRID at N = 1, TAIL_GRID_MULTI at N > 1")

@@ -199,6 +199,6 @@ OPT_TRAVERSAL, OPT_FAST_SLAB, OPT_BLOCK_WAVES, OPT_DEFER, OPT_BOUNCE_THRESHOLD, 
 OPT_BOUNCE_BLOCKS, OPT_QUAD_DRAIN, OPT_LEAF_BATCH, OPT_QUAD_BATCH, OPT_ZERO_COPY = 9, 11, 14, 15, 17
 OPT_QUEUE_ORDER, OPT_DEBUG_STALL_MS, OPT_CONT_QUEUE = 18, 19, 20
 TRAV_TILE, TRAV_WAVEFRONT = 0, 5
-MULTI_COPY, MULTI_HOST_DIRECT = 1, 2
+MULTI_COPY, MULTI_HOST_DIRECT, MULTI_QUEUE_AHEAD = 1, 2, 4
 MULTI_FULL_GRID = 1
 MULTI_OPT_TIMEOUT_MS, MULTI_OPT_EMULATE_WORLD, MULTI_OPT_EMULATE_RANK, MULTI_OPT_DIRECT_COPY = 256, 257, 258, 259

@@ -117,8 +117,17 @@ struct Launch {
 // on rank 0, the copy-mode events and each rank's completion event.
 struct Lane {
     std::vector<mirt_ctx*> ctx;       // rank r's context (device dev[r], its own stream)
+    bool owns_ctx = true;             // MIRT_MULTI_QUEUE_AHEAD: lanes l and l + contexts share lane l's contexts
     std::vector<hipEvent_t> rendered; // copy mode: rank r's slabs are complete
-    std::vector<hipEvent_t> done;     // rank r's stream: the launch's last operation there
+    std::vector<hipEvent_t> done;     // rank r: the launch's last operation (on the copy stream with QUEUE_AHEAD)
+    // MIRT_MULTI_QUEUE_AHEAD: this lane's own display slabs per rank (the
+    // context's stream renders the next lane's launch into ITS slabs while
+    // this one's copies run), the copy stream and the event it waits on
+    std::vector<uint32_t*> slab;
+    std::vector<size_t> slab_cap;
+    std::vector<hipStream_t> cstream;
+    std::vector<hipEvent_t> kdone;
+    std::vector<char> kdone_set;      // rank r's copy stream already waits for this launch (rank r's thread only)
     uint32_t* gathered = nullptr;     // rank 0: every shard's displays
     size_t gathered_cap = 0;
     uint32_t* frame = nullptr;        // rank 0: the de-interleaved frames
@@ -166,6 +175,8 @@ struct RankThread {
 
 struct mirt_multi {
     int n = 0;
+    int nctx = 0;                     // context sets (the `lanes` argument)
+    bool ahead = false;               // MIRT_MULTI_QUEUE_AHEAD: 2 x nctx lanes, two launches per context
     std::vector<int> dev;
     bool rccl = false;
     bool direct = false;              // MIRT_MULTI_HOST_DIRECT
@@ -345,6 +356,23 @@ int prepare(mirt_multi* m, Lane& L, const mirt_camera* cam, const mirt_frame_des
     return MIRT_OK;
 }
 
+// Where rank r's delivery copies of lane L go: the context's stream, or with
+// MIRT_MULTI_QUEUE_AHEAD the lane's copy stream, made to wait (once per
+// launch) for everything the context's stream has been given so far -- so the
+// next lane's launch on the same context starts its kernels while these
+// copies run.
+hipStream_t copy_stream(mirt_multi* m, Lane& L, int r)
+{
+    const hipStream_t st = stream_of(L.ctx[r]);
+    if (!m->ahead) return st;
+    if (!L.kdone_set[r]) {
+        (void)hipEventRecord(L.kdone[r], st);
+        (void)hipStreamWaitEvent(L.cstream[r], L.kdone[r], 0);
+        L.kdone_set[r] = 1;
+    }
+    return L.cstream[r];
+}
+
 // Rank r's part of lane L's current launch, on its own device and stream:
 // its row blocks of every frame, then its share of the delivery, then the
 // completion event. Called by rank r's thread (or, for one rank, the
@@ -359,13 +387,21 @@ int issue_rank_body(mirt_multi* m, Lane& L, int r)
     sd.shard = s;
     mirt_ctx* c = L.ctx[r];
     hipStream_t st = stream_of(c);
+    if (m->ahead) L.kdone_set[r] = 0;
     int keep = 0;
     if (J.flags & MIRT_MULTI_FULL_GRID) {
         keep = mirt_get_option(c, MIRT_OPT_BOUNCE_BLOCKS);
         (void)mirt_set_option(c, MIRT_OPT_BOUNCE_BLOCKS, 0);
     }
     uint32_t* disp = nullptr;
-    int rc = enqueue_frame_device(c, &J.cam, &sd, nullptr, &disp, "mirt_multi_render_frames_async", J.nframes > 1);
+    uint32_t* out = nullptr;
+    if (m->ahead) {
+        // the lane's own slabs: every frame of the launch (spp * nframes samples)
+        const size_t need = 4 * elems * (size_t)std::max(1, sd.samples) + 4;
+        if (int g = grow(m->dev[r], &L.slab[r], &L.slab_cap[r], need)) return g;
+        out = L.slab[r];
+    }
+    int rc = enqueue_frame_device(c, &J.cam, &sd, out, &disp, "mirt_multi_render_frames_async", J.nframes > 1);
     if (J.flags & MIRT_MULTI_FULL_GRID) (void)mirt_set_option(c, MIRT_OPT_BOUNCE_BLOCKS, keep);
     if (rc) return rc;
     uint32_t* src = disp - (size_t)(J.nframes - 1) * elems;   // spp == 1 when nframes > 1: slab j = frame j
@@ -449,10 +485,12 @@ int issue_rank_body(mirt_multi* m, Lane& L, int r)
                     MHIP(hipGetLastError());
                     frames = L.frame;
                 }
-                if (J.deliver)
+                if (J.deliver) {
+                    const hipStream_t cs = copy_stream(m, L, r);
                     for (int j = 0; j < J.nframes; j++)
                         MHIP(hipMemcpyAsync(J.dst[j], frames + (size_t)j * J.frame_elems, 4 * J.frame_elems,
-                                            hipMemcpyDeviceToHost, st));
+                                            hipMemcpyDeviceToHost, cs));
+                }
             }
         }
     } else if (J.deliver) {
@@ -466,6 +504,7 @@ int issue_rank_body(mirt_multi* m, Lane& L, int r)
         const int nb = s < blocks ? (last - s) / world + 1 : 0;     // this shard's blocks
         const bool has_short = H % rb != 0 && nb > 0 && last % world == s;
         const int nfull = nb - (has_short ? 1 : 0);
+        st = copy_stream(m, L, r);   // the copies (with QUEUE_AHEAD on the lane's copy stream)
         for (int j = 0; j < J.nframes; j++) {
             const uint32_t* sj = src + (size_t)j * elems;
             uint32_t* dj = (uint32_t*)J.dst[j];
@@ -480,7 +519,9 @@ int issue_rank_body(mirt_multi* m, Lane& L, int r)
                                     (size_t)(H - last * rb) * W * 4, hipMemcpyDeviceToHost, st));
         }
     }
-    MHIP(hipEventRecord(L.done[r], st));
+    // the launch's last operation on this rank: its copy stream when the
+    // lane has one (it waited for everything the context's stream did)
+    MHIP(hipEventRecord(L.done[r], copy_stream(m, L, r)));
     return MIRT_OK;
 }
 
@@ -588,7 +629,8 @@ extern "C" {
 
 int mirt_multi_create(const int* devices, int n, int lanes, int flags, mirt_multi** out)
 try {
-    if (!out || n <= 0 || n > kMaxShards || lanes <= 0 || (flags & ~(MIRT_MULTI_COPY | MIRT_MULTI_HOST_DIRECT))) {
+    if (!out || n <= 0 || n > kMaxShards || lanes <= 0 ||
+        (flags & ~(MIRT_MULTI_COPY | MIRT_MULTI_HOST_DIRECT | MIRT_MULTI_QUEUE_AHEAD))) {
         set_error("mirt_multi_create: invalid arguments");
         return MIRT_E_INVALID;
     }
@@ -608,6 +650,8 @@ try {
         for (int q = 0; q < r; q++) distinct = distinct && m->dev[q] != m->dev[r];
     }
     m->direct = (flags & MIRT_MULTI_HOST_DIRECT) != 0;
+    m->ahead = (flags & MIRT_MULTI_QUEUE_AHEAD) != 0;
+    m->nctx = lanes;
     m->rccl = distinct && !(flags & MIRT_MULTI_COPY);
     auto fail = [&](int rc) {
         mirt_multi_destroy(m);
@@ -631,21 +675,36 @@ try {
             }
         }
     }
-    m->lanes.resize(lanes);
-    for (int l = 0; l < lanes; l++) {
+    const int slots = m->ahead ? 2 * lanes : lanes;
+    m->lanes.resize(slots);
+    for (int l = 0; l < slots; l++) {
         Lane& L = m->lanes[l];
         L.ctx.assign(n, nullptr);
         L.rendered.assign(n, nullptr);
         L.done.assign(n, nullptr);
         L.src.assign(n, nullptr);
+        L.slab.assign(n, nullptr);
+        L.slab_cap.assign(n, 0);
+        L.cstream.assign(n, nullptr);
+        L.kdone.assign(n, nullptr);
+        L.kdone_set.assign(n, 0);
+        L.owns_ctx = l < lanes;
         for (int r = 0; r < n; r++) L.slabs_ready.emplace_back(new std::atomic<uint64_t>(0));
         for (int r = 0; r < n; r++) {
-            int rc = mirt_create(m->dev[r], &L.ctx[r]);
-            if (rc) return fail(rc);
             (void)hipSetDevice(m->dev[r]);
             hipError_t e = hipEventCreateWithFlags(&L.rendered[r], hipEventDisableTiming);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&L.done[r], hipEventDisableTiming);
-            if (e != hipSuccess) return fail(hip_err(e, "mirt_multi_create: hipEventCreate"));
+            if (e == hipSuccess && m->ahead) e = hipEventCreateWithFlags(&L.kdone[r], hipEventDisableTiming);
+            if (e == hipSuccess && m->ahead) e = hipStreamCreateWithFlags(&L.cstream[r], hipStreamNonBlocking);
+            if (e != hipSuccess) return fail(hip_err(e, "mirt_multi_create: hipEventCreate / hipStreamCreate"));
+            if (!L.owns_ctx) {
+                // the second launch slot of context set l - lanes: its kernels
+                // queue behind that lane's on the same stream
+                L.ctx[r] = m->lanes[l - lanes].ctx[r];
+                continue;
+            }
+            int rc = mirt_create(m->dev[r], &L.ctx[r]);
+            if (rc) return fail(rc);
             if (lanes > 1) {
                 // launches in flight share the chip: each bounce pass at 1.5
                 // persistent workgroups per CU instead of the full grid
@@ -708,7 +767,10 @@ void mirt_multi_destroy(mirt_multi* m)
             (void)hipSetDevice(m->dev[r]);
             if (L.rendered[r]) (void)hipEventDestroy(L.rendered[r]);
             if (L.done[r]) (void)hipEventDestroy(L.done[r]);
-            mirt_destroy(L.ctx[r]);
+            if (r < (int)L.kdone.size() && L.kdone[r]) (void)hipEventDestroy(L.kdone[r]);
+            if (r < (int)L.cstream.size() && L.cstream[r]) (void)hipStreamDestroy(L.cstream[r]);
+            if (r < (int)L.slab.size() && L.slab[r]) (void)hipFree(L.slab[r]);
+            if (L.owns_ctx) mirt_destroy(L.ctx[r]);
         }
         (void)hipSetDevice(m->dev[0]);
         if (L.gathered) (void)hipFree(L.gathered);
@@ -762,8 +824,9 @@ int mirt_multi_set_option(mirt_multi* m, int option, int value)
         return MIRT_OK;
     default:
         for (Lane& L : m->lanes)
-            for (mirt_ctx* c : L.ctx)
-                if (int rc = mirt_set_option(c, option, value)) return rc;
+            if (L.owns_ctx)
+                for (mirt_ctx* c : L.ctx)
+                    if (int rc = mirt_set_option(c, option, value)) return rc;
         return MIRT_OK;
     }
     set_error("mirt_multi_set_option: invalid option %d / value %d", option, value);
@@ -786,8 +849,9 @@ int mirt_multi_scene_upload(mirt_multi* m, const mirt_sphere* spheres, int num_s
     for (int l = 0; l < (int)m->lanes.size(); l++)
         if (int rc = wait_lane(m, l)) return rc;
     for (Lane& L : m->lanes)
-        for (mirt_ctx* c : L.ctx)
-            if (int rc = mirt_scene_upload(c, spheres, num_spheres, root)) return rc;
+        if (L.owns_ctx)
+            for (mirt_ctx* c : L.ctx)
+                if (int rc = mirt_scene_upload(c, spheres, num_spheres, root)) return rc;
     return MIRT_OK;
 }
 
@@ -798,8 +862,9 @@ int mirt_multi_scene_upload_flat(mirt_multi* m, const mirt_sphere* spheres, int 
     for (int l = 0; l < (int)m->lanes.size(); l++)
         if (int rc = wait_lane(m, l)) return rc;
     for (Lane& L : m->lanes)
-        for (mirt_ctx* c : L.ctx)
-            if (int rc = mirt_scene_upload_flat(c, spheres, num_spheres, nodes, num_nodes)) return rc;
+        if (L.owns_ctx)
+            for (mirt_ctx* c : L.ctx)
+                if (int rc = mirt_scene_upload_flat(c, spheres, num_spheres, nodes, num_nodes)) return rc;
     return MIRT_OK;
 }
 

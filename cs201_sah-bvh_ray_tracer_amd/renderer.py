@@ -436,15 +436,16 @@ class MultiRenderer:
     `lanes` launches in flight, each of one or more frames. Frames equal
     Renderer.render_frame's on one GPU."""
 
-    def __init__(self, devices, lanes=1, copy=False, host_direct=False):
+    def __init__(self, devices, lanes=1, copy=False, host_direct=False, queue_ahead=False):
         self.L = load()
         devs = (C.c_int * len(devices))(*devices)
         h = C.c_void_p()
-        flags = (abi.MULTI_COPY if copy else 0) | (abi.MULTI_HOST_DIRECT if host_direct else 0)
+        flags = ((abi.MULTI_COPY if copy else 0) | (abi.MULTI_HOST_DIRECT if host_direct else 0)
+                 | (abi.MULTI_QUEUE_AHEAD if queue_ahead else 0))
         check(self.L.mirt_multi_create(devs, len(devices), lanes, flags, C.byref(h)), "mirt_multi_create")
         self.h = h
         self.devices = list(devices)
-        self.lanes = lanes
+        self.lanes = self.L.mirt_multi_lanes(h)   # launch slots (2 x lanes with queue_ahead)
         self.launches = 0   # launch k runs on lane k % lanes (mirt_multi's rotation)
 
     def close(self):

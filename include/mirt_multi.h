@@ -63,9 +63,14 @@ enum {
                                    distinct; implied when a device repeats (RCCL refuses two ranks on one
                                    device): n ranks on one GPU render the same shards, so the frame geometry
                                    of an n-GPU node is testable on one */
-    MIRT_MULTI_HOST_DIRECT = 2  /* frames delivered to host memory by every rank: rank r copies its row
+    MIRT_MULTI_HOST_DIRECT = 2, /* frames delivered to host memory by every rank: rank r copies its row
                                    blocks of each frame straight into the caller's buffer (one strided DMA
                                    per frame from its own device); no gather to device 0 */
+    MIRT_MULTI_QUEUE_AHEAD = 4  /* 2 x `lanes` launch slots over `lanes` context sets: slot l + lanes queues
+                                   its kernels behind slot l's on the same contexts' streams (so a context
+                                   starts its next launch the moment its last one's kernels end, with no
+                                   host turnaround), renders into its own slabs, and delivers on its own
+                                   copy stream; mirt_multi_lanes() then returns 2 x lanes */
 };
 
 /* mirt_multi_render_frames_async flags */
@@ -94,7 +99,8 @@ enum {
    mirt_init(n) of SURVEY §8(b) is mirt_multi_create(NULL, n, 1, 0, &m). */
 int mirt_multi_create(const int *devices, int n, int lanes, int flags, mirt_multi **out);
 void mirt_multi_destroy(mirt_multi *m);
-/* Ranks (GPUs, or same-device shards), lanes, the gather path ("rccl" or
+/* Ranks (GPUs, or same-device shards), launch slots (lanes; 2 x lanes with
+   MIRT_MULTI_QUEUE_AHEAD), the gather path ("rccl" or
    "copy"), the delivery ("gather" or "host-direct"), and 1 once the object has
    failed (0 otherwise). */
 int mirt_multi_size(const mirt_multi *m);

@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--device-only", action="store_true", help="frames left on the devices (no delivery to host)")
     ap.add_argument("--sweep", default="", help="LANES:BATCH:TAIL[,...] schedules to emulate instead of the bench's")
     ap.add_argument("--direct-copy", type=int, default=0, help="MIRT_MULTI_OPT_DIRECT_COPY for host-direct")
+    ap.add_argument("--queue-ahead", type=int, default=-1, help="MIRT_MULTI_QUEUE_AHEAD (default: bench.py's per N)")
     a = ap.parse_args()
     if a.hw_queues and int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < a.hw_queues:
         os.environ["GPU_MAX_HW_QUEUES"] = str(a.hw_queues)   # before the first HIP call of this process
@@ -63,9 +64,10 @@ def main():
         if combo:
             a.pipeline, a.batch, a.tail_grid = combo
         lanes, per, tail_n, blocks = bench.schedule(a, world)
-        m = bench.open_multi(1, lanes, a.delivery == "host-direct", spheres, bvh, blocks, a.opt)
+        ahead = bench.queue_ahead(a, world)
+        m = bench.open_multi(1, lanes, a.delivery == "host-direct", spheres, bvh, blocks, a.opt, ahead=ahead)
         m.set_option(mirt.abi.MULTI_OPT_DIRECT_COPY, a.direct_copy)
-        bufs = bench.host_bufs(lanes, per)
+        bufs = bench.host_bufs(m.lanes, per)
         bench.prime(m, cam, bufs, per)
         timed = bench.plan(a.warmup, a.steps, per)
         tail = bench.tail_of(timed, tail_n, lanes, blocks)
@@ -85,7 +87,8 @@ def main():
         print(json.dumps({
             "workload": a.workload, "delivery": "device-only" if a.device_only else a.delivery,
             "direct_copy": a.direct_copy, "world": world, "steps": a.steps, "warmup": a.warmup,
-            "lanes": lanes, "frames_per_launch": per, "tail_grid": len(tail), "bounce_blocks": blocks,
+            "lanes": lanes, "queue_ahead": ahead, "frames_per_launch": per, "tail_grid": len(tail),
+            "bounce_blocks": blocks,
             "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
             "rank_ms_per_frame": [round(t / a.steps * 1e3, 4) for t in per_rank],
             "slowest_rank": per_rank.index(slow),

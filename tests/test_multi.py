@@ -79,7 +79,8 @@ def test_multi_ragged_frames_equal_one_gpu(gpu, mirt, n, rb):
 
 
 @pytest.mark.gpu
-def test_multi_lanes_accumulating_loop(gpu, mirt, scene10k):
+@pytest.mark.parametrize("ahead", [False, True])
+def test_multi_lanes_accumulating_loop(gpu, mirt, scene10k, ahead):
     """main.c:349-408's loop with frames in flight: 3 lanes x 2 shards, a
     fresh frame, accumulating frames, a camera move, more accumulation; every
     host frame equals the same sequence of blocking one-ctx frames."""
@@ -93,7 +94,7 @@ def test_multi_lanes_accumulating_loop(gpu, mirt, scene10k):
     gpu.upload(s, b)
     want = [gpu.render_frame(c, W, H, depth=5, seed=2, sample=k, accumulate=a, frames=f)
             for k, (c, a, f) in enumerate(seq)]
-    with mirt.MultiRenderer([0, 0], lanes=3) as m:
+    with mirt.MultiRenderer([0, 0], lanes=3, queue_ahead=ahead) as m:
         m.upload(s, b)
         bufs = [mirt.HostBuffer((H, W, 4)) for _ in range(3)]
         got = []
@@ -145,20 +146,26 @@ def test_multi_rejects_sharded_descriptor(mirt, scene10k):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("devices,direct,batch", [([0], False, 4), ([0], True, 4), ([0, 0, 0], False, 3),
-                                                  ([0, 0, 0], True, 4), ([0] * 8, True, 2)])
-def test_multi_batched_launches_equal_one_gpu(gpu, mirt, scene10k, devices, direct, batch):
+@pytest.mark.parametrize("devices,direct,batch,ahead", [([0], False, 4, False), ([0], True, 4, False),
+                                                        ([0, 0, 0], False, 3, False), ([0, 0, 0], True, 4, False),
+                                                        ([0] * 8, True, 2, False), ([0], False, 1, True),
+                                                        ([0], False, 4, True), ([0, 0, 0], False, 3, True),
+                                                        ([0, 0, 0], True, 4, True)])
+def test_multi_batched_launches_equal_one_gpu(gpu, mirt, scene10k, devices, direct, batch, ahead):
     """Launches of several successive fresh frames (bench.py's N >= 4
     schedule), lanes in flight, the gather (RCCL at n = 1, copy across
     same-device ranks) or the host-direct delivery (each rank's strided copies
     into the host frame): frame j of every launch equals one context's
-    blocking frame of that RNG sample; the last launch on the full grid."""
+    blocking frame of that RNG sample; the last launch on the full grid.
+    `ahead`: MIRT_MULTI_QUEUE_AHEAD (two launch slots per context, each with
+    its own slabs and copy stream)."""
     s, b = scene10k
     W, H, F = 333, 187, 9    # ragged: the last 8-row block is short
     cam = mirt.default_camera()
     bufs = [mirt.HostBuffer((H, W, 4)) for _ in range(F)]
     try:
-        with mirt.MultiRenderer(devices, lanes=3, host_direct=direct) as m:
+        with mirt.MultiRenderer(devices, lanes=3, host_direct=direct, queue_ahead=ahead) as m:
+            assert m.lanes == (6 if ahead else 3)
             m.upload(s, b)
             for f0 in range(0, F, batch):
                 k = min(batch, F - f0)
