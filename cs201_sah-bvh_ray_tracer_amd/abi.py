@@ -202,3 +202,4 @@ TRAV_TILE, TRAV_WAVEFRONT = 0, 5
 MULTI_COPY, MULTI_HOST_DIRECT, MULTI_QUEUE_AHEAD = 1, 2, 4
 MULTI_FULL_GRID = 1
 MULTI_OPT_TIMEOUT_MS, MULTI_OPT_EMULATE_WORLD, MULTI_OPT_EMULATE_RANK, MULTI_OPT_DIRECT_COPY = 256, 257, 258, 259
+MULTI_OPT_COPY_STREAM = 260

@@ -177,6 +177,7 @@ struct mirt_multi {
     int n = 0;
     int nctx = 0;                     // context sets (the `lanes` argument)
     bool ahead = false;               // MIRT_MULTI_QUEUE_AHEAD: 2 x nctx lanes, two launches per context
+    int ahead_copy_stream = 0;        // MIRT_MULTI_OPT_COPY_STREAM: the copies on the context's copy stream
     std::vector<int> dev;
     bool rccl = false;
     bool direct = false;              // MIRT_MULTI_HOST_DIRECT
@@ -364,7 +365,7 @@ int prepare(mirt_multi* m, Lane& L, const mirt_camera* cam, const mirt_frame_des
 hipStream_t copy_stream(mirt_multi* m, Lane& L, int r)
 {
     const hipStream_t st = stream_of(L.ctx[r]);
-    if (!m->ahead) return st;
+    if (!m->ahead || !m->ahead_copy_stream) return st;
     if (!L.kdone_set[r]) {
         (void)hipEventRecord(L.kdone[r], st);
         (void)hipStreamWaitEvent(L.cstream[r], L.kdone[r], 0);
@@ -695,12 +696,17 @@ try {
             hipError_t e = hipEventCreateWithFlags(&L.rendered[r], hipEventDisableTiming);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&L.done[r], hipEventDisableTiming);
             if (e == hipSuccess && m->ahead) e = hipEventCreateWithFlags(&L.kdone[r], hipEventDisableTiming);
-            if (e == hipSuccess && m->ahead) e = hipStreamCreateWithFlags(&L.cstream[r], hipStreamNonBlocking);
+            // one copy stream per context, shared by its two launch slots (a
+            // stream beyond the process's hardware queues shares one with
+            // another stream, whose waits then block it)
+            if (e == hipSuccess && m->ahead && L.owns_ctx)
+                e = hipStreamCreateWithFlags(&L.cstream[r], hipStreamNonBlocking);
             if (e != hipSuccess) return fail(hip_err(e, "mirt_multi_create: hipEventCreate / hipStreamCreate"));
             if (!L.owns_ctx) {
                 // the second launch slot of context set l - lanes: its kernels
                 // queue behind that lane's on the same stream
                 L.ctx[r] = m->lanes[l - lanes].ctx[r];
+                L.cstream[r] = m->lanes[l - lanes].cstream[r];
                 continue;
             }
             int rc = mirt_create(m->dev[r], &L.ctx[r]);
@@ -768,7 +774,7 @@ void mirt_multi_destroy(mirt_multi* m)
             if (L.rendered[r]) (void)hipEventDestroy(L.rendered[r]);
             if (L.done[r]) (void)hipEventDestroy(L.done[r]);
             if (r < (int)L.kdone.size() && L.kdone[r]) (void)hipEventDestroy(L.kdone[r]);
-            if (r < (int)L.cstream.size() && L.cstream[r]) (void)hipStreamDestroy(L.cstream[r]);
+            if (L.owns_ctx && r < (int)L.cstream.size() && L.cstream[r]) (void)hipStreamDestroy(L.cstream[r]);
             if (r < (int)L.slab.size() && L.slab[r]) (void)hipFree(L.slab[r]);
             if (L.owns_ctx) mirt_destroy(L.ctx[r]);
         }
@@ -818,6 +824,10 @@ int mirt_multi_set_option(mirt_multi* m, int option, int value)
         if (value < 0 || value > 1) break;
         m->direct_copy = value;
         return MIRT_OK;
+    case MIRT_MULTI_OPT_COPY_STREAM:
+        if (value < 0 || value > 1) break;
+        m->ahead_copy_stream = value;
+        return MIRT_OK;
     case MIRT_MULTI_OPT_EMULATE_RANK:
         if (value < 0 || value >= std::max(1, m->emu_world)) break;
         m->emu_rank = value;
@@ -840,6 +850,7 @@ int mirt_multi_get_option(mirt_multi* m, int option)
     if (option == MIRT_MULTI_OPT_EMULATE_WORLD) return m->emu_world;
     if (option == MIRT_MULTI_OPT_EMULATE_RANK) return m->emu_rank;
     if (option == MIRT_MULTI_OPT_DIRECT_COPY) return m->direct_copy;
+    if (option == MIRT_MULTI_OPT_COPY_STREAM) return m->ahead_copy_stream;
     return mirt_get_option(m->lanes[0].ctx[0], option);
 }
 

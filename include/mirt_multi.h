@@ -69,8 +69,10 @@ enum {
     MIRT_MULTI_QUEUE_AHEAD = 4  /* 2 x `lanes` launch slots over `lanes` context sets: slot l + lanes queues
                                    its kernels behind slot l's on the same contexts' streams (so a context
                                    starts its next launch the moment its last one's kernels end, with no
-                                   host turnaround), renders into its own slabs, and delivers on its own
-                                   copy stream; mirt_multi_lanes() then returns 2 x lanes */
+                                   host turnaround), renders into its own slabs, and delivers them on its
+                                   context's copy stream (2 streams per context:
+                                   give the process GPU_MAX_HW_QUEUES >= 2 x lanes); mirt_multi_lanes()
+                                   then returns 2 x lanes */
 };
 
 /* mirt_multi_render_frames_async flags */
@@ -89,8 +91,13 @@ enum {
                                             receives, the de-interleave and the frame's D2H; the frames
                                             delivered are NOT complete. 0 or 1 = off (default) */
     MIRT_MULTI_OPT_EMULATE_RANK = 258,
-    MIRT_MULTI_OPT_DIRECT_COPY = 259     /* MIRT_MULTI_HOST_DIRECT: each rank's blocks of a frame as one strided
+    MIRT_MULTI_OPT_DIRECT_COPY = 259,    /* MIRT_MULTI_HOST_DIRECT: each rank's blocks of a frame as one strided
                                             copy (hipMemcpy2DAsync, 0, default) or one copy per row block (1) */
+    MIRT_MULTI_OPT_COPY_STREAM = 260     /* MIRT_MULTI_QUEUE_AHEAD: a launch's copies on its context's stream
+                                            behind its kernels (0, default) or on the context's copy stream (1:
+                                            the next launch's kernels then start while they run, but a copy
+                                            stream's wait on a kernel stream can block the issuing thread in
+                                            the runtime: measured slower) */
 };
 
 /* n ranks on devices[0..n-1] (NULL: devices 0..n-1; n <= 64), `lanes` launches in
