@@ -127,7 +127,7 @@ TAIL_GRID_MULTI = 0
 # current one on its stream (own slabs, copies on a copy stream), so no
 # context idles through its frame's D2H and the host's turnaround
 QUEUE_AHEAD, QUEUE_AHEAD_MULTI = False, False
-KERNEL = "bounce_kernel<true, 2, false>"   # dominant kernel of the default (wavefront, four-wide) schedule
+KERNEL = "bounce_kernel<true, 2, false, false>"   # dominant kernel of the default (wavefront, four-wide) schedule
 # the PMC-derived bound of the timed launch shape, per workload
 # (scripts/pmc_bench.sh over this script's own command + scripts/pmc_summary.py);
 # the newest round's file wins
