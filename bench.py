@@ -318,13 +318,17 @@ def gather_peak(probe, tcp_per_inst):
 def trace_check():
     """The same launch shape ALONE under rocprofv3 --kernel-trace --stats
     (committed summary): its mean duration must agree with kernel_ms."""
-    path = os.path.join(ROOT, "profiles", "r04q", "exclusive_bounce_trace.json")
-    if W != 1920 or NSPH != 10000 or not os.path.exists(path):
-        return None
-    with open(path) as f:
-        d = json.load(f)
-    return {"mean_ms": d["mean_ms"], "median_ms": d["median_ms"], "dispatches": d["dispatches"],
-            "source": os.path.relpath(path, ROOT) + " (profiles/r04q/prof_exclusive_kernel_stats.csv)"}
+    for path, stats in ((os.path.join(ROOT, "profiles", "r05_exclusive_bounce_trace.json"),
+                         "profiles/r05_logs/r05z/prof_exclusive_kernel_stats.csv"),
+                        (os.path.join(ROOT, "profiles", "r04q", "exclusive_bounce_trace.json"),
+                         "profiles/r04q/prof_exclusive_kernel_stats.csv")):
+        if W == 1920 and NSPH == 10000 and os.path.exists(path):
+            with open(path) as f:
+                d = json.load(f)
+            return {"mean_ms": d["mean_ms"], "median_ms": d["median_ms"], "dispatches": d["dispatches"],
+                    "pmc_exclusive_ms": d.get("pmc_exclusive_ms"),
+                    "source": os.path.relpath(path, ROOT) + f" ({stats}; scripts/exclusive_trace.py)"}
+    return None
 
 
 def vmem_roofline(pmc, pmc_path, ms_per_step, frames_per_launch):

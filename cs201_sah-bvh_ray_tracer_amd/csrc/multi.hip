@@ -38,6 +38,13 @@ using namespace mirt;
 namespace {
 
 constexpr int kMaxShards = 64;  // shards of one frame (ranks, or the emulated world)
+// A/B switch (measurement only): 0 gives every lane its own accumulation
+// buffer, so fresh frames write it in the render kernel with no ordered fold
+// across the lanes -- NOT exact for an accumulating frame in flight after
+// fresh frames of other lanes
+#ifndef MIRT_MULTI_SHARE_ACCUM
+#define MIRT_MULTI_SHARE_ACCUM 1
+#endif
 
 // Where every shard's displays are (kernel argument of deinterleave_kernel):
 // shard s's `nframes` displays at p[s], frame j at + j * rows[s] * width --
@@ -723,7 +730,7 @@ try {
             }
             // the lanes of a rank keep ONE accumulation buffer: frames in
             // flight of the accumulating loop (main.c:379-408) fold in order
-            if (l > 0) {
+            if (MIRT_MULTI_SHARE_ACCUM && l > 0) {
                 rc = mirt_ctx_share_accum(L.ctx[r], m->lanes[0].ctx[r]);
                 if (rc) return fail(rc);
             }

@@ -1,35 +1,43 @@
-"""The bounce launch of the timed shape ALONE under the kernel trace
-(scripts/r04q_gpu.sh's prof_exclusive run: bench.py --pipeline 1
---bounce-blocks 384) against the counter pass's exclusive time: both must
-agree for bench.py's roofline kernel_ms (trace_check).
+"""The exclusive-time check of bench.py's roofline (kernel_ms_trace_check):
+the bounce launches of the timed shape (384 workgroups) run ONE at a time
+under rocprofv3 --kernel-trace, their mean duration beside the counter pass's
+exclusive time.
 
-    python scripts/exclusive_trace.py <rocprofv3 -d dir> <pmc bound json> <out json>
+    rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/<tag>/prof_exclusive -o run -- \
+        python3 bench.py --no-cpu --no-host --pipeline 1 --bounce-blocks 384 --steps 20 --warmup 5
+    python scripts/exclusive_trace.py gpurun_out/<tag>/prof_exclusive/run_kernel_trace.csv \
+        --pmc profiles/r05_pmc_bound_1080p_10k.json --json profiles/r05_exclusive_bounce_trace.json
 """
+import argparse
 import csv
 import json
-import os
 import statistics
-import sys
+
+BOUNCE = "bounce_kernel<true, 2, false, false>"
 
 
 def main():
-    d, pmc_path, out = sys.argv[1:4]
-    grid = 384 * 256
-    ms = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
-          for r in csv.DictReader(open(os.path.join(d, "run_kernel_trace.csv")))
-          if "bounce_kernel" in r["Kernel_Name"] and int(r["Grid_Size_X"]) == grid]
-    pmc = json.load(open(pmc_path))
-    res = {"command": "rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu --no-host --pipeline 1 "
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--pmc", required=True)
+    ap.add_argument("--grid", type=int, default=384 * 256)
+    ap.add_argument("--json")
+    a = ap.parse_args()
+    rows = [r for r in csv.DictReader(open(a.trace)) if BOUNCE in r["Kernel_Name"] and int(r["Grid_Size_X"]) == a.grid]
+    ms = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows]
+    pmc = json.load(open(a.pmc))
+    out = {"command": "rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu --no-host --pipeline 1 "
                       "--bounce-blocks 384 --steps 20 --warmup 5",
-           "kernel": "bounce_kernel<true, 2, false>, grid 98304 work-items (384 workgroups: the timed launch shape), "
-                     "one launch at a time",
-           "dispatches": len(ms), "mean_ms": round(statistics.mean(ms), 4),
-           "median_ms": round(statistics.median(ms), 4), "min_ms": round(min(ms), 4), "max_ms": round(max(ms), 4),
+           "kernel": f"{BOUNCE}, grid {a.grid} work-items (384 workgroups: the timed launch shape), one launch at "
+                     "a time",
+           "dispatches": len(ms), "mean_ms": round(statistics.mean(ms), 4), "median_ms": round(statistics.median(ms), 4),
+           "min_ms": round(min(ms), 4), "max_ms": round(max(ms), 4),
            "pmc_exclusive_ms": pmc["kernels"]["timed/bounce"]["vmem_pass"]["kernel_ms_at_2400MHz"],
-           "pmc_source": pmc_path + " timed/bounce vmem_pass.kernel_ms_at_2400MHz"}
-    with open(out, "w") as f:
-        json.dump(res, f, indent=1)
-    print(json.dumps(res))
+           "pmc_source": a.pmc + " timed/bounce vmem_pass.kernel_ms_at_2400MHz"}
+    print(json.dumps(out))
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(out, f, indent=1)
 
 
 if __name__ == "__main__":
