@@ -290,6 +290,48 @@ int wait_lane(mirt_multi* m, int li)
     return MIRT_OK;
 }
 
+// MIRT_MULTI_OPT_COPY_STREAM 2: before a launch on lane li, the KERNELS of
+// the launch in the same contexts' other slot must have finished (its copies
+// may still run on the copy streams): one launch's kernels per context at a
+// time, as without QUEUE_AHEAD, but a frame's D2H no longer holds its context.
+int wait_sibling_kernels(mirt_multi* m, int li)
+{
+    const int sib = li < m->nctx ? li + m->nctx : li - m->nctx;
+    Lane& S = m->lanes[sib];
+    if (!S.pending) return MIRT_OK;
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    auto over = [&]() {
+        return m->timeout_ms > 0 && std::chrono::duration<double, std::milli>(clk::now() - t0).count() > m->timeout_ms;
+    };
+    for (long polls = 0; S.issued->load(std::memory_order_acquire) < m->n; polls++) {
+        if (over()) return fail_multi(m, "lane " + std::to_string(sib) + ": the rank threads did not issue the launch");
+        if (polls < 2000)
+            std::this_thread::yield();
+        else
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    for (int r = 0; r < m->n; r++) {
+        if (!S.kdone_set[r]) continue;
+        for (long polls = 0;; polls++) {
+            const hipError_t e = hipEventQuery(S.kdone[r]);
+            if (e == hipSuccess) break;
+            if (e != hipErrorNotReady) {
+                (void)hipGetLastError();
+                return fail_multi(m, std::string("rank ") + std::to_string(r) + ": " + hipGetErrorString(e));
+            }
+            if (over())
+                return fail_multi(m, "lane " + std::to_string(sib) + " kernels not done after " +
+                                         std::to_string(m->timeout_ms) + " ms (MIRT_MULTI_OPT_TIMEOUT_MS)");
+            if (polls < 2000)
+                std::this_thread::yield();
+            else
+                std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+    }
+    return MIRT_OK;
+}
+
 int communicators(mirt_multi* m)
 {
     if (!m->comm.empty()) return MIRT_OK;
@@ -832,7 +874,7 @@ int mirt_multi_set_option(mirt_multi* m, int option, int value)
         m->direct_copy = value;
         return MIRT_OK;
     case MIRT_MULTI_OPT_COPY_STREAM:
-        if (value < 0 || value > 1) break;
+        if (value < 0 || value > 2) break;
         m->ahead_copy_stream = value;
         return MIRT_OK;
     case MIRT_MULTI_OPT_EMULATE_RANK:
@@ -895,6 +937,8 @@ try {
     if (int rc = check_frame(m, cam, fd, nframes, outs, fn)) return rc;
     const int li = m->next;
     if (int rc = wait_lane(m, li)) return rc;
+    if (m->ahead && m->ahead_copy_stream == 2)
+        if (int rc = wait_sibling_kernels(m, li)) return rc;
     m->next = (m->next + 1) % (int)m->lanes.size();
     // an error here (before any rank issued) leaves the lane as it was; the
     // ranks' own issue errors come back from the lane's wait

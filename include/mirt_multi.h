@@ -94,10 +94,11 @@ enum {
     MIRT_MULTI_OPT_DIRECT_COPY = 259,    /* MIRT_MULTI_HOST_DIRECT: each rank's blocks of a frame as one strided
                                             copy (hipMemcpy2DAsync, 0, default) or one copy per row block (1) */
     MIRT_MULTI_OPT_COPY_STREAM = 260     /* MIRT_MULTI_QUEUE_AHEAD: a launch's copies on its context's stream
-                                            behind its kernels (0, default) or on the context's copy stream (1:
-                                            the next launch's kernels then start while they run, but a copy
-                                            stream's wait on a kernel stream can block the issuing thread in
-                                            the runtime: measured slower) */
+                                            behind its kernels (0, default) or on the context's copy stream (1);
+                                            2: on the copy stream, and a launch is enqueued only once the
+                                            kernels of the launch in its contexts' other slot have finished
+                                            (one launch's kernels per context at a time; its copies still
+                                            running). DESIGN §8 has the measurements */
 };
 
 /* n ranks on devices[0..n-1] (NULL: devices 0..n-1; n <= 64), `lanes` launches in
