@@ -49,6 +49,7 @@ def main():
     ap.add_argument("--sweep", default="", help="LANES:BATCH:TAIL[,...] schedules to emulate instead of the bench's")
     ap.add_argument("--direct-copy", type=int, default=0, help="MIRT_MULTI_OPT_DIRECT_COPY for host-direct")
     ap.add_argument("--queue-ahead", type=int, default=-1, help="MIRT_MULTI_QUEUE_AHEAD (default: bench.py's per N)")
+    ap.add_argument("--row-block", type=int, default=8, help="rows per interleaved shard block (fd->row_block)")
     a = ap.parse_args()
     if a.hw_queues and int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < a.hw_queues:
         os.environ["GPU_MAX_HW_QUEUES"] = str(a.hw_queues)   # before the first HIP call of this process
@@ -57,6 +58,7 @@ def main():
     bench.W, bench.H, bench.NSPH, bench.KIND, bench.SPP, bench.JITTER = (wl["W"], wl["H"], wl["NSPH"], wl["KIND"],
                                                                           wl["SPP"], wl["JITTER"])
     W, H, SPP = bench.W, bench.H, bench.SPP
+    bench.ROW_BLOCK = a.row_block
     spheres, bvh, _ = bench.make_scene()
     cam = mirt.default_camera()
     combos = [tuple(int(v) for v in c.split(":")) for c in a.sweep.split(",")] if a.sweep else [None]
@@ -87,7 +89,7 @@ def main():
         print(json.dumps({
             "workload": a.workload, "delivery": "device-only" if a.device_only else a.delivery,
             "direct_copy": a.direct_copy, "world": world, "steps": a.steps, "warmup": a.warmup,
-            "lanes": lanes, "queue_ahead": ahead, "frames_per_launch": per, "tail_grid": len(tail),
+            "lanes": lanes, "queue_ahead": ahead, "row_block": a.row_block, "frames_per_launch": per, "tail_grid": len(tail),
             "bounce_blocks": blocks,
             "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
             "rank_ms_per_frame": [round(t / a.steps * 1e3, 4) for t in per_rank],
