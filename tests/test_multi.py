@@ -146,19 +146,23 @@ def test_multi_rejects_sharded_descriptor(mirt, scene10k):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("devices,direct,batch,ahead", [([0], False, 4, False), ([0], True, 4, False),
-                                                        ([0, 0, 0], False, 3, False), ([0, 0, 0], True, 4, False),
-                                                        ([0] * 8, True, 2, False), ([0], False, 1, True),
-                                                        ([0], False, 4, True), ([0, 0, 0], False, 3, True),
-                                                        ([0, 0, 0], True, 4, True)])
-def test_multi_batched_launches_equal_one_gpu(gpu, mirt, scene10k, devices, direct, batch, ahead):
+@pytest.mark.parametrize("devices,direct,batch,ahead,cs", [([0], False, 4, False, 0), ([0], True, 4, False, 0),
+                                                           ([0, 0, 0], False, 3, False, 0),
+                                                           ([0, 0, 0], True, 4, False, 0), ([0] * 8, True, 2, False, 0),
+                                                           ([0], False, 1, True, 0), ([0], False, 4, True, 0),
+                                                           ([0, 0, 0], False, 3, True, 0), ([0, 0, 0], True, 4, True, 0),
+                                                           ([0], False, 1, True, 1), ([0, 0, 0], True, 4, True, 1),
+                                                           ([0], False, 4, True, 2), ([0, 0, 0], False, 3, True, 2)])
+def test_multi_batched_launches_equal_one_gpu(gpu, mirt, scene10k, devices, direct, batch, ahead, cs):
     """Launches of several successive fresh frames (bench.py's N >= 4
     schedule), lanes in flight, the gather (RCCL at n = 1, copy across
     same-device ranks) or the host-direct delivery (each rank's strided copies
     into the host frame): frame j of every launch equals one context's
     blocking frame of that RNG sample; the last launch on the full grid.
     `ahead`: MIRT_MULTI_QUEUE_AHEAD (two launch slots per context, each with
-    its own slabs and copy stream)."""
+    its own slabs), `cs`: its copies behind the kernels (0), on the context's
+    copy stream (1), or there with the next launch waiting only for the
+    other slot's kernels (2)."""
     s, b = scene10k
     W, H, F = 333, 187, 9    # ragged: the last 8-row block is short
     cam = mirt.default_camera()
@@ -166,6 +170,8 @@ def test_multi_batched_launches_equal_one_gpu(gpu, mirt, scene10k, devices, dire
     try:
         with mirt.MultiRenderer(devices, lanes=3, host_direct=direct, queue_ahead=ahead) as m:
             assert m.lanes == (6 if ahead else 3)
+            m.set_option(mirt.abi.MULTI_OPT_COPY_STREAM, cs)
+            assert m.get_option(mirt.abi.MULTI_OPT_COPY_STREAM) == cs
             m.upload(s, b)
             for f0 in range(0, F, batch):
                 k = min(batch, F - f0)
