@@ -360,7 +360,7 @@ def vmem_roofline(pmc, pmc_path, ms_per_step, frames_per_launch):
     share = min(1.0, cb.get("SQ_WAVES", WAVE_SLOTS) / WAVE_SLOTS)
     vmem_step = (vmem + cp.get("SQ_INSTS_VMEM_RD", 0.0)) / frames_per_launch
     step_rate = vmem_step / (ms_per_step * 1e-3) / 1e9
-    return {
+    out = {
         "bound": "vmem", "achieved": round(achieved, 3), "peak": round(peak, 3), "unit": "Ginst/s",
         "frac": round(achieved / peak, 4),
         "traffic": db.get("hbm_bytes"),
@@ -389,6 +389,12 @@ def vmem_roofline(pmc, pmc_path, ms_per_step, frames_per_launch):
         "kernel_ms_trace_check": trace_check(),
         "reconcile": reconcile_busy(probe, vb, db, kb.get("counters", {}), achieved),
     }
+    rec = out["reconcile"]
+    if rec and rec.get("mix_matched"):
+        # the frame loop's load rate against the ceiling of the kernel's own
+        # instruction mix (the probe case at 5 waves per SIMD, alone on the chip)
+        out["timed_loop"]["frac_vs_mix_ceiling"] = round(step_rate / rec["mix_matched"]["ceiling_ginst_per_s"], 4)
+    return out
 
 
 def reconcile_busy(probe, vb, db, counters, achieved):
