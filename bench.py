@@ -787,6 +787,20 @@ def measure(args):
                 m2.close()
             if bufs2 is not None:
                 close_bufs(bufs2)
+        if not args.accumulate and "error" not in other:
+            # one blocking frame through a ONE-lane renderer of that delivery (the
+            # simplest form of the n-GPU exchange) against one context's frame
+            try:
+                with mirt.MultiRenderer(list(range(n)), lanes=1, host_direct=od == "host-direct") as m1:
+                    m1.set_option(mirt.abi.MULTI_OPT_TIMEOUT_MS, 60000)
+                    m1.upload(spheres, bvh)
+                    f1 = m1.render_frame(cam, W, H, depth=DEPTH, seed=SEED, sample=0, samples=SPP, jitter=JITTER)
+                with mirt.Renderer(0) as r1:
+                    r1.upload(spheres, bvh)
+                    one1 = r1.render_frame(cam, W, H, depth=DEPTH, seed=SEED, sample=0, samples=SPP, jitter=JITTER)
+                other["one_lane_frame_equals_one_context"] = frame_sha(f1) == frame_sha(one1)
+            except Exception as e:   # noqa: BLE001
+                other["one_lane_error"] = f"{type(e).__name__}: {e}"
 
     value = W * H * SPP * args.steps / elapsed / 1e6
     line = {
