@@ -327,6 +327,14 @@ constexpr int kBounceDiag = 12;  // mirt_bounce_stats words per wave  // HNodes 
 #ifndef MIRT_QSEG
 #define MIRT_QSEG 8
 #endif
+// A/B (round 5): each segment taken from its END. The primary pass appends a
+// workgroup's first bounces when it finishes, so the records of the costly
+// (dense) tiles -- whose chains bounce longest -- sit late in each segment;
+// taking them first starts the longest chains first (longest-processing-time
+// order), so fewer of them are still running when the queue runs dry.
+#ifndef MIRT_QUEUE_REVERSE
+#define MIRT_QUEUE_REVERSE 0
+#endif
 constexpr uint32_t kQSeg = MIRT_QSEG;
 constexpr uint32_t kQLine = 32;                        // dwords per 128-B line
 constexpr size_t kQCtlBytes = 4 * kQLine * (1 + kQSeg);
@@ -830,7 +838,7 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                 const uint32_t lane0 = threadIdx.x & 63;
                 const uint32_t idx = b + (uint32_t)__popcll(need & ((1ull << lane0) - 1));
                 if (idx < sz) {
-                    const BounceRec rec = queue[lo + idx];
+                    const BounceRec rec = queue[lo + (MIRT_QUEUE_REVERSE ? sz - 1 - idx : idx)];
                     ray = Ray{rec.ox, rec.oy, rec.oz, rec.dx, rec.dy, rec.dz};
                     sr = slab_ray(ray);
                     sp = sph_ray(ray);

@@ -62,6 +62,8 @@ def main():
                               "serial_bounce_ms": sl.get("bounce_ms"), "serial_primary_ms": sl.get("primary_ms"),
                               "depth1": d["depth1_mrays_s"]}), flush=True)
     for lib, v in res.items():
+        if not v:
+            continue
         best = max(v)
         print("BEST", lib, "value %.1f bounce %.4f primary %.4f serial frame %.4f depth1 %.1f" % best)
 
