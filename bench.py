@@ -643,8 +643,17 @@ def make_scene():
     return spheres, bvh, time.perf_counter() - t0
 
 
+# --same-device (rehearsal on a one-GPU box): the N ranks all on GPU 0 -- the
+# copy exchange instead of RCCL, otherwise the N > 1 flow of a real node
+SAME_DEVICE = False
+
+
+def devices_for(n):
+    return [0] * n if SAME_DEVICE else list(range(n))
+
+
 def open_multi(n, lanes, host_direct, spheres, bvh, blocks, opts, timeout_ms=120000, ahead=False):
-    m = mirt.MultiRenderer(list(range(n)), lanes=lanes, host_direct=host_direct, queue_ahead=ahead)
+    m = mirt.MultiRenderer(devices_for(n), lanes=lanes, host_direct=host_direct, queue_ahead=ahead)
     m.set_option(mirt.abi.MULTI_OPT_TIMEOUT_MS, timeout_ms)
     m.upload(spheres, bvh)
     if blocks >= 0:
@@ -791,7 +800,7 @@ def measure(args):
             # one blocking frame through a ONE-lane renderer of that delivery (the
             # simplest form of the n-GPU exchange) against one context's frame
             try:
-                with mirt.MultiRenderer(list(range(n)), lanes=1, host_direct=od == "host-direct") as m1:
+                with mirt.MultiRenderer(devices_for(n), lanes=1, host_direct=od == "host-direct") as m1:
                     m1.set_option(mirt.abi.MULTI_OPT_TIMEOUT_MS, 60000)
                     m1.upload(spheres, bvh)
                     f1 = m1.render_frame(cam, W, H, depth=DEPTH, seed=SEED, sample=0, samples=SPP, jitter=JITTER)
@@ -853,6 +862,8 @@ def measure(args):
         line["other_delivery"] = other
     if args.opt:
         line["options"] = args.opt
+    if SAME_DEVICE:
+        line["rehearsal_same_device"] = "every rank on GPU 0 (copy exchange): a plumbing rehearsal, not a measurement"
     if n == 1:
         line.update(single_gpu_extras(args, spheres, bvh, cam, value, elapsed, bounce_ms, primary_ms, per))
     print(json.dumps(line), flush=True)
@@ -1007,11 +1018,14 @@ def main():
                     help="GPU_MAX_HW_QUEUES for the measuring process (-1: the environment's at N = 1, 16 at "
                          "N > 1; 0: keep the environment's)")
     ap.add_argument("--measure-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal: all N ranks on GPU 0 (copy exchange, no RCCL); not a measurement")
     ap.add_argument("--blocking-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--opt", action="append", default=[],
                     help="OPTION=VALUE (mirt_multi_set_option on every context), repeatable")
     args = ap.parse_args()
-    global W, H, NSPH, KIND, SPP, JITTER, WORKLOAD
+    global W, H, NSPH, KIND, SPP, JITTER, WORKLOAD, SAME_DEVICE
+    SAME_DEVICE = args.same_device
     WORKLOAD = args.workload
     wl = WORKLOADS[args.workload]
     W, H, NSPH, KIND, SPP, JITTER = wl["W"], wl["H"], wl["NSPH"], wl["KIND"], wl["SPP"], wl["JITTER"]
