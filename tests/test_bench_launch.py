@@ -108,3 +108,18 @@ def test_bench_line_one_gpu_short():
     assert d["n_gpus"] == 1 and d["value"] > 0 and d["device_resident_mrays_s"] > 0
     assert d["last_frame_equals_one_context"] is True
     assert d["config"]["delivery"] == "gather" and d["depth1_mrays_s"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_bench_line_two_ranks_same_device_rehearsal():
+    """The N > 1 flow on one GPU (--same-device: the copy exchange in place of
+    RCCL): the measuring child, the host-direct headline, the gather leg
+    beside it and the one-lane check, every checked frame equal to one
+    context's; the line is marked as a rehearsal."""
+    d = _run("--gpus", "2", "--same-device", "--steps", "8", "--warmup", "2", "--no-cpu", "--no-host", timeout=400)
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["rehearsal_same_device"]
+    assert d["config"]["delivery"] == "host-direct" and d["last_frame_equals_one_context"] is True
+    o = d["other_delivery"]
+    assert o["delivery"] == "gather" and "error" not in o, o
+    assert o["last_frame_equals_one_context"] is True and o["one_lane_frame_equals_one_context"] is True
