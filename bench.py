@@ -866,8 +866,31 @@ def measure(args):
         line["rehearsal_same_device"] = "every rank on GPU 0 (copy exchange): a plumbing rehearsal, not a measurement"
     if n == 1:
         line.update(single_gpu_extras(args, spheres, bvh, cam, value, elapsed, bounce_ms, primary_ms, per))
+    else:
+        line["reference_work"] = multi_reference_work(spheres, bvh, cam, n, elapsed, args.steps)
     print(json.dumps(line), flush=True)
     return 0
+
+
+def multi_reference_work(spheres, bvh, cam, n, elapsed, steps):
+    """N > 1, SURVEY §8(e)'s scaling figure: the REFERENCE's exhaustive-DFS
+    bytes of one frame (the same at every N: the frame does not change) per
+    second of the timed loop, over N GPUs' HBM peak -- B / t / (G x 8 TB/s).
+    Counted by the instrumented build on GPU 0 (pruning off), after the
+    measurement."""
+    try:
+        with mirt.Renderer(0) as r:
+            r.upload(spheres, bvh)
+            r.set_option(mirt.abi.OPT_PRUNE, 0)
+            ref = r.count_frame(cam, W, H, depth=DEPTH, seed=SEED, row_block=ROW_BLOCK, samples=SPP, jitter=JITTER)
+        b = algorithmic_bytes(ref, H * W * SPP)
+        gbs = b * steps / elapsed / 1e9
+        return {"definition": "SURVEY 8(d)/(e): the reference's exhaustive-DFS bytes per frame (32 B/node test + 16 "
+                              "B/sphere test + 4 B/hit colour + 4 B/pixel) per second, over G x the HBM peak",
+                "bytes_per_frame": int(b), "gbs": round(gbs, 1),
+                "frac_of_g_hbm_peak": round(gbs / (n * PEAK_HBM_GBS), 4)}
+    except Exception as e:   # noqa: BLE001 -- a counting failure must not cost the line
+        return {"error": f"{type(e).__name__}: {e}"}
 
 
 def single_gpu_extras(args, spheres, bvh, cam, value, elapsed, bounce_ms, primary_ms, per):
