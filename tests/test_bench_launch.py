@@ -123,3 +123,4 @@ def test_bench_line_two_ranks_same_device_rehearsal():
     o = d["other_delivery"]
     assert o["delivery"] == "gather" and "error" not in o, o
     assert o["last_frame_equals_one_context"] is True and o["one_lane_frame_equals_one_context"] is True
+    assert d["reference_work"]["bytes_per_frame"] > 0 and d["reference_work"]["frac_of_g_hbm_peak"] > 0
