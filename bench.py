@@ -32,7 +32,7 @@ ranks hold no GPU work and join rank 0 only at a gloo barrier at the end.
 
 The schedule: `pipeline` lanes (4 at N = 1, 8 at N > 1), each
 context's bounce pass at 1.5 persistent workgroups per CU, `batch` frames
-per launch (1 at N <= 2, 4 at N >= 4); `--tail-grid T` puts the burst's
+per launch (1 at N <= 2, 2 at N = 4, 4 at N = 8); `--tail-grid T` puts the burst's
 last T launches on the full grid (MIRT_MULTI_FULL_GRID; 0 by default: it
 lost through mirt_multi in round 5's emulation).
 
@@ -94,8 +94,11 @@ NODE_B, SPHERE_B, COLOR_B, PIXEL_B = 32, 16, 4, 4
 # one-frame split at N ranks emulated shard by shard on one GPU
 # (scripts/shard_times.py --pipeline 4 --batch B, profiles/r03d/k20_*):
 # N = 2: 4,634 / 4,517 / 4,372, N = 4: 7,286 / 7,393 / 7,966, N = 8:
-# 9,460 / 11,243 / 13,735 Mrays/s before the gather
-DEFAULT_BATCH = {1: 1, 2: 1, 4: 4, 8: 4}
+# 9,460 / 11,243 / 13,735 Mrays/s before the gather. Round 5, through
+# mirt_multi (host-direct, 8 lanes, three interleaved rounds,
+# profiles/r05_logs/r05an/): N = 2 1 / 2 frames 4,707-4,752 / 4,641-4,704;
+# N = 4 2 / 4 frames 8,165-8,452 / 7,359-7,566; N = 8 keeps 4 (r05h, r05k)
+DEFAULT_BATCH = {1: 1, 2: 1, 4: 2, 8: 4}
 # at N > 1: contexts in flight per rank and the hardware queues that gives
 # them (emulated at N = 8, K = 20, 4 frames per launch: 4 ctxs / 4 queues with
 # a gather-sized copy on a fifth stream 11.9 Grays/s, 8 queues 13.2; 8 ctxs on
