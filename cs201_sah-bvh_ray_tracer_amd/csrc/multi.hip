@@ -72,6 +72,28 @@ __global__ void __launch_bounds__(256) deinterleave_kernel(ShardSrc src, uint32_
     frames[((size_t)j * height + y) * width + x] = src.p[s][((size_t)j * src.rows[s] + row) * width + x];
 }
 
+// MIRT_MULTI_OPT_DIRECT_COPY 2: shard s's compact rows straight into the
+// row-major host frame (device-visible address of page-locked memory) by a
+// kernel, 16 B per thread, instead of a strided DMA: compact row r is image
+// row (r / rb * world + s) * rb + r % rb (host_scene.cpp shard_row_count's
+// geometry; the image's short last block lies at the slab's end).
+__global__ void __launch_bounds__(256) scatter_rows_kernel(const uint32_t* __restrict__ slab,
+                                                           uint32_t* __restrict__ frame, int width, int rows,
+                                                           int rb, int world, int s)
+{
+    const int r = blockIdx.y;
+    const int x = (int)(blockIdx.x * 256 + threadIdx.x) * 4;
+    if (r >= rows || x >= width) return;
+    const int y = (r / rb * world + s) * rb + r % rb;
+    const uint32_t* src = slab + (size_t)r * width + x;
+    uint32_t* dst = frame + (size_t)y * width + x;
+    if (x + 4 <= width && (((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+        *(uint4*)dst = *(const uint4*)src;
+    } else {
+        for (int i = 0; i < 4 && x + i < width; i++) dst[i] = src[i];
+    }
+}
+
 int hip_err(hipError_t e, const char* what)
 {
     set_error("%s: %s", what, hipGetErrorString(e));
@@ -558,6 +580,18 @@ int issue_rank_body(mirt_multi* m, Lane& L, int r)
         for (int j = 0; j < J.nframes; j++) {
             const uint32_t* sj = src + (size_t)j * elems;
             uint32_t* dj = (uint32_t*)J.dst[j];
+            if (m->direct_copy == 2 && J.sr.rows[s] > 0) {
+                // a copy kernel storing into the mapped frame (staged outputs too: page-locked)
+                uint32_t* dd = host_device_ptr(dj, 4 * (size_t)W * H);
+                if (!dd) {
+                    set_error("mirt_multi: the frame is not one mapped page-locked range (DIRECT_COPY 2)");
+                    return MIRT_E_INVALID;
+                }
+                const dim3 grid((unsigned)((W + 1023) / 1024), (unsigned)J.sr.rows[s]);
+                scatter_rows_kernel<<<grid, 256, 0, st>>>(sj, dd, W, J.sr.rows[s], rb, world, s);
+                MHIP(hipGetLastError());
+                continue;
+            }
             if (nfull > 0 && m->direct_copy == 0)
                 MHIP(hipMemcpy2DAsync(dj + (size_t)s * rb * W, (size_t)world * rb * W * 4, sj, (size_t)rb * W * 4,
                                       (size_t)rb * W * 4, nfull, hipMemcpyDeviceToHost, st));
@@ -870,7 +904,7 @@ int mirt_multi_set_option(mirt_multi* m, int option, int value)
         if (m->emu_rank >= std::max(1, value)) m->emu_rank = 0;
         return MIRT_OK;
     case MIRT_MULTI_OPT_DIRECT_COPY:
-        if (value < 0 || value > 1) break;
+        if (value < 0 || value > 2) break;
         m->direct_copy = value;
         return MIRT_OK;
     case MIRT_MULTI_OPT_COPY_STREAM:

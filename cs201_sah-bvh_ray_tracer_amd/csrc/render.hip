@@ -2537,6 +2537,9 @@ uint32_t* host_mapped(const void* p, size_t bytes)
 
 extern "C++" {
 namespace mirt {
+// The device-visible address of a page-locked host range (null if it is not
+// one contiguous mapping): mirt_multi's copy kernels store into it.
+uint32_t* host_device_ptr(const void* p, size_t bytes) { return host_mapped(p, bytes); }
 // Page-locked ranges this library handed out or registered (mirt_host_alloc /
 // mirt_host_register): checked without a HIP call, which the frame loops of
 // mirt_multi make for every output of every launch.

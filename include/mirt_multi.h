@@ -92,7 +92,8 @@ enum {
                                             delivered are NOT complete. 0 or 1 = off (default) */
     MIRT_MULTI_OPT_EMULATE_RANK = 258,
     MIRT_MULTI_OPT_DIRECT_COPY = 259,    /* MIRT_MULTI_HOST_DIRECT: each rank's blocks of a frame as one strided
-                                            copy (hipMemcpy2DAsync, 0, default) or one copy per row block (1) */
+                                            copy (hipMemcpy2DAsync, 0, default), one copy per row block (1), or
+                                            a kernel storing them into the mapped page-locked frame (2) */
     MIRT_MULTI_OPT_COPY_STREAM = 260     /* MIRT_MULTI_QUEUE_AHEAD: a launch's copies on its context's stream
                                             behind its kernels (0, default) or on the context's copy stream (1);
                                             2: on the copy stream, and a launch is enqueued only once the

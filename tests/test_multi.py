@@ -258,3 +258,33 @@ def test_multi_timeout_fails_with_status(mirt, scene10k):
     with mirt.Renderer(0) as r:
         r.upload(s, b)
         assert r.render_frame(mirt.default_camera(), 64, 36, depth=5, seed=1).shape == (36, 64, 4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices,dc", [([0, 0], 2), ([0, 0, 0], 2), ([0] * 8, 2), ([0, 0, 0], 1)])
+def test_multi_host_direct_copy_methods(gpu, mirt, scene10k, devices, dc):
+    """MIRT_MULTI_OPT_DIRECT_COPY: the ranks' rows into the host frame by a
+    copy kernel storing into the mapped page-locked frame (2) or one DMA per
+    row block (1), into page-locked and pageable outputs, ragged frames
+    (the image's short last row block): equal to one context's frames."""
+    s, b = scene10k
+    W, H = 333, 187
+    cam = mirt.default_camera()
+    hb = [mirt.HostBuffer((H, W, 4)) for _ in range(4)]
+    try:
+        with mirt.MultiRenderer(devices, lanes=2, host_direct=True) as m:
+            m.set_option(mirt.abi.MULTI_OPT_DIRECT_COPY, dc)
+            assert m.get_option(mirt.abi.MULTI_OPT_DIRECT_COPY) == dc
+            m.upload(s, b)
+            m.render_frames_async(cam, mirt.frame_desc(W, H, depth=5, seed=6, sample=0), hb[:2])
+            m.render_frames_async(cam, mirt.frame_desc(W, H, depth=5, seed=6, sample=2), hb[2:])
+            m.wait()
+            got = [x.array.copy() for x in hb]
+            pageable = m.render_frame(cam, W, H, depth=5, seed=6, sample=4)
+    finally:
+        for x in hb:
+            x.close()
+    gpu.upload(s, b)
+    for j in range(4):
+        assert (got[j] == gpu.render_frame(cam, W, H, depth=5, seed=6, sample=j)).all(), j
+    assert (pageable == gpu.render_frame(cam, W, H, depth=5, seed=6, sample=4)).all()
