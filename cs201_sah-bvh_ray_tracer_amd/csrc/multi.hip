@@ -38,6 +38,13 @@ using namespace mirt;
 namespace {
 
 constexpr int kMaxShards = 64;  // shards of one frame (ranks, or the emulated world)
+// A/B (round 5): the frame's D2H as a copy that may not use compute units
+// (the runtime otherwise runs some of these copies as blit kernels on the
+// context's compute queue: __amd_rocclr_copyBuffer in the timed loop's trace)
+#ifndef MIRT_D2H_NOCU
+#define MIRT_D2H_NOCU 0
+#endif
+constexpr hipMemcpyKind kD2HKind = MIRT_D2H_NOCU ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToHost;
 // A/B switch (measurement only): 0 gives every lane its own accumulation
 // buffer, so fresh frames write it in the render kernel with no ordered fold
 // across the lanes -- NOT exact for an accumulating frame in flight after
@@ -561,7 +568,7 @@ int issue_rank_body(mirt_multi* m, Lane& L, int r)
                     const hipStream_t cs = copy_stream(m, L, r);
                     for (int j = 0; j < J.nframes; j++)
                         MHIP(hipMemcpyAsync(J.dst[j], frames + (size_t)j * J.frame_elems, 4 * J.frame_elems,
-                                            hipMemcpyDeviceToHost, cs));
+                                            kD2HKind, cs));
                 }
             }
         }
