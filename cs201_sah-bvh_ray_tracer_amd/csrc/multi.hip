@@ -605,9 +605,14 @@ int issue_rank_body(mirt_multi* m, Lane& L, int r)
             for (int i = 0; m->direct_copy == 1 && i < nfull; i++)   // one copy per row block
                 MHIP(hipMemcpyAsync(dj + ((size_t)i * world + s) * rb * W, sj + (size_t)i * rb * W,
                                     (size_t)rb * W * 4, hipMemcpyDeviceToHost, st));
-            if (has_short)
-                MHIP(hipMemcpyAsync(dj + (size_t)last * rb * W, sj + (size_t)nfull * rb * W,
-                                    (size_t)(H - last * rb) * W * 4, hipMemcpyDeviceToHost, st));
+            // the short block as a one-row 2D copy too: a 1D copy after the strided one on the
+            // same stream cost a rank ~0.5 ms per frame (N = 2, 16-row blocks: profiles/r05_logs/r05at/),
+            // the runtime moving between its copy paths
+            if (has_short) {
+                const size_t sb = (size_t)(H - last * rb) * W * 4;
+                MHIP(hipMemcpy2DAsync(dj + (size_t)last * rb * W, sb, sj + (size_t)nfull * rb * W, sb, sb, 1,
+                                      hipMemcpyDeviceToHost, st));
+            }
         }
     }
     // the launch's last operation on this rank: its copy stream when the
