@@ -45,6 +45,16 @@ constexpr int kMaxShards = 64;  // shards of one frame (ranks, or the emulated w
 #define MIRT_D2H_NOCU 0
 #endif
 constexpr hipMemcpyKind kD2HKind = MIRT_D2H_NOCU ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToHost;
+// The frame's D2H issued as a 2D copy (H rows of W pixels, the path the
+// host-direct copies take): the runtime runs it on a DMA engine, where a 1D
+// copy of the same bytes ran as a blit kernel on the context's compute queue
+// for most frames (14 of 20 in the timed loop's trace), taking CU time from
+// the frames in flight. Measured (profiles/r05_logs/r05av/): N = 1
+// host-inclusive 2,477-2,525 -> 2,543-2,572 Mrays/s, depth 1 6,775-6,930 ->
+// 8,431-8,455.
+#ifndef MIRT_D2H_2D
+#define MIRT_D2H_2D 1
+#endif
 // A/B switch (measurement only): 0 gives every lane its own accumulation
 // buffer, so fresh frames write it in the render kernel with no ordered fold
 // across the lanes -- NOT exact for an accumulating frame in flight after
@@ -566,9 +576,14 @@ int issue_rank_body(mirt_multi* m, Lane& L, int r)
                 }
                 if (J.deliver) {
                     const hipStream_t cs = copy_stream(m, L, r);
-                    for (int j = 0; j < J.nframes; j++)
-                        MHIP(hipMemcpyAsync(J.dst[j], frames + (size_t)j * J.frame_elems, 4 * J.frame_elems,
-                                            kD2HKind, cs));
+                    for (int j = 0; j < J.nframes; j++) {
+                        if (MIRT_D2H_2D)   // as a 2D copy (H rows of W pixels): the runtime's rect copy path
+                            MHIP(hipMemcpy2DAsync(J.dst[j], 4 * (size_t)J.W, frames + (size_t)j * J.frame_elems,
+                                                  4 * (size_t)J.W, 4 * (size_t)J.W, J.H, hipMemcpyDeviceToHost, cs));
+                        else
+                            MHIP(hipMemcpyAsync(J.dst[j], frames + (size_t)j * J.frame_elems, 4 * J.frame_elems,
+                                                kD2HKind, cs));
+                    }
                 }
             }
         }

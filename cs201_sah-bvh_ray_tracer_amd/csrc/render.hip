@@ -2496,8 +2496,11 @@ int enqueue_host_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_des
     }
     uint32_t* disp = nullptr;
     if (int rc = enqueue_frame(c, cam, fd, nullptr, &disp, fn)) return rc;
-    const size_t pixels = (size_t)shard_row_count(fd) * fd->width;
-    HIP_TRY(hipMemcpyAsync(out, disp, pixels * 4, hipMemcpyDeviceToHost, c->stream));
+    // as a 2D copy (rows x width): the runtime takes a DMA engine for it, where a
+    // 1D copy of the same bytes often runs as a blit kernel on this stream's
+    // compute queue (multi.hip MIRT_D2H_2D)
+    const size_t row = (size_t)fd->width * 4;
+    HIP_TRY(hipMemcpy2DAsync(out, row, disp, row, row, (size_t)shard_row_count(fd), hipMemcpyDeviceToHost, c->stream));
     return MIRT_OK;
 }
 
