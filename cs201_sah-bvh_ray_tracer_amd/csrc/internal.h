@@ -37,6 +37,7 @@ int ctx_device(const mirt_ctx* c);
 // mirt_host_register): copies into it are DMA, asynchronous to the host.
 bool host_page_locked(const void* p, size_t bytes);
 uint32_t* host_device_ptr(const void* p, size_t bytes);
+int accum_settle(mirt_ctx* c);
 void pinned_add(const void* p, size_t bytes);   // mirt_host_alloc / mirt_host_register ranges
 void pinned_remove(const void* p);
 

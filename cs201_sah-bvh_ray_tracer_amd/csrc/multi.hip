@@ -487,6 +487,8 @@ int issue_rank_body(mirt_multi* m, Lane& L, int r)
     if (m->ahead) {
         // the lane's own slabs: every frame of the launch (spp * nframes samples)
         const size_t need = 4 * elems * (size_t)std::max(1, sd.samples) + 4;
+        if (need > L.slab_cap[r])   // a pending fold of the old slab (MIRT_LAZY_FOLD) is taken first
+            if (int g = accum_settle(c)) return g;
         if (int g = grow(m->dev[r], &L.slab[r], &L.slab_cap[r], need)) return g;
         out = L.slab[r];
     }

@@ -1520,7 +1520,20 @@ struct AccumShare {
     size_t pixels = 0;       // pixels of the running accumulation (0: none yet)
     hipEvent_t folded = nullptr;
     bool has_fold = false;   // `folded` was recorded at least once
+    // Lazy fold (round 5, MIRT_LAZY_FOLD): the display slab of the last FRESH
+    // frame issued on the share and not yet folded into d_acc. A fresh
+    // frame's accumulation state is its colours / 255 (main.c:368-370), which
+    // its slab holds exactly, so it is folded only when a frame or a read
+    // needs d_acc (accum_materialize) -- fresh frames in flight no longer wait
+    // for each other's folds, and a fresh frame superseded by a later one is
+    // never folded at all.
+    const uint32_t* pend = nullptr;
+    mirt_ctx* pend_ctx = nullptr;   // the ctx that rendered it (its slab must outlive the read)
+    hipEvent_t pend_ev = nullptr;   // recorded after that frame's render
 };
+#ifndef MIRT_LAZY_FOLD
+#define MIRT_LAZY_FOLD 1
+#endif
 
 #ifndef MIRT_PRIMARY_DEPTH1
 #define MIRT_PRIMARY_DEPTH1 1
@@ -1555,6 +1568,10 @@ struct mirt_ctx {
     // the frame scratch (queue, deferral list, phase events) is per ctx: a
     // launch on another stream than the previous one waits for it
     hipEvent_t done = nullptr;
+    // MIRT_LAZY_FOLD: another stream read this ctx's display slab for the
+    // share's pending fold; the ctx's next write to it waits for `slab_free`
+    hipEvent_t slab_free = nullptr;
+    bool slab_guard = false;
     hipStream_t last_stream = nullptr;
     bool launched = false;
     // scene (replicated per device, uploaded once)
@@ -1957,6 +1974,11 @@ AccumShare* accum_new(int device)
         delete a;
         return nullptr;
     }
+    if (hipEventCreateWithFlags(&a->pend_ev, hipEventDisableTiming) != hipSuccess) {
+        (void)hipEventDestroy(a->folded);
+        delete a;
+        return nullptr;
+    }
     return a;
 }
 
@@ -1965,7 +1987,49 @@ void accum_release(AccumShare* a)
     if (!a || --a->refs > 0) return;
     if (a->d_acc) (void)hipFree(a->d_acc);
     if (a->folded) (void)hipEventDestroy(a->folded);
+    if (a->pend_ev) (void)hipEventDestroy(a->pend_ev);
     delete a;
+}
+
+// A fresh frame's accumulation state from its display: acc = c / 255 per
+// channel, exactly store_pixel's fresh branch (main.c:368-370).
+__global__ void acc_from_display_kernel(const uint32_t* __restrict__ disp, float* __restrict__ acc, size_t n)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t c = disp[i];
+    for (int ch = 0; ch < 3; ch++) acc[3 * i + ch] = (float)((c >> (8 * ch)) & 0xff) / 255.0f;
+}
+
+// The share's pending fresh frame folded into d_acc on stream s, behind the
+// share's last fold and that frame's render; the slab's ctx then waits for
+// this read before writing its slab again.
+int accum_materialize(AccumShare* a, hipStream_t s)
+{
+    if (!a || !a->pend) return MIRT_OK;
+    if (a->has_fold) HIP_TRY(hipStreamWaitEvent(s, a->folded, 0));
+    HIP_TRY(hipStreamWaitEvent(s, a->pend_ev, 0));
+    const size_t n = a->pixels;
+    acc_from_display_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(a->pend, a->d_acc, n);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(a->folded, s));
+    a->has_fold = true;
+    mirt_ctx* pc = a->pend_ctx;
+    HIP_TRY(hipEventRecord(pc->slab_free, s));
+    pc->slab_guard = true;
+    a->pend = nullptr;
+    a->pend_ctx = nullptr;
+    return MIRT_OK;
+}
+
+// A fresh frame's display left pending on its share (MIRT_LAZY_FOLD): the
+// newest fresh frame supersedes any earlier one.
+int accum_set_pending(AccumShare* a, mirt_ctx* c, const uint32_t* disp, hipStream_t s)
+{
+    HIP_TRY(hipEventRecord(a->pend_ev, s));
+    a->pend = disp;
+    a->pend_ctx = c;
+    return MIRT_OK;
 }
 
 // The accumulation buffer for frames of `pixels` pixels, enqueued on stream
@@ -1981,6 +2045,8 @@ int accum_prepare(AccumShare* a, size_t pixels, hipStream_t s)
         a->pixels = 0;
     }
     if (a->pixels != pixels) {
+        a->pend = nullptr;   // a frame of the old geometry: a new accumulation starts
+        a->pend_ctx = nullptr;
         if (a->has_fold) HIP_TRY(hipStreamWaitEvent(s, a->folded, 0));
         HIP_TRY(hipMemsetAsync(a->d_acc, 0, pixels * 12, s));
         HIP_TRY(hipEventRecord(a->folded, s));
@@ -2035,6 +2101,10 @@ int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_ac
                   mirt_counts* d_counts, uint32_t* d_wave_stats = nullptr, uint64_t* d_bdiag = nullptr)
 {
     if (c->launched && c->last_stream != s) HIP_TRY(hipStreamWaitEvent(s, c->done, 0));
+    if (c->slab_guard) {   // another stream still reads this ctx's slab (a pending fold)
+        HIP_TRY(hipStreamWaitEvent(s, c->slab_free, 0));
+        c->slab_guard = false;
+    }
     const int rc = launch_render_body(c, f, d_out, d_acc, s, timed, d_counts, d_wave_stats, d_bdiag,
                                       d_counts ? nullptr : accum_chain(c));
     if (rc) return rc;
@@ -2065,8 +2135,22 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
     // fold into a shared buffer, whichever stream enqueued it)
     float* const d_fold = f.samples > 1 || chain ? d_acc : nullptr;
     if (d_fold) d_acc = nullptr;
+    // MIRT_LAZY_FOLD: a fresh one-sample frame on a share leaves its display
+    // pending instead of folding it; any other frame that folds first takes
+    // the pending one (an accumulating frame needs it in d_acc) or drops it (a
+    // fresh multi-sample fold overwrites d_acc whole)
+    const bool lazy = MIRT_LAZY_FOLD && chain && d_fold && !f.accumulate && f.samples == 1;
+    if (MIRT_LAZY_FOLD && chain && d_fold && !lazy) {
+        if (f.accumulate) {
+            if (int rc = accum_materialize(chain, s)) return rc;   // before this frame's render can touch a slab
+        } else {
+            chain->pend = nullptr;
+            chain->pend_ctx = nullptr;
+        }
+    }
     auto fold = [&]() -> int {
         if (!d_fold) return MIRT_OK;
+        if (lazy) return accum_set_pending(chain, c, d_out, s);
         const size_t n = (size_t)f.shard_rows * f.width;
         if (chain && chain->has_fold) HIP_TRY(hipStreamWaitEvent(s, chain->folded, 0));
         fold_samples_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(f, d_out, d_fold);
@@ -2261,6 +2345,7 @@ int mirt_create(int device, mirt_ctx** out)
         if (e == hipSuccess) e = hipEventCreate(&c->ph2[k]);
     }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->slab_free, hipEventDisableTiming);
     if (e == hipSuccess) e = hipMalloc((void**)&c->d_counts, sizeof(mirt_counts));
     if (e == hipSuccess) {
         c->acc = accum_new(device);
@@ -2287,7 +2372,10 @@ void mirt_destroy(mirt_ctx* c)
 {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    // a share that lives on must not keep a pending fold of this ctx's slab
+    if (c->acc && c->acc->refs > 1 && c->acc->pend_ctx == c) (void)accum_materialize(c->acc, c->stream);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->slab_guard) (void)hipEventSynchronize(c->slab_free);   // another stream's read of the slab
     accum_release(c->acc);
     for (void* p : {(void*)c->d_nodes, (void*)c->d_nodes32, (void*)c->d_geo, (void*)c->d_color, (void*)c->d_out,
                     c->d_in, c->d_res, (void*)c->d_counts, (void*)c->d_defer, c->d_queue, c->d_cq, (void*)c->d_keys, (void*)c->d_pnodes,
@@ -2300,6 +2388,7 @@ void mirt_destroy(mirt_ctx* c)
         for (hipEvent_t ev : {c->ph0[k], c->ph1[k], c->ph2[k]})
             if (ev) (void)hipEventDestroy(ev);
     if (c->done) (void)hipEventDestroy(c->done);
+    if (c->slab_free) (void)hipEventDestroy(c->slab_free);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -2453,6 +2542,18 @@ int enqueue_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd
     }
     const FrameConst f = make_frame_const(cam, fd);
     const size_t pixels = (size_t)f.shard_rows * f.width;  // one frame (several: slab j = display after frame j)
+    if (!d_out && c->out_cap < pixels * f.samples * 4 + 4) {
+        // the slab is reallocated: a pending fold of it is taken first, and
+        // any other stream's read of it has ended
+        if (c->acc->pend_ctx == c) {
+            if (int rc = accum_materialize(c->acc, c->stream)) return rc;
+        }
+        if (c->slab_guard) {
+            HIP_TRY(hipEventSynchronize(c->slab_free));
+            c->slab_guard = false;
+        }
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
     if (!d_out) {
         int rc = ensure((void**)&c->d_out, &c->out_cap, pixels * f.samples * 4 + 4);
         if (rc) return rc;
@@ -2473,6 +2574,12 @@ int enqueue_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd
         f1.samples = 1;
         f1.accumulate = 0;
         AccumShare* chain = accum_chain(c);
+        if (MIRT_LAZY_FOLD && chain) {
+            // fresh frames: the last one's display left pending on the share
+            if (int rc2 = accum_set_pending(chain, c, *d_display, c->stream)) return rc2;
+            HIP_TRY(hipEventRecord(c->done, c->stream));
+            return MIRT_OK;
+        }
         if (chain && chain->has_fold) HIP_TRY(hipStreamWaitEvent(c->stream, chain->folded, 0));
         fold_samples_kernel<<<(unsigned)((pixels + 255) / 256), 256, 0, c->stream>>>(f1, *d_display, c->acc->d_acc);
         HIP_TRY(hipGetLastError());
@@ -2543,6 +2650,20 @@ namespace mirt {
 // The device-visible address of a page-locked host range (null if it is not
 // one contiguous mapping): mirt_multi's copy kernels store into it.
 uint32_t* host_device_ptr(const void* p, size_t bytes) { return host_mapped(p, bytes); }
+// Before a caller frees or reallocates an external slab ctx c rendered into:
+// a pending fold of it is taken now and every read of it has ended.
+int accum_settle(mirt_ctx* c)
+{
+    if (c->acc && c->acc->pend_ctx == c) {
+        if (int rc = accum_materialize(c->acc, c->stream)) return rc;
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->slab_guard) {
+        HIP_TRY(hipEventSynchronize(c->slab_free));
+        c->slab_guard = false;
+    }
+    return MIRT_OK;
+}
 // Page-locked ranges this library handed out or registered (mirt_host_alloc /
 // mirt_host_register): checked without a HIP call, which the frame loops of
 // mirt_multi make for every output of every launch.
@@ -2675,6 +2796,7 @@ int mirt_accum_download(mirt_ctx* c, float* out, size_t count)
         return MIRT_E_INVALID;
     }
     // after every fold enqueued so far, whichever ctx's stream carries it
+    if (int rc = accum_materialize(a, c->stream)) return rc;
     if (a->has_fold) HIP_TRY(hipStreamWaitEvent(c->stream, a->folded, 0));
     HIP_TRY(hipMemcpyAsync(out, a->d_acc, count * sizeof(float), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -2707,8 +2829,16 @@ int mirt_ctx_share_accum(mirt_ctx* c, mirt_ctx* owner)
         }
         next->refs++;
     }
-    // c's frames enqueued so far still use its old buffer
+    // c's frames enqueued so far still use its old buffer (and a pending
+    // fold of c's slab is taken into it before c leaves)
+    if (c->acc->pend_ctx == c) {
+        if (int rc = accum_materialize(c->acc, c->stream)) return rc;
+    }
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->slab_guard) {
+        HIP_TRY(hipEventSynchronize(c->slab_free));
+        c->slab_guard = false;
+    }
     accum_release(c->acc);
     c->acc = next;
     return MIRT_OK;

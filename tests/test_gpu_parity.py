@@ -361,6 +361,87 @@ def test_shared_accumulation_frames_in_flight(gpu, mirt, oracle, small, W, H, n)
             x.close()
 
 
+def test_lazy_fold_fresh_frames_in_flight(gpu, mirt):
+    """MIRT_LAZY_FOLD: fresh frames on four ctxs sharing one accumulation
+    buffer leave their displays pending instead of folding in order. After
+    six fresh frames in flight the shared buffer (read back) is the last
+    frame's colours / 255; an accumulating frame on ANOTHER ctx then continues
+    from it; a fresh frame on the pending frame's OWN ctx supersedes it; and
+    the frames shown equal one ctx's blocking sequence throughout."""
+    W, H = 320, 180
+    s, b = _scene(mirt, "render", 10000)
+    cam = mirt.default_camera()
+    rs = [mirt.Renderer(0) for _ in range(4)]
+    bufs = [mirt.HostBuffer((H, W, 4)) for _ in rs]
+    try:
+        for x in rs:
+            x.upload(s, b)
+            x.share_accum(rs[0])
+        seq = [(k, False, 1) for k in range(7)] + [(7, True, 2), (8, True, 3), (9, False, 1), (10, True, 2)]
+        # frame 6 supersedes frame 5 on the same ctx; frame 7 (another ctx) takes frame 6's pending
+        # display from ctx 1's slab; frame 8 then writes that slab (its guard); frame 10 accumulates
+        # on the ctx whose own slab holds the pending frame 9
+        ctx_of = [0, 1, 2, 3, 0, 1, 1, 3, 1, 0, 0]
+        got = []
+        for j, (k, acc, fr) in enumerate(seq):
+            i = ctx_of[j]
+            rs[i].wait()
+            fd = mirt.frame_desc(W, H, depth=5, seed=9, sample=k, accumulate=acc, frames=fr)
+            rs[i].render_frame_async(cam, fd, bufs[i])
+            rs[i].wait()
+            got.append(bufs[i].array.copy())
+            if j == 5:
+                shared_after_fresh = rs[2].accum(W * H * 3)
+        gpu.upload(s, b)
+        for j, (k, acc, fr) in enumerate(seq):
+            want = gpu.render_frame(cam, W, H, depth=5, seed=9, sample=k, accumulate=acc, frames=fr)
+            assert (got[j] == want).all(), j
+            if j == 5:
+                assert shared_after_fresh.tobytes() == gpu.accum(W * H * 3).tobytes()
+        assert rs[3].accum(W * H * 3).tobytes() == gpu.accum(W * H * 3).tobytes()
+    finally:
+        for x in bufs:
+            x.close()
+        for x in rs:
+            x.close()
+
+
+def test_lazy_fold_many_in_flight(gpu, mirt):
+    """Fresh frames issued on four sharing ctxs WITHOUT waiting between them
+    (each ctx waits only for its own previous frame), then one accumulating
+    frame: it must continue from the LAST fresh frame issued, whichever ctx
+    finished last."""
+    W, H = 640, 360
+    s, b = _scene(mirt, "render", 10000)
+    cam = mirt.default_camera()
+    rs = [mirt.Renderer(0) for _ in range(4)]
+    bufs = [mirt.HostBuffer((H, W, 4)) for _ in rs]
+    try:
+        for x in rs:
+            x.upload(s, b)
+            x.share_accum(rs[0])
+        for k in range(9):
+            i = k % 4
+            rs[i].wait()
+            rs[i].render_frame_async(cam, mirt.frame_desc(W, H, depth=5, seed=2, sample=k), bufs[i])
+        i = 9 % 4
+        rs[i].wait()
+        rs[i].render_frame_async(cam, mirt.frame_desc(W, H, depth=5, seed=2, sample=9, accumulate=True, frames=2),
+                                 bufs[i])
+        for x in rs:
+            x.wait()
+        got = bufs[i].array.copy()
+        gpu.upload(s, b)
+        gpu.render_frame(cam, W, H, depth=5, seed=2, sample=8)
+        want = gpu.render_frame(cam, W, H, depth=5, seed=2, sample=9, accumulate=True, frames=2)
+        assert (got == want).all()
+    finally:
+        for x in bufs:
+            x.close()
+        for x in rs:
+            x.close()
+
+
 def test_share_after_private_async_frames(gpu, mirt):
     """A ctx that starts sharing a buffer whose owner still has frames in
     flight that wrote it privately (no fold event): the sharer's first fold
