@@ -1534,6 +1534,14 @@ struct AccumShare {
 #ifndef MIRT_LAZY_FOLD
 #define MIRT_LAZY_FOLD 1
 #endif
+// The same for a launch of several fresh frames (mirt_multi at N >= 4): off --
+// there the ordered fold per launch keeps the lanes finishing in the order the
+// caller rotates through them; left pending, the slowest shard of an 8-way
+// split ran 2-4% slower (four interleaved rounds, profiles/r05_logs/r05bc/),
+// where a one-frame launch gains (N = 1 +1.8%, depth 1 +4.7%, r05ax/)
+#ifndef MIRT_LAZY_FOLD_BATCH
+#define MIRT_LAZY_FOLD_BATCH 0
+#endif
 
 #ifndef MIRT_PRIMARY_DEPTH1
 #define MIRT_PRIMARY_DEPTH1 1
@@ -2574,7 +2582,7 @@ int enqueue_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd
         f1.samples = 1;
         f1.accumulate = 0;
         AccumShare* chain = accum_chain(c);
-        if (MIRT_LAZY_FOLD && chain) {
+        if (MIRT_LAZY_FOLD_BATCH && chain) {
             // fresh frames: the last one's display left pending on the share
             if (int rc2 = accum_set_pending(chain, c, *d_display, c->stream)) return rc2;
             HIP_TRY(hipEventRecord(c->done, c->stream));
