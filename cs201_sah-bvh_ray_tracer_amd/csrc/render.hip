@@ -2588,6 +2588,10 @@ int enqueue_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd
             HIP_TRY(hipEventRecord(c->done, c->stream));
             return MIRT_OK;
         }
+        if (chain) {   // this fold is newer than a pending fresh display: that one is dropped
+            chain->pend = nullptr;
+            chain->pend_ctx = nullptr;
+        }
         if (chain && chain->has_fold) HIP_TRY(hipStreamWaitEvent(c->stream, chain->folded, 0));
         fold_samples_kernel<<<(unsigned)((pixels + 255) / 256), 256, 0, c->stream>>>(f1, *d_display, c->acc->d_acc);
         HIP_TRY(hipGetLastError());

@@ -288,3 +288,32 @@ def test_multi_host_direct_copy_methods(gpu, mirt, scene10k, devices, dc):
     for j in range(4):
         assert (got[j] == gpu.render_frame(cam, W, H, depth=5, seed=6, sample=j)).all(), j
     assert (pageable == gpu.render_frame(cam, W, H, depth=5, seed=6, sample=4)).all()
+
+
+@pytest.mark.gpu
+def test_multi_lazy_then_batch_then_accumulate(gpu, mirt, scene10k):
+    """A one-frame fresh launch (its display left pending on the lanes'
+    shared buffer), then a launch of two fresh frames (folded in order: it
+    supersedes the pending one), then an accumulating frame: equal to one
+    context's sequence (MIRT_LAZY_FOLD with batched launches)."""
+    s, b = scene10k
+    W, H = 320, 180
+    cam = mirt.default_camera()
+    hb = [mirt.HostBuffer((H, W, 4)) for _ in range(4)]
+    try:
+        with mirt.MultiRenderer([0, 0], lanes=3) as m:
+            m.upload(s, b)
+            m.render_frame_async(cam, mirt.frame_desc(W, H, depth=5, seed=8, sample=0), hb[0])
+            m.render_frames_async(cam, mirt.frame_desc(W, H, depth=5, seed=8, sample=1), hb[1:3])
+            m.render_frame_async(cam, mirt.frame_desc(W, H, depth=5, seed=8, sample=3, accumulate=True, frames=2),
+                                 hb[3])
+            m.wait()
+            got = [x.array.copy() for x in hb]
+    finally:
+        for x in hb:
+            x.close()
+    gpu.upload(s, b)
+    want = [gpu.render_frame(cam, W, H, depth=5, seed=8, sample=k) for k in range(3)]
+    want.append(gpu.render_frame(cam, W, H, depth=5, seed=8, sample=3, accumulate=True, frames=2))
+    for j in range(4):
+        assert (got[j] == want[j]).all(), j
