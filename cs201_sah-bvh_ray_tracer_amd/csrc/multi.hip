@@ -59,6 +59,11 @@ constexpr hipMemcpyKind kD2HKind = MIRT_D2H_NOCU ? hipMemcpyDeviceToDeviceNoCU :
 // buffer, so fresh frames write it in the render kernel with no ordered fold
 // across the lanes -- NOT exact for an accumulating frame in flight after
 // fresh frames of other lanes
+// A/B (round 5): launches complete in issue order by a stream barrier on the
+// previous launch's completion event (with MIRT_LAZY_FOLD_BATCH: no fold kernel)
+#ifndef MIRT_MULTI_ORDER_DONE
+#define MIRT_MULTI_ORDER_DONE 0
+#endif
 #ifndef MIRT_MULTI_SHARE_ACCUM
 #define MIRT_MULTI_SHARE_ACCUM 1
 #endif
@@ -634,6 +639,13 @@ int issue_rank_body(mirt_multi* m, Lane& L, int r)
     }
     // the launch's last operation on this rank: its copy stream when the
     // lane has one (it waited for everything the context's stream did)
+    if (MIRT_MULTI_ORDER_DONE) {
+        // launches complete in issue order (the order the caller rotates through
+        // the lanes), by a barrier on the previous launch's completion: the
+        // ordering the per-launch fold chain gave, without its kernel
+        const int li = (int)(&L - m->lanes.data()), nl = (int)m->lanes.size();
+        MHIP(hipStreamWaitEvent(copy_stream(m, L, r), m->lanes[(li + nl - 1) % nl].done[r], 0));
+    }
     MHIP(hipEventRecord(L.done[r], copy_stream(m, L, r)));
     return MIRT_OK;
 }
