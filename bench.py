@@ -27,7 +27,10 @@ touches a GPU; it starts ONE fresh child (`--measure-child`) with
 GPU_MAX_HW_QUEUES raised to 16 in its environment (read when the child's
 HIP runtime starts: one hardware queue per lane's stream) and relays its
 line; a child still running after --rank-timeout seconds is terminated and
-the parent exits 124. Under torchrun the same happens in rank 0; the other
+the parent exits 124 -- unless the child had already measured the headline
+and saved its line (before the secondary delivery's leg, whose n-GPU RCCL
+exchange is the untried part): then the parent prints that line, the
+unfinished leg marked in `other_delivery`, and exits 0. Under torchrun the same happens in rank 0; the other
 ranks hold no GPU work and join rank 0 only at a gloo barrier at the end.
 
 The schedule: `pipeline` lanes (4 at N = 1, 8 at N > 1), each
@@ -53,6 +56,7 @@ import json
 import os
 import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -526,7 +530,25 @@ def launcher_main(args, world_env, rank):
                 have = 0
             if have < q:
                 env["GPU_MAX_HW_QUEUES"] = str(q)
-        rc = spawn_child(env, args.rank_timeout, child_argv())
+        fd, partial = tempfile.mkstemp(prefix="mirt_bench_", suffix=".json")
+        os.close(fd)
+        os.remove(partial)        # the child creates it once the headline is measured
+        env[PARTIAL_ENV] = partial
+        try:
+            rc = spawn_child(env, args.rank_timeout, child_argv())
+            if os.path.exists(partial):
+                # the child measured the headline, then did not finish (its
+                # status is in the line): print the saved line in its place
+                with open(partial) as f:
+                    part = json.load(f)
+                part["measuring_process_exit"] = rc
+                print(f"bench.py: the measuring process exited {rc} after saving its headline; printing the "
+                      "saved line (the unfinished leg is marked in other_delivery)", file=sys.stderr, flush=True)
+                print(json.dumps(part), flush=True)
+                rc = 0
+        finally:
+            if os.path.exists(partial):
+                os.remove(partial)
     if pg:
         # the job ends together: rank 0 reports the child's status
         t = torch.tensor([rc], dtype=torch.int64)
@@ -542,7 +564,8 @@ def dry_main(args):
     slabs through both deliveries' index math (shard.py's restatements of
     multi.hip's deinterleave_kernel and strided host copies), the frame plan
     and the timing. MIRT_BENCH_DRY_HANG=1 makes the child hang (the deadline
-    tests)."""
+    tests; "after-headline": the child saves its line as measure() does
+    before the secondary leg, then hangs)."""
     if os.environ.get("MIRT_BENCH_DRY_HANG") == "1":
         time.sleep(3600)
     n = args.gpus
@@ -559,14 +582,19 @@ def dry_main(args):
     got_d = shard.assemble_direct(slabs, H, ROW_BLOCK)
     dt = time.perf_counter() - t0
     ok = bool((got_g == want).all() and (got_d == want).all())
-    print(json.dumps({"metric": METRIC, "value": None, "unit": "Mrays/s", "n_gpus": n, "steps": args.steps,
-                      "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "strong",
-                      "vs_baseline": None, "dtype": "f32", "dry": True,
-                      "data": "synthetic slabs (no rendering): launcher / shard geometry / delivery plumbing check",
-                      "frame_assembled_ok": ok, "assemble_ms": round(dt * 1e3, 3),
-                      "config": {"workload": WORKLOADS[args.workload]["desc"], "name": args.workload,
-                                 "frames_per_launch": frames,
-                                 "parallelism": f"row-block shard x{n}, one process (mirt_multi)"}}), flush=True)
+    line = {"metric": METRIC, "value": None, "unit": "Mrays/s", "n_gpus": n, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f32", "dry": True,
+            "data": "synthetic slabs (no rendering): launcher / shard geometry / delivery plumbing check",
+            "frame_assembled_ok": ok, "assemble_ms": round(dt * 1e3, 3),
+            "config": {"workload": WORKLOADS[args.workload]["desc"], "name": args.workload,
+                       "frames_per_launch": frames, "delivery": "gather" if n == 1 else "host-direct",
+                       "parallelism": f"row-block shard x{n}, one process (mirt_multi)"}}
+    if os.environ.get("MIRT_BENCH_DRY_HANG") == "after-headline":
+        save_partial(line, n, args)
+        time.sleep(3600)
+    drop_partial()
+    print(json.dumps(line), flush=True)
     return 0
 
 
@@ -762,6 +790,59 @@ def measure(args):
             r1.upload(spheres, bvh)
             one = r1.render_frame(cam, W, H, depth=DEPTH, seed=SEED, sample=last_sample, samples=SPP, jitter=JITTER)
             same = frame_sha(one) == frame_sha(last_frame)
+    value = W * H * SPP * args.steps / elapsed / 1e6
+    line = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "Mrays/s",
+        "n_gpus": n,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (create_random_sphere scene, srand(1); default camera main.c:203-211)",
+        "config": {"workload": WORKLOADS[WORKLOAD]["desc"], "name": WORKLOAD,
+                   "width": W, "height": H, "spheres": NSPH, "scene": KIND, "max_depth": DEPTH, "spp": SPP,
+                   "jitter": JITTER, "frames_per_step": 1, "frames_per_launch": per,
+                   "launches": len(timed_launches), "pipeline": lanes, "queue_ahead": ahead,
+                   "bounce_blocks": blocks,
+                   "tail_grid": len(tail), "bvh_nodes": len(bvh), "row_block": ROW_BLOCK,
+                   "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+                   "delivery": delivery,
+                   "step": ("1 frame of the still-camera display loop (main.c:379-408), lanes sharing one "
+                            "accumulation buffer" if args.accumulate else "1 fresh frame (main.c:358-374)")
+                           + f", {SPP} sample(s), {per} frame(s) per launch, launches rotating over {lanes} lanes, "
+                             "every frame delivered to page-locked host memory",
+                   "parallelism": (f"row-block shard x{n}, one process: mirt_multi over ncclCommInitAll, "
+                                   + ("one D2H per frame" if n == 1 else "RCCL gather to GPU 0 + D2H"
+                                      if delivery == "gather" else "per-GPU strided D2H into the host frame"))},
+        "timing": "one process drives all GPUs (include/mirt_multi.h); the timed region is bracketed by "
+                  "mirt_multi_wait on both sides, so it ends when every frame is in host memory on every lane",
+        "device_resident_mrays_s": round(W * H * SPP * args.steps / el_dev / 1e6, 3) if el_dev else None,
+        "device_resident_note": ("the same launches with the frames left in device memory (no D2H)" if n == 1 else
+                                 "the same launches with every frame gathered on GPU 0 over RCCL and "
+                                 "de-interleaved there (no D2H)"),
+        "depth1_mrays_s": round(W * H * SPP * args.steps / el_d1 / 1e6, 3),
+        "bvh_build_s": round(build_s, 4),
+        "frame_sha_last": frame_sha(last_frame),
+        "last_frame_equals_one_context": same,
+        "phases_under_overlap_ms": {"primary": round(primary_ms, 4), "bounce": round(bounce_ms, 4),
+                                    "launches": len(phases)},
+        "host_enqueue_ms_per_launch": {"median": enqueue_ms[0], "max": enqueue_ms[1],
+                                       "note": "host time of one mirt_multi_render_frames_async (every rank's "
+                                               "launch issued from this one thread; includes waiting for the "
+                                               "lane's previous launch)"},
+    }
+    if n > 1:
+        line["reference_work"] = multi_reference_work(spheres, bvh, cam, n, elapsed, args.steps)
+    if SAME_DEVICE:
+        line["rehearsal_same_device"] = "every rank on GPU 0 (copy exchange): a plumbing rehearsal, not a measurement"
+    if args.opt:
+        line["options"] = args.opt
+    save_partial(line, n, args)
     # the other delivery at N > 1: the RCCL gather to GPU 0, to host memory
     # and device-resident (a second renderer, same schedule). It is measured
     # BESIDE the headline: an error in it (the n-GPU RCCL exchange has not run
@@ -814,65 +895,48 @@ def measure(args):
             except Exception as e:   # noqa: BLE001
                 other["one_lane_error"] = f"{type(e).__name__}: {e}"
 
-    value = W * H * SPP * args.steps / elapsed / 1e6
-    line = {
-        "metric": METRIC,
-        "value": round(value, 3),
-        "unit": "Mrays/s",
-        "n_gpus": n,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "strong",
-        "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic (create_random_sphere scene, srand(1); default camera main.c:203-211)",
-        "config": {"workload": WORKLOADS[WORKLOAD]["desc"], "name": WORKLOAD,
-                   "width": W, "height": H, "spheres": NSPH, "scene": KIND, "max_depth": DEPTH, "spp": SPP,
-                   "jitter": JITTER, "frames_per_step": 1, "frames_per_launch": per,
-                   "launches": len(timed_launches), "pipeline": lanes, "queue_ahead": ahead,
-                   "bounce_blocks": blocks,
-                   "tail_grid": len(tail), "bvh_nodes": len(bvh), "row_block": ROW_BLOCK,
-                   "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
-                   "delivery": delivery,
-                   "step": ("1 frame of the still-camera display loop (main.c:379-408), lanes sharing one "
-                            "accumulation buffer" if args.accumulate else "1 fresh frame (main.c:358-374)")
-                           + f", {SPP} sample(s), {per} frame(s) per launch, launches rotating over {lanes} lanes, "
-                             "every frame delivered to page-locked host memory",
-                   "parallelism": (f"row-block shard x{n}, one process: mirt_multi over ncclCommInitAll, "
-                                   + ("one D2H per frame" if n == 1 else "RCCL gather to GPU 0 + D2H"
-                                      if delivery == "gather" else "per-GPU strided D2H into the host frame"))},
-        "timing": "one process drives all GPUs (include/mirt_multi.h); the timed region is bracketed by "
-                  "mirt_multi_wait on both sides, so it ends when every frame is in host memory on every lane",
-        "device_resident_mrays_s": round(W * H * SPP * args.steps / el_dev / 1e6, 3) if el_dev else None,
-        "device_resident_note": ("the same launches with the frames left in device memory (no D2H)" if n == 1 else
-                                 "the same launches with every frame gathered on GPU 0 over RCCL and "
-                                 "de-interleaved there (no D2H)"),
-        "depth1_mrays_s": round(W * H * SPP * args.steps / el_d1 / 1e6, 3),
-        "bvh_build_s": round(build_s, 4),
-        "frame_sha_last": frame_sha(last_frame),
-        "last_frame_equals_one_context": same,
-        "phases_under_overlap_ms": {"primary": round(primary_ms, 4), "bounce": round(bounce_ms, 4),
-                                    "launches": len(phases)},
-        "host_enqueue_ms_per_launch": {"median": enqueue_ms[0], "max": enqueue_ms[1],
-                                       "note": "host time of one mirt_multi_render_frames_async (every rank's "
-                                               "launch issued from this one thread; includes waiting for the "
-                                               "lane's previous launch)"},
-    }
     if other:
         line["value_" + other["delivery"].replace("-", "_")] = other.get("mrays_s")
         line["other_delivery"] = other
-    if args.opt:
-        line["options"] = args.opt
-    if SAME_DEVICE:
-        line["rehearsal_same_device"] = "every rank on GPU 0 (copy exchange): a plumbing rehearsal, not a measurement"
+    if el_dev:
+        line["device_resident_mrays_s"] = round(W * H * SPP * args.steps / el_dev / 1e6, 3)
     if n == 1:
         line.update(single_gpu_extras(args, spheres, bvh, cam, value, elapsed, bounce_ms, primary_ms, per))
-    else:
-        line["reference_work"] = multi_reference_work(spheres, bvh, cam, n, elapsed, args.steps)
+    drop_partial()
     print(json.dumps(line), flush=True)
     return 0
+
+
+# N > 1: the measuring child saves its line here once the headline loop and
+# its frame check are done, before the other delivery's leg (whose n-GPU RCCL
+# exchange has not yet run on a multi-GPU node). If the child is then stopped
+# at the deadline or dies, the parent prints this line, so a stuck secondary
+# leg cannot cost the headline; the file is removed before the child prints.
+PARTIAL_ENV = "MIRT_BENCH_PARTIAL"
+
+
+def save_partial(line, n, args):
+    path = os.environ.get(PARTIAL_ENV)
+    if not path or n == 1:
+        return
+    part = dict(line)
+    if not args.no_other:
+        od = "gather" if part["config"]["delivery"] == "host-direct" else "host-direct"
+        part["other_delivery"] = {"delivery": od, "error": "not finished: the measuring process ended in this leg "
+                                                           "(terminated at --rank-timeout, or died); this line was "
+                                                           "saved before it"}
+    with open(path + ".tmp", "w") as f:
+        json.dump(part, f)
+    os.replace(path + ".tmp", path)
+
+
+def drop_partial():
+    path = os.environ.get(PARTIAL_ENV)
+    if path:
+        try:
+            os.remove(path)
+        except FileNotFoundError:
+            pass
 
 
 def multi_reference_work(spheres, bvh, cam, n, elapsed, steps):

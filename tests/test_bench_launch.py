@@ -68,6 +68,33 @@ def test_stuck_child_hits_the_deadline():
     assert "deadline" in p.stderr
 
 
+def test_stuck_secondary_leg_keeps_the_headline():
+    """A measuring process stuck AFTER its headline (in the other delivery's
+    n-GPU RCCL leg) costs that leg only: at --rank-timeout the parent prints
+    the line the child saved before the leg, the leg marked unfinished, the
+    child's exit status in the line, and exits 0 with exactly one line."""
+    deadline = 15.0
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry", "--steps", "2",
+                        "--warmup", "1", "--rank-timeout", str(deadline)], capture_output=True, text=True,
+                       timeout=120, env=_env(MIRT_BENCH_DRY_HANG="after-headline"), cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = _lines(p.stdout)
+    assert len(lines) == 1, p.stdout
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["frame_assembled_ok"] is True and d["measuring_process_exit"] == 124
+    assert d["other_delivery"]["delivery"] == "gather" and "not finished" in d["other_delivery"]["error"]
+
+
+def test_finished_child_leaves_no_saved_line(tmp_path):
+    """A child that finishes prints its own line and removes the saved one."""
+    path = str(tmp_path / "partial.json")
+    with open(path, "w") as f:
+        f.write("{}")         # as if saved before a secondary leg
+    d = _run("--gpus", "2", "--dry", "--steps", "2", "--warmup", "1", "--measure-child",
+             env=_env(MIRT_BENCH_PARTIAL=path))
+    assert "measuring_process_exit" not in d and not os.path.exists(path)
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
