@@ -1012,6 +1012,16 @@ def single_gpu_extras(args, spheres, bvh, cam, value, elapsed, bounce_ms, primar
         bm["source"] = (os.path.relpath(pmc_path, ROOT) + " (medians over the dispatches of the timed launch shape, "
                         "one rocprofv3 --pmc pass of this command per counter set; rocprofv3 serialises the "
                         "dispatches it counts)")
+    # the blocking leg in THIS process, after the timed burst (beside the
+    # child's figure below: zero-copy stores ran ~3% slower here)
+    after_burst = None
+    if not args.no_host:
+        try:
+            ab = blocking_leg(r, cam, n=11)
+            after_burst = {k: ab[k] for k in ("pinned_ms", "pinned_mrays_s", "registered_mrays_s",
+                                              "pageable_mrays_s", "equal")}
+        except Exception as e:   # noqa: BLE001 -- an extra figure must not cost the line
+            after_burst = {"error": f"{type(e).__name__}: {e}"}
     r.close()
     out = {
         "roofline": roof,
@@ -1064,6 +1074,10 @@ def single_gpu_extras(args, spheres, bvh, cam, value, elapsed, bounce_ms, primar
                             "(MIRT_OPT_ZERO_COPY), median of 11, in a child process holding one ctx and its frame "
                             "buffer, as main.c's loop runs (bench.py --blocking-child); pageable = the caller's "
                             "plain malloc'd buffer, the same process")})
+        if after_burst:
+            after_burst["note"] = ("the same blocking leg in the bench's own process after the timed burst "
+                                   "(pinned = zero-copy into mirt_host_alloc memory, pageable = a malloc'd buffer)")
+            out["host_blocking_after_burst"] = after_burst
     if not args.no_cpu:
         cb = cpu_baseline()
         out["cpu_baseline"] = cb
