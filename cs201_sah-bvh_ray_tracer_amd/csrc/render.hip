@@ -451,9 +451,12 @@ __global__ __launch_bounds__(256) MIRT_PRIMARY_ATTR void primary_kernel(DevScene
     if (!ORD && dfr.blocks > 0 && alive && slab_ray(ray).generic) alive = false;  // traced by a deferred wave
     float t;
     int s;
-    if constexpr (ORD)
-        closest_packet_ordered<FAST, false>(sc, ray, alive, t, s, cnt);
-    else
+    if constexpr (ORD) {
+        if (MIRT_PACKET_HALVES)
+            closest_packet_halves<FAST, false>(sc, ray, alive, t, s, cnt);
+        else
+            closest_packet_ordered<FAST, false>(sc, ray, alive, t, s, cnt);
+    } else
         closest_hit<true, FAST, false>(sc, ray, alive, t, s, cnt);
     const size_t i = (size_t)r * f.width + x;
     bool push = false;
