@@ -86,6 +86,13 @@ class Counts(C.Structure):
                 ("hits_primary", C.c_uint64)]
 
 
+class MultiStats(C.Structure):
+    """mirt_multi_stats (include/mirt_multi.h)"""
+    _fields_ = [("launches", C.c_uint64), ("comm_inits", C.c_uint64), ("rccl_groups", C.c_uint64),
+                ("rccl_sends", C.c_uint64), ("rccl_recvs", C.c_uint64), ("rccl_bytes", C.c_uint64),
+                ("device_copies", C.c_uint64)]
+
+
 def default_camera():
     """main.c:203-211: position (0,4,50), looking down -z, fov 45, yaw -pi."""
     cam = Camera()
@@ -160,7 +167,6 @@ SIGNATURES = [
     ("mirt_last_phase_ms", I, [P, C.POINTER(C.c_float)]),
     ("mirt_phase_log", I, [P, C.POINTER(C.c_float), I]),
     ("mirt_bounce_stats", I, [P, P, P, P, I]),
-    ("mirt_cont_queue_stats", I, [P, P, I]),
     ("mirt_set_option", I, [P, I, I]),
     ("mirt_get_option", I, [P, I]),
     # include/mirt_dropin.h: the per-ray surface
@@ -192,14 +198,17 @@ SIGNATURES = [
     ("mirt_multi_render_frame_async", I, [P, P, P, P]),
     ("mirt_multi_render_frames_async", I, [P, P, P, I, I, C.POINTER(P)]),
     ("mirt_multi_wait", I, [P]),
+    ("mirt_multi_get_stats", I, [P, P]),
+    ("mirt_multi_read_gathered", I, [P, I, I, I, P, C.c_size_t]),
 ]
 
 OPT_TRAVERSAL, OPT_FAST_SLAB, OPT_BLOCK_WAVES, OPT_DEFER, OPT_BOUNCE_THRESHOLD, OPT_PRUNE, OPT_ORDERED = (
     1, 2, 3, 4, 5, 6, 7)
 OPT_BOUNCE_BLOCKS, OPT_QUAD_DRAIN, OPT_LEAF_BATCH, OPT_QUAD_BATCH, OPT_ZERO_COPY = 9, 11, 14, 15, 17
-OPT_QUEUE_ORDER, OPT_DEBUG_STALL_MS, OPT_CONT_QUEUE = 18, 19, 20
+OPT_QUEUE_ORDER, OPT_DEBUG_STALL_MS = 18, 19
 TRAV_TILE, TRAV_WAVEFRONT = 0, 5
 MULTI_COPY, MULTI_HOST_DIRECT, MULTI_QUEUE_AHEAD = 1, 2, 4
 MULTI_FULL_GRID = 1
 MULTI_OPT_TIMEOUT_MS, MULTI_OPT_EMULATE_WORLD, MULTI_OPT_EMULATE_RANK, MULTI_OPT_DIRECT_COPY = 256, 257, 258, 259
 MULTI_OPT_COPY_STREAM = 260
+MULTI_OPT_GATHER_SELF = 261

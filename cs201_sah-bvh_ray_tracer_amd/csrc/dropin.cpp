@@ -318,7 +318,7 @@ mirt_hit_record mirt_ray_bvh_intersect(mirt_ray ray, mirt_bvh_node* node)
         // new array -- one leaf, reached through the current tree, tells)
         const mirt_bvh_node* leaf = node;
         while (leaf && !leaf->sphere) leaf = leaf->left ? leaf->left : leaf->right;
-        const bool same_array = leaf && leaf->sphere >= s.spheres && leaf->sphere <= s.spheres + s.num_spheres;
+        const bool same_array = leaf && leaf->sphere >= s.spheres && leaf->sphere < s.spheres + s.num_spheres;
         if (!(s.bound && s.root == node && same_array && s.tree_fp == tree_fingerprint(node))) {
             // a tree seen without its sphere array: the leaves span it, or
             // the array the caller declared (mirt_dropin_scene) holds them

@@ -38,35 +38,13 @@ using namespace mirt;
 namespace {
 
 constexpr int kMaxShards = 64;  // shards of one frame (ranks, or the emulated world)
-// A/B (round 5): the frame's D2H as a copy that may not use compute units
-// (the runtime otherwise runs some of these copies as blit kernels on the
-// context's compute queue: __amd_rocclr_copyBuffer in the timed loop's trace)
-#ifndef MIRT_D2H_NOCU
-#define MIRT_D2H_NOCU 0
-#endif
-constexpr hipMemcpyKind kD2HKind = MIRT_D2H_NOCU ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToHost;
-// The frame's D2H issued as a 2D copy (H rows of W pixels, the path the
+// The frame's D2H is issued as a 2D copy (H rows of W pixels, the path the
 // host-direct copies take): the runtime runs it on a DMA engine, where a 1D
 // copy of the same bytes ran as a blit kernel on the context's compute queue
 // for most frames (14 of 20 in the timed loop's trace), taking CU time from
 // the frames in flight. Measured (profiles/r05_logs/r05av/): N = 1
 // host-inclusive 2,477-2,525 -> 2,543-2,572 Mrays/s, depth 1 6,775-6,930 ->
 // 8,431-8,455.
-#ifndef MIRT_D2H_2D
-#define MIRT_D2H_2D 1
-#endif
-// A/B switch (measurement only): 0 gives every lane its own accumulation
-// buffer, so fresh frames write it in the render kernel with no ordered fold
-// across the lanes -- NOT exact for an accumulating frame in flight after
-// fresh frames of other lanes
-// A/B (round 5): launches complete in issue order by a stream barrier on the
-// previous launch's completion event (with MIRT_LAZY_FOLD_BATCH: no fold kernel)
-#ifndef MIRT_MULTI_ORDER_DONE
-#define MIRT_MULTI_ORDER_DONE 0
-#endif
-#ifndef MIRT_MULTI_SHARE_ACCUM
-#define MIRT_MULTI_SHARE_ACCUM 1
-#endif
 
 // Where every shard's displays are (kernel argument of deinterleave_kernel):
 // shard s's `nframes` displays at p[s], frame j at + j * rows[s] * width --
@@ -159,6 +137,7 @@ struct Launch {
     mirt_frame_desc sd;             // shard geometry of the frame (num_shards = world), samples = spp * nframes
     int nframes = 1, flags = 0, world = 1, W = 0, H = 0, rb = 8;
     bool emu = false, gather = false, rank0_assembles = false, deliver = false;
+    bool self = false;              // MIRT_MULTI_OPT_GATHER_SELF: rank 0's own slabs into its slot too
     ShardSrc sr{};                  // rows of every shard (p[] filled by rank 0)
     size_t shard_stride = 0, frame_elems = 0;
     std::vector<mirt_rgba8*> dst;   // frame j's host destination (page-locked: the caller's or the staging)
@@ -239,8 +218,19 @@ struct mirt_multi {
     int timeout_ms = 60000;           // MIRT_MULTI_OPT_TIMEOUT_MS (0: unbounded)
     int emu_world = 0, emu_rank = 0;  // MIRT_MULTI_OPT_EMULATE_*: this one rank plays shard emu_rank of emu_world
     int direct_copy = 0;              // MIRT_MULTI_OPT_DIRECT_COPY: 0 one strided copy per frame, 1 one per row block
-    bool failed = false;              // a wait timed out or a device call failed: every call returns fail_msg
+    bool gather_self = false;         // MIRT_MULTI_OPT_GATHER_SELF: rank 0's own slabs travel through the gather too
+    int last_lane = -1;               // lane of the last launch enqueued
+    // a wait timed out or a device call failed: every call returns fail_msg;
+    // read by the rank threads before every issue and every RCCL call
+    std::atomic<bool> failed{false};
     std::string fail_msg;
+    // rank r's RCCL calls hold comm_mu[r]; fail_multi takes it before aborting
+    // the communicator, so no rank thread is between its `failed` check and
+    // its call when the communicator goes
+    std::vector<std::unique_ptr<std::timed_mutex>> comm_mu;
+    // mirt_multi_get_stats
+    std::atomic<uint64_t> st_launches{0}, st_comm_inits{0}, st_groups{0}, st_sends{0}, st_recvs{0}, st_bytes{0},
+        st_copies{0};
 };
 
 namespace {
@@ -255,16 +245,23 @@ int failed_status(const mirt_multi* m, const char* fn)
 
 // The object cannot go on: abort the communicators (an RCCL kernel stuck on a
 // peer polls the abort flag and exits), remember why, and fail from now on.
+// Called on the caller's thread only (the waits). The rank threads see
+// `failed` before their next issue and before every RCCL call, and stop
+// issuing; a rank thread still inside an RCCL call (holding comm_mu[r] past
+// the grace period: stuck on a peer) is released by the abort itself. The
+// communicator handles stay set (never used again; a failed object's destroy
+// does not destroy them).
 int fail_multi(mirt_multi* m, const std::string& why)
 {
-    m->failed = true;
-    for (Lane& L : m->lanes) L.deferred.clear();
     m->fail_msg = why;
-    for (ncclComm_t& c : m->comm)
-        if (c) {
-            (void)ncclCommAbort(c);
-            c = nullptr;
-        }
+    m->failed.store(true, std::memory_order_seq_cst);
+    for (Lane& L : m->lanes) L.deferred.clear();
+    for (size_t r = 0; r < m->comm.size(); r++) {
+        if (!m->comm[r]) continue;
+        std::unique_lock<std::timed_mutex> lk(*m->comm_mu[r], std::defer_lock);
+        (void)lk.try_lock_for(std::chrono::milliseconds(200));
+        (void)ncclCommAbort(m->comm[r]);
+    }
     set_error("%s", why.c_str());
     return MIRT_E_DEVICE;
 }
@@ -385,6 +382,7 @@ int communicators(mirt_multi* m)
         m->comm.clear();
         return nccl_err(e, "mirt_multi: ncclCommInitAll");
     }
+    m->st_comm_inits.fetch_add(1);
     return MIRT_OK;
 }
 
@@ -418,12 +416,13 @@ int prepare(mirt_multi* m, Lane& L, const mirt_camera* cam, const mirt_frame_des
     J.gather = !m->direct;                                     // frames to device 0
     J.rank0_assembles = J.gather && (!J.emu || m->emu_rank == 0);
     J.deliver = outs != nullptr;
-    if (J.gather && J.world > 1) {
+    J.self = J.gather && m->gather_self;
+    if (J.gather && (J.world > 1 || J.self)) {
         int rc = grow(m->dev[0], &L.gathered, &L.gathered_cap, 4 * J.shard_stride * J.world + 4);
         if (!rc && J.rank0_assembles) rc = grow(m->dev[0], &L.frame, &L.frame_cap, 4 * J.frame_elems * nframes + 4);
         if (rc) return rc;
     }
-    if (m->rccl && J.gather && (m->n > 1 || (J.emu && m->emu_rank > 0)))
+    if (m->rccl && J.gather && (m->n > 1 || J.emu || m->gather_self))
         if (int rc = communicators(m)) return rc;
     // where frame j lands: the caller's buffer if it is page-locked, else
     // the lane's staging area (copied out by wait_lane)
@@ -492,7 +491,7 @@ int issue_rank_body(mirt_multi* m, Lane& L, int r)
     if (m->ahead) {
         // the lane's own slabs: every frame of the launch (spp * nframes samples)
         const size_t need = 4 * elems * (size_t)std::max(1, sd.samples) + 4;
-        if (need > L.slab_cap[r])   // a pending fold of the old slab (MIRT_LAZY_FOLD) is taken first
+        if (need > L.slab_cap[r])   // a pending fold of the old slab (the lazy fold) is taken first
             if (int g = accum_settle(c)) return g;
         if (int g = grow(m->dev[r], &L.slab[r], &L.slab_cap[r], need)) return g;
         out = L.slab[r];
@@ -505,43 +504,71 @@ int issue_rank_body(mirt_multi* m, Lane& L, int r)
     L.src[r] = src;
     MHIP(hipSetDevice(m->dev[r]));
     if (J.gather) {
-        // slabs that travel: every rank's but rank 0's own (read in place);
-        // an emulated rank k > 0 sends its own to itself
-        const bool exchange = n > 1 || (J.emu && m->emu_rank > 0);
+        // slabs that travel: every rank's but rank 0's own (read in place,
+        // unless MIRT_MULTI_OPT_GATHER_SELF sends it to itself too); one
+        // emulated rank sends its own to itself, as rank k > 0 its shard, as
+        // rank 0 a stand-in for each other shard's receive
+        const bool self = J.self;
+        const bool exchange = n > 1 || J.emu || self;
         if (!m->rccl && r > 0) {
             // copy mode: rank 0's stream copies this rank's slabs once they are done
             MHIP(hipEventRecord(L.rendered[r], st));
             L.slabs_ready[r]->store(L.seq, std::memory_order_release);
         } else if (m->rccl && exchange && r > 0) {
             // RCCL: this rank's displays to rank 0, on the stream that rendered them
+            std::lock_guard<std::timed_mutex> lk(*m->comm_mu[r]);
+            if (m->failed.load()) return failed_status(m, "mirt_multi_render_frames_async");
             MNCCL(ncclSend(src, cnt, ncclUint32, 0, m->comm[r], st));
+            m->st_sends.fetch_add(1);
         }
         if (r == 0) {
             ShardSrc sr = J.sr;
-            // rank 0's own displays stay where it rendered them; the other
-            // shards' land in the gather buffer
-            sr.p[s] = src;
-            for (int q = 0; q < J.world; q++)
-                if (q != s) sr.p[q] = L.gathered + (size_t)q * J.shard_stride;
+            // the shards' displays in the gather buffer; rank 0's own where it
+            // rendered them (or, sent to itself, in its slot too)
+            for (int q = 0; q < J.world; q++) sr.p[q] = L.gathered + (size_t)q * J.shard_stride;
+            if (!self) sr.p[s] = src;
             if (m->rccl && exchange) {
-                // one group: rank 0 receives shard q at gathered + q * stride
-                // (emulated rank k > 0: its send, as a send to itself)
+                // one group on rank 0's stream: shard q arrives at gathered + q * stride
+                struct P2p {
+                    const uint32_t* from;   // null: a receive from rank `peer` only
+                    size_t count;
+                    int slot, peer;
+                };
+                std::vector<P2p> ops;
+                if (self || (J.emu && m->emu_rank > 0)) ops.push_back({src, cnt, s, 0});
+                if (J.emu && m->emu_rank == 0)   // the other shards' receives, its own slab standing in
+                    for (int q = 1; q < J.world; q++)
+                        ops.push_back({src, std::min(cnt, (size_t)J.sr.rows[q] * J.W * J.nframes), q, 0});
+                for (int q = 1; q < n; q++) ops.push_back({nullptr, (size_t)J.sr.rows[q] * J.W * J.nframes, q, q});
+                std::lock_guard<std::timed_mutex> lk(*m->comm_mu[0]);
+                if (m->failed.load()) return failed_status(m, "mirt_multi_render_frames_async");
                 MNCCL(ncclGroupStart());
                 ncclResult_t e = ncclSuccess;
-                if (n == 1) {
-                    e = ncclSend(src, cnt, ncclUint32, 0, m->comm[0], st);
-                    if (e == ncclSuccess) e = ncclRecv(L.gathered + (size_t)s * J.shard_stride, cnt, ncclUint32, 0,
-                                                       m->comm[0], st);
+                for (const P2p& o : ops) {
+                    if (o.count == 0) continue;
+                    if (o.from) {
+                        e = ncclSend(o.from, o.count, ncclUint32, 0, m->comm[0], st);
+                        if (e != ncclSuccess) break;
+                        m->st_sends.fetch_add(1);
+                    }
+                    e = ncclRecv(L.gathered + (size_t)o.slot * J.shard_stride, o.count, ncclUint32, o.peer,
+                                 m->comm[0], st);
+                    if (e != ncclSuccess) break;
+                    m->st_recvs.fetch_add(1);
+                    m->st_bytes.fetch_add(4 * o.count);
                 }
-                for (int q = 1; q < n && e == ncclSuccess; q++)
-                    e = ncclRecv(L.gathered + (size_t)q * J.shard_stride, (size_t)J.sr.rows[q] * J.W * J.nframes,
-                                 ncclUint32, q, m->comm[0], st);
                 if (e != ncclSuccess) {
                     (void)ncclGroupEnd();
                     return nccl_err(e, "mirt_multi_render_frames_async: ncclSend/ncclRecv");
                 }
                 MNCCL(ncclGroupEnd());
+                m->st_groups.fetch_add(1);
             } else if (!m->rccl) {
+                if (self) {   // rank 0's own slabs into its slot, as the other ranks' are copied
+                    MHIP(hipMemcpyAsync(L.gathered + (size_t)s * J.shard_stride, src, 4 * cnt, hipMemcpyDeviceToDevice,
+                                        st));
+                    m->st_copies.fetch_add(1);
+                }
                 // copy mode: wait for each rank's slabs, then copy them
                 // (peer-to-peer across devices, device-local otherwise)
                 using clk = std::chrono::steady_clock;
@@ -562,19 +589,23 @@ int issue_rank_body(mirt_multi* m, Lane& L, int r)
                         MHIP(hipMemcpyAsync(to, L.src[q], 4 * cq, hipMemcpyDeviceToDevice, st));
                     else
                         MHIP(hipMemcpyPeerAsync(to, m->dev[0], L.src[q], m->dev[q], 4 * cq, st));
+                    m->st_copies.fetch_add(1);
+                }
+                if (J.emu && m->emu_rank == 0) {
+                    // emulated rank 0 of a `world`-rank job in copy mode: the
+                    // other shards' slabs arrive as device copies of its own
+                    // (HBM writes of the receives; no wire time, no receive kernels)
+                    for (int q = 1; q < J.world; q++) {
+                        MHIP(hipMemcpyAsync(L.gathered + (size_t)q * J.shard_stride, src,
+                                            4 * std::min(cnt, (size_t)J.sr.rows[q] * J.W * J.nframes),
+                                            hipMemcpyDeviceToDevice, st));
+                        m->st_copies.fetch_add(1);
+                    }
                 }
             }
-            if (J.emu && m->emu_rank == 0) {
-                // emulated rank 0 of a `world`-rank job: the other shards' slabs
-                // arrive too (HBM writes of the receives; the xGMI wire time and
-                // the receive kernels are not modelled), copied from its own
-                for (int q = 1; q < J.world; q++)
-                    MHIP(hipMemcpyAsync(L.gathered + (size_t)q * J.shard_stride, src,
-                                        4 * std::min(cnt, (size_t)J.sr.rows[q] * J.W * J.nframes),
-                                        hipMemcpyDeviceToDevice, st));
-            }
             if (J.rank0_assembles) {
-                const uint32_t* frames = src;   // one shard: its displays are the frames
+                // one shard: its displays are the frames (in its slot when sent to itself)
+                const uint32_t* frames = self ? L.gathered + (size_t)s * J.shard_stride : src;
                 if (J.world > 1) {
                     const dim3 grid((J.W + 255) / 256, J.H, J.nframes);
                     deinterleave_kernel<<<grid, 256, 0, st>>>(sr, L.frame, J.W, J.H, J.rb, J.world);
@@ -583,14 +614,9 @@ int issue_rank_body(mirt_multi* m, Lane& L, int r)
                 }
                 if (J.deliver) {
                     const hipStream_t cs = copy_stream(m, L, r);
-                    for (int j = 0; j < J.nframes; j++) {
-                        if (MIRT_D2H_2D)   // as a 2D copy (H rows of W pixels): the runtime's rect copy path
-                            MHIP(hipMemcpy2DAsync(J.dst[j], 4 * (size_t)J.W, frames + (size_t)j * J.frame_elems,
-                                                  4 * (size_t)J.W, 4 * (size_t)J.W, J.H, hipMemcpyDeviceToHost, cs));
-                        else
-                            MHIP(hipMemcpyAsync(J.dst[j], frames + (size_t)j * J.frame_elems, 4 * J.frame_elems,
-                                                kD2HKind, cs));
-                    }
+                    for (int j = 0; j < J.nframes; j++)   // as a 2D copy (H rows of W pixels): a DMA engine
+                        MHIP(hipMemcpy2DAsync(J.dst[j], 4 * (size_t)J.W, frames + (size_t)j * J.frame_elems,
+                                              4 * (size_t)J.W, 4 * (size_t)J.W, J.H, hipMemcpyDeviceToHost, cs));
                 }
             }
         }
@@ -639,13 +665,6 @@ int issue_rank_body(mirt_multi* m, Lane& L, int r)
     }
     // the launch's last operation on this rank: its copy stream when the
     // lane has one (it waited for everything the context's stream did)
-    if (MIRT_MULTI_ORDER_DONE) {
-        // launches complete in issue order (the order the caller rotates through
-        // the lanes), by a barrier on the previous launch's completion: the
-        // ordering the per-launch fold chain gave, without its kernel
-        const int li = (int)(&L - m->lanes.data()), nl = (int)m->lanes.size();
-        MHIP(hipStreamWaitEvent(copy_stream(m, L, r), m->lanes[(li + nl - 1) % nl].done[r], 0));
-    }
     MHIP(hipEventRecord(L.done[r], copy_stream(m, L, r)));
     return MIRT_OK;
 }
@@ -655,7 +674,8 @@ int issue_rank_body(mirt_multi* m, Lane& L, int r)
 // error, the completion event over whatever did reach the stream.
 void issue_rank(mirt_multi* m, Lane& L, int r)
 {
-    const int rc = issue_rank_body(m, L, r);
+    // a failed object issues nothing more (its lanes are never waited for again)
+    const int rc = m->failed.load() ? failed_status(m, "mirt_multi_render_frames_async") : issue_rank_body(m, L, r);
     if (rc) {
         (void)hipSetDevice(m->dev[r]);
         (void)hipEventRecord(L.done[r], stream_of(L.ctx[r]));
@@ -670,9 +690,12 @@ void issue_rank(mirt_multi* m, Lane& L, int r)
     L.issued->fetch_add(1, std::memory_order_acq_rel);
 }
 
-void rank_thread_main(mirt_multi* m, int r)
+// `w` is passed in, not read from m->workers: the caller's thread is still
+// appending the later ranks' workers (reallocating that vector) while the
+// first threads start.
+void rank_thread_main(mirt_multi* m, int r, RankThread* wp)
 {
-    RankThread& w = *m->workers[r];
+    RankThread& w = *wp;
     (void)hipSetDevice(m->dev[r]);
     for (;;) {
         int li;
@@ -778,6 +801,7 @@ try {
     m->ahead = (flags & MIRT_MULTI_QUEUE_AHEAD) != 0;
     m->nctx = lanes;
     m->rccl = distinct && !(flags & MIRT_MULTI_COPY);
+    for (int r = 0; r < n; r++) m->comm_mu.emplace_back(new std::timed_mutex);
     auto fail = [&](int rc) {
         mirt_multi_destroy(m);
         return rc;
@@ -847,18 +871,21 @@ try {
             }
             // the lanes of a rank keep ONE accumulation buffer: frames in
             // flight of the accumulating loop (main.c:379-408) fold in order
-            if (MIRT_MULTI_SHARE_ACCUM && l > 0) {
+            if (l > 0) {
                 rc = mirt_ctx_share_accum(L.ctx[r], m->lanes[0].ctx[r]);
                 if (rc) return fail(rc);
             }
         }
     }
     // one issuing thread per rank (n > 1)
-    if (n > 1)
+    if (n > 1) {
+        m->workers.reserve(n);
         for (int r = 0; r < n; r++) {
             m->workers.emplace_back(new RankThread());
-            m->workers.back()->th = std::thread(rank_thread_main, m, r);
+            RankThread* w = m->workers.back().get();
+            w->th = std::thread(rank_thread_main, m, r, w);
         }
+    }
     *out = m;
     return MIRT_OK;
 } catch (const std::bad_alloc&) {
@@ -892,6 +919,13 @@ void mirt_multi_destroy(mirt_multi* m)
     }
     for (auto& w : m->workers) w->th.join();
     m->workers.clear();
+    // a fresh frame's display left pending on a rank's shared accumulation
+    // buffer (the lazy fold) may lie in a lane's own slab (QUEUE_AHEAD):
+    // fold it, and let every read of the slabs end, before any slab is freed
+    for (Lane& L : m->lanes)
+        if (L.owns_ctx)
+            for (mirt_ctx* c : L.ctx)
+                if (c) (void)accum_settle(c);
     for (Lane& L : m->lanes) {
         for (int r = 0; r < (int)L.ctx.size(); r++) {
             (void)hipSetDevice(m->dev[r]);
@@ -956,6 +990,10 @@ int mirt_multi_set_option(mirt_multi* m, int option, int value)
         if (value < 0 || value >= std::max(1, m->emu_world)) break;
         m->emu_rank = value;
         return MIRT_OK;
+    case MIRT_MULTI_OPT_GATHER_SELF:
+        if (value < 0 || value > 1) break;
+        m->gather_self = value == 1;
+        return MIRT_OK;
     default:
         for (Lane& L : m->lanes)
             if (L.owns_ctx)
@@ -975,6 +1013,7 @@ int mirt_multi_get_option(mirt_multi* m, int option)
     if (option == MIRT_MULTI_OPT_EMULATE_RANK) return m->emu_rank;
     if (option == MIRT_MULTI_OPT_DIRECT_COPY) return m->direct_copy;
     if (option == MIRT_MULTI_OPT_COPY_STREAM) return m->ahead_copy_stream;
+    if (option == MIRT_MULTI_OPT_GATHER_SELF) return m->gather_self ? 1 : 0;
     return mirt_get_option(m->lanes[0].ctx[0], option);
 }
 
@@ -1014,10 +1053,13 @@ try {
     if (int rc = wait_lane(m, li)) return rc;
     if (m->ahead && m->ahead_copy_stream == 2)
         if (int rc = wait_sibling_kernels(m, li)) return rc;
+    // an error here (before any rank issued) leaves the lane and the rotation
+    // as they were; the ranks' own issue errors come back from the lane's wait
+    if (int rc = enqueue(m, li, cam, fd, nframes, flags, outs)) return rc;
     m->next = (m->next + 1) % (int)m->lanes.size();
-    // an error here (before any rank issued) leaves the lane as it was; the
-    // ranks' own issue errors come back from the lane's wait
-    return enqueue(m, li, cam, fd, nframes, flags, outs);
+    m->last_lane = li;
+    m->st_launches.fetch_add(1);
+    return MIRT_OK;
 } catch (const std::bad_alloc&) {
     set_error("mirt_multi_render_frames_async: out of host memory");
     return MIRT_E_NOMEM;
@@ -1047,6 +1089,53 @@ int mirt_multi_wait(mirt_multi* m)
     for (int l = 0; l < (int)m->lanes.size(); l++)
         if (int rc = wait_lane(m, l)) return rc;
     return MIRT_OK;
+}
+
+int mirt_multi_get_stats(const mirt_multi* m, mirt_multi_stats* out)
+{
+    if (!m || !out) {
+        set_error("mirt_multi_get_stats: invalid arguments");
+        return MIRT_E_INVALID;
+    }
+    out->launches = m->st_launches.load();
+    out->comm_inits = m->st_comm_inits.load();
+    out->rccl_groups = m->st_groups.load();
+    out->rccl_sends = m->st_sends.load();
+    out->rccl_recvs = m->st_recvs.load();
+    out->rccl_bytes = m->st_bytes.load();
+    out->device_copies = m->st_copies.load();
+    return MIRT_OK;
+}
+
+int mirt_multi_read_gathered(mirt_multi* m, int lane, int shard, int frame, mirt_rgba8* out, size_t bytes)
+try {
+    const char* fn = "mirt_multi_read_gathered";
+    if (!multi_ok(m, fn)) return MIRT_E_INVALID;
+    if (m->failed) return failed_status(m, fn);
+    if (lane < 0) lane = m->last_lane;
+    if (lane < 0 || lane >= (int)m->lanes.size() || !out) {
+        set_error("%s: no such lane (or no launch yet), or null output", fn);
+        return MIRT_E_INVALID;
+    }
+    if (int rc = wait_lane(m, lane)) return rc;
+    Lane& L = m->lanes[lane];
+    const Launch& J = L.job;
+    if (!J.gather || (J.world <= 1 && !J.self) || !L.gathered || shard < 0 || shard >= J.world || frame < 0 ||
+        frame >= J.nframes) {
+        set_error("%s: the lane's last launch gathered no such shard / frame (gather delivery, world > 1)", fn);
+        return MIRT_E_INVALID;
+    }
+    const size_t n = (size_t)J.sr.rows[shard] * J.W;
+    if (bytes < 4 * n) {
+        set_error("%s: output holds %zu bytes, the shard's slab %zu", fn, bytes, 4 * n);
+        return MIRT_E_INVALID;
+    }
+    MHIP(hipSetDevice(m->dev[0]));
+    MHIP(hipMemcpy(out, L.gathered + (size_t)shard * J.shard_stride + (size_t)frame * n, 4 * n, hipMemcpyDeviceToHost));
+    return MIRT_OK;
+} catch (const std::bad_alloc&) {
+    set_error("mirt_multi_read_gathered: out of host memory");
+    return MIRT_E_NOMEM;
 }
 
 }  // extern "C"

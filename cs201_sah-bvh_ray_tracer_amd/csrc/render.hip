@@ -327,14 +327,6 @@ constexpr int kBounceDiag = 12;  // mirt_bounce_stats words per wave  // HNodes 
 #ifndef MIRT_QSEG
 #define MIRT_QSEG 8
 #endif
-// A/B (round 5): each segment taken from its END. The primary pass appends a
-// workgroup's first bounces when it finishes, so the records of the costly
-// (dense) tiles -- whose chains bounce longest -- sit late in each segment;
-// taking them first starts the longest chains first (longest-processing-time
-// order), so fewer of them are still running when the queue runs dry.
-#ifndef MIRT_QUEUE_REVERSE
-#define MIRT_QUEUE_REVERSE 0
-#endif
 constexpr uint32_t kQSeg = MIRT_QSEG;
 constexpr uint32_t kQLine = 32;                        // dwords per 128-B line
 constexpr size_t kQCtlBytes = 4 * kQLine * (1 + kQSeg);
@@ -348,33 +340,6 @@ struct BounceRec {
     uint32_t pad;
 };
 
-// A/B (round 5): the queue's records are streamed once (written by the camera
-// pass, read once by the bounce pass): moved with non-temporal loads and
-// stores, so 60 MB per 1080p frame do not push the tree's nodes out of L2.
-#ifndef MIRT_QUEUE_NT
-#define MIRT_QUEUE_NT 0
-#endif
-__device__ __forceinline__ void rec_store(BounceRec* dst, const BounceRec& r)
-{
-    if (MIRT_QUEUE_NT) {
-        const uint32_t* s = reinterpret_cast<const uint32_t*>(&r);
-        uint32_t* d = reinterpret_cast<uint32_t*>(dst);
-        for (int i = 0; i < 10; i++) __builtin_nontemporal_store(s[i], d + i);
-    } else {
-        *dst = r;
-    }
-}
-__device__ __forceinline__ BounceRec rec_load(const BounceRec* src)
-{
-    if (MIRT_QUEUE_NT) {
-        BounceRec r;
-        const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
-        uint32_t* d = reinterpret_cast<uint32_t*>(&r);
-        for (int i = 0; i < 10; i++) d[i] = __builtin_nontemporal_load(s + i);
-        return r;
-    }
-    return *src;
-}
 
 // ORD: the tree admits the ordered packet walk (DevScene::ordered), which
 // also takes zero-component rays -- that build has no deferred waves and no
@@ -388,12 +353,9 @@ template <bool FAST, bool ORD>
 #ifndef MIRT_PRIMARY_WAVES
 #define MIRT_PRIMARY_WAVES 8
 #endif
-// A/B (round 3): group each primary workgroup's first bounces by direction
-// octant in the queue (scripts/tree_quality.cpp's lockstep model: distinct
-// nodes per lane-step -9%, busy lanes per step +13%)
-#ifndef MIRT_PRIMARY_GROUP
-#define MIRT_PRIMARY_GROUP 1
-#endif
+// (Round 3: the ordered kernel groups each workgroup's first bounces by
+// direction octant in the queue -- scripts/tree_quality.cpp's lockstep model:
+// distinct nodes per lane-step -9%, busy lanes per step +13%; measured +1.8%.)
 #define MIRT_PRIMARY_ATTR __attribute__((amdgpu_waves_per_eu(ORD ? MIRT_PRIMARY_WAVES : 1)))
 __global__ __launch_bounds__(256) MIRT_PRIMARY_ATTR void primary_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
                                                       float* __restrict__ acc, Deferred dfr,
@@ -404,7 +366,6 @@ __global__ __launch_bounds__(256) MIRT_PRIMARY_ATTR void primary_kernel(DevScene
     Counters cnt{0, 0, 0, 0, 0};
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-#if MIRT_PRIMARY_GROUP
     // the workgroup's first bounces, grouped by direction octant before they
     // enter the queue (the last of the four waves to finish writes them)
     __shared__ BounceRec grec[ORD ? 256 : 1];
@@ -413,7 +374,6 @@ __global__ __launch_bounds__(256) MIRT_PRIMARY_ATTR void primary_kernel(DevScene
         if (threadIdx.x == 0) gdone = 0;
         __syncthreads();
     }
-#endif
     if (!ORD && (int)blockIdx.x < dfr.blocks) {  // zero-component camera rays: whole path in this wave
         const uint32_t n = __builtin_amdgcn_readfirstlane(*dfr.count);
         const uint32_t stride = (uint32_t)(dfr.blocks * 4);
@@ -452,10 +412,7 @@ __global__ __launch_bounds__(256) MIRT_PRIMARY_ATTR void primary_kernel(DevScene
     float t;
     int s;
     if constexpr (ORD) {
-        if (MIRT_PACKET_HALVES)
-            closest_packet_halves<FAST, false>(sc, ray, alive, t, s, cnt);
-        else
-            closest_packet_ordered<FAST, false>(sc, ray, alive, t, s, cnt);
+        closest_packet_ordered<FAST, false>(sc, ray, alive, t, s, cnt);
     } else
         closest_hit<true, FAST, false>(sc, ray, alive, t, s, cnt);
     const size_t i = (size_t)r * f.width + x;
@@ -481,7 +438,6 @@ __global__ __launch_bounds__(256) MIRT_PRIMARY_ATTR void primary_kernel(DevScene
         }
     }
     const uint64_t pm = __ballot(push);
-#if MIRT_PRIMARY_GROUP
     if constexpr (ORD) {
         if (push) grec[wave * 64 + lanes_below(pm)] = rec;
         if (lane == 0) gcount[wave] = (uint32_t)__popcll(pm);
@@ -523,17 +479,16 @@ __global__ __launch_bounds__(256) MIRT_PRIMARY_ATTR void primary_kernel(DevScene
                 if (has[w] && oct[w] == o) pos = run[o] + lanes_below(m);
                 run[o] += (uint32_t)__popcll(m);
             }
-            if (has[w]) rec_store(queue + pos, grec[w * 64 + lane]);
+            if (has[w]) queue[pos] = grec[w * 64 + lane];
         }
         return;
     }
-#endif
     if (pm) {  // one atomic per wave; records stay in tile order
         const int leader = __builtin_ctzll(pm);
         uint32_t base = 0;
         if (lane == leader) base = atomicAdd(&qctl[0], (uint32_t)__popcll(pm));
         base = __builtin_amdgcn_readlane(base, leader);
-        if (push) rec_store(queue + base + lanes_below(pm), rec);
+        if (push) queue[base + lanes_below(pm)] = rec;
     }
 }
 
@@ -624,11 +579,6 @@ __device__ __forceinline__ bool shade_level(const DevScene& sc, const FrameConst
     return false;
 }
 
-// MIRT_SOLO_DRAIN: the last ray of a bounce wave walked by all 16 of the
-// wave's quads at once (trace.h solo_step)
-#ifndef MIRT_SOLO_DRAIN
-#define MIRT_SOLO_DRAIN 1
-#endif
 
 // The rest of the chain of the wave's one remaining ray (held by the quad of
 // lane l0), every lane of the wave taking part: its state broadcast from l0,
@@ -679,110 +629,6 @@ __device__ __forceinline__ void solo_chain(const DevScene& sc, const FrameConst&
     }
 }
 
-// Continuation queue (lone frames: the blocking call; MIRT_OPT_CONT_QUEUE).
-// Once a frame's first-bounce queue is dry, its remaining chains sit in the
-// waves that drew them, and the waves that finished early would leave the
-// chip while the last chains are walked one lane (or one quad) per ray. With
-// the queue on, waves that run out of chains stay and WAIT, and a wave that
-// still holds several chains hands a chain that goes on to its next level to
-// them (never more than are waiting) as a 64-B record; a waiting wave takes
-// one record and walks that chain with all 16 of its quads (solo_chain), so
-// the tail's chains get the whole chip instead of a lane each. Termination:
-// every wave counts itself a possible pusher until its own chains are done;
-// a waiting wave leaves once no pusher is left and the queue is empty (a
-// pusher's records are published before it stops being one, so none is
-// orphaned). Every wait is bounded (kContSpinTicks of the 100 MHz clock): a
-// wait that runs out sets the error word and gives up (a wrong frame, never
-// a hung grid).
-struct ContRec {                    // one chain at the start of a bounce level
-    float ox, oy, oz, dx, dy, dz;
-    uint32_t pixel, k, base0, level;
-    uint32_t col[6];                // colour stack rows 0 .. level - 2 (levels 1 .. level - 1)
-};
-static_assert(sizeof(ContRec) == 64, "continuation record is 64 B");
-struct ContQ {
-    uint32_t* ctl;    // kCq* words, each in its own 128-B line
-    ContRec* rec;     // cap records (a ring)
-    uint32_t* flag;   // per record slot: 0 free, else the epoch of the record published there
-    uint32_t cap;     // records: the launch's lanes (chains alive after the queue is dry <= lanes)
-    uint32_t consumers;  // workgroups whose first wave waits for records (the others leave when done)
-};
-constexpr uint32_t kCqHead = 0, kCqTail = 32, kCqPushers = 64, kCqWaiters = 96, kCqError = 128;
-constexpr size_t kCqCtlBytes = 4 * 160;
-constexpr uint64_t kContSpinTicks = 2000000;   // 20 ms of the 100 MHz real-time clock
-// pushes from waves still walking one chain per lane (1), or only from waves
-// in the quad drain (0)
-#ifndef MIRT_CQ_LANE_PUSH
-#define MIRT_CQ_LANE_PUSH 1
-#endif
-// A/B of the queue's costs (0 = the queue): 1 no pushes (no room reads),
-// 2 room reads but no pushes, 3 no waiting waves and no pushes
-#ifndef MIRT_CQ_VARIANT
-#define MIRT_CQ_VARIANT 0
-#endif
-
-// Cross-XCD traffic without cache maintenance: the eight XCDs' L2s are not
-// coherent with each other, and an acquire / release at agent scope costs an
-// L2 invalidate / write-back (buffer_inv / buffer_wbl2 sc1) that throws away
-// every wave's cached tree nodes -- so every word of the queue is read and
-// written with RELAXED agent-scope atomics (sc0 sc1: they bypass the caches),
-// and ordering comes from waiting for this wave's own memory operations to
-// complete (a workgroup-scope fence: s_waitcnt, nothing flushed).
-__device__ __forceinline__ uint32_t cq_load(const uint32_t* p)
-{
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void cq_store(uint32_t* p, uint32_t v)
-{
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void cq_complete()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // this wave's loads / stores done
-}
-
-// Pushes the waiting waves would take at once: waiters - records queued.
-__device__ __forceinline__ uint32_t cq_room(const ContQ& q)
-{
-    if (MIRT_CQ_VARIANT == 1 || MIRT_CQ_VARIANT == 3) return 0u;
-    if (MIRT_CQ_VARIANT == 2) return cq_load(q.ctl + kCqWaiters) + cq_load(q.ctl + kCqHead) + cq_load(q.ctl + kCqTail) == 0xffffffffu ? 1u : 0u;
-    const uint32_t w = cq_load(q.ctl + kCqWaiters), h = cq_load(q.ctl + kCqHead), t = cq_load(q.ctl + kCqTail);
-    const uint32_t queued = h - t;
-    return w > queued ? w - queued : 0u;
-}
-
-// One lane publishes its chain (ray of level `level`, colours at cs[(l) * cstride]).
-__device__ __forceinline__ void cq_push(const ContQ& q, const Ray& ray, uint32_t pixel, uint32_t k, uint32_t base0,
-                                        int level, const uint32_t* cs, int cstride)
-{
-    const uint32_t idx = atomicAdd(q.ctl + kCqHead, 1u);
-    const uint32_t slot = idx % q.cap, epoch = idx / q.cap + 1u;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (cq_load(q.flag + slot) != 0u) {     // the ring slot's previous record is still being read
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kContSpinTicks) {
-            atomicOr(q.ctl + kCqError, 1u);
-            return;
-        }
-        __builtin_amdgcn_s_sleep(2);
-    }
-    uint32_t* d = (uint32_t*)(q.rec + slot);
-    cq_store(d + 0, __float_as_uint(ray.ox));
-    cq_store(d + 1, __float_as_uint(ray.oy));
-    cq_store(d + 2, __float_as_uint(ray.oz));
-    cq_store(d + 3, __float_as_uint(ray.dx));
-    cq_store(d + 4, __float_as_uint(ray.dy));
-    cq_store(d + 5, __float_as_uint(ray.dz));
-    cq_store(d + 6, pixel);
-    cq_store(d + 7, k);
-    cq_store(d + 8, base0);
-    cq_store(d + 9, (uint32_t)level);
-#pragma unroll
-    for (int l = 0; l < 6; l++)
-        if (l < level - 1) cq_store(d + 10 + l, cs[l * cstride]);
-    cq_complete();                              // the record is in memory before its flag
-    cq_store(q.flag + slot, epoch);
-}
-
 // Persistent bounce pass: each lane owns one pixel's chain of bounces,
 // refilled from the primary pass's queue. WALK 2 (default) ends with a QUAD
 // DRAIN: once the queue is dry and at most 16 of
@@ -798,14 +644,12 @@ __device__ __forceinline__ void cq_push(const ContQ& q, const Ray& ray, uint32_t
 #define MIRT_BOUNCE_WAVES 5
 #endif
 #define MIRT_BOUNCE_ATTR __attribute__((amdgpu_waves_per_eu(MIRT_BOUNCE_WAVES)))
-template <bool FAST, int WALK, bool DIAG = false, bool CQ = false>
+template <bool FAST, int WALK, bool DIAG = false>
 __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
                                                      float* __restrict__ acc, const BounceRec* __restrict__ queue,
                                                      uint32_t* __restrict__ qctl, int threshold, int quad_drain,
-                                                     uint64_t* __restrict__ diag = nullptr, ContQ cq = ContQ{})
+                                                     uint64_t* __restrict__ diag = nullptr)
 {
-    static_assert(!CQ || ((WALK == 2 || WALK == 4) && !DIAG), "the continuation queue rides on the quad drain");
-    if (CQ && (threadIdx.x & 63) == 0) atomicAdd(cq.ctl + kCqPushers, 1u);   // this wave may push
     uint64_t dg_it = 0, dg_lanes = 0, dg_it_x = 0, dg_lanes_x = 0, dg_tx = 0, dg_qit = 0, dg_tq = 0;
     const uint64_t dg_t0 = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
     uint32_t dg_steps = 0, dg_chain = 0, dg_walk_max = 0, dg_chain_max = 0;
@@ -849,7 +693,6 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
     uint32_t pixel = 0, k = 0, base0 = 0;
     int level = 0, best_s = -1;
     float best_t = INFINITY;
-    bool cont = false;   // CQ: this lane's chain just started its next level after the queue ran dry
     for (;;) {
         // refill lanes that own no chain (one atomic per wave, tile order
         // kept), from the next segment while the current one is dry
@@ -869,7 +712,7 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                 const uint32_t lane0 = threadIdx.x & 63;
                 const uint32_t idx = b + (uint32_t)__popcll(need & ((1ull << lane0) - 1));
                 if (idx < sz) {
-                    const BounceRec rec = rec_load(queue + lo + (MIRT_QUEUE_REVERSE ? sz - 1 - idx : idx));
+                    const BounceRec rec = queue[lo + idx];
                     ray = Ray{rec.ox, rec.oy, rec.oz, rec.dx, rec.dy, rec.dz};
                     sr = slab_ray(ray);
                     sp = sph_ray(ray);
@@ -931,30 +774,12 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                 best_t = INFINITY;
                 best_s = -1;
                 pr = prune_off();
-                cont = CQ && exhausted;
             } else {
                 has = false;
                 if (DIAG) {
                     dg_chain_max = max(dg_chain_max, dg_chain);
                     dg_chain = 0;
                 }
-            }
-        }
-        if constexpr (CQ && MIRT_CQ_LANE_PUSH) {
-            // chains starting a new level after the queue ran dry: as many as
-            // waves are waiting go to them (the wave keeps at least one)
-            const uint64_t cm = __ballot(cont);
-            if (cm) {
-                const int lead = __builtin_ctzll(cm);
-                uint32_t room = 0;
-                if ((int)(threadIdx.x & 63) == lead) room = cq_room(cq);
-                room = min((uint32_t)__builtin_amdgcn_readlane((int)room, lead),
-                           (uint32_t)__popcll(__ballot(has)) - 1u);
-                if (cont && lanes_below(cm) < room) {
-                    cq_push(cq, ray, pixel, k, base0, level, cs, cstride);
-                    has = false;
-                }
-                cont = false;
             }
         }
     }
@@ -992,7 +817,7 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
             if (DIAG) dg_tq = __builtin_amdgcn_s_memrealtime();
             while (__ballot(has)) {
                 if (DIAG) dg_qit++;
-                if (MIRT_SOLO_DRAIN && !DIAG) {
+                if (!DIAG) {
                     // one ray left in the wave: every quad of the wave walks it
                     const uint64_t rays = __ballot(has && (lane & 3) == 0);
                     if (__popcll(rays) == 1) {
@@ -1005,7 +830,6 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                 if (has && qw.cur != kPNone)
                     quad_step<FAST, kWideStride, kWideStack>(sc, sr, sp, pr, qw, qstk, best_t, best_s,
                                                              (lds_uint4*)hcache, hc_n);
-                bool qcont = false;
                 if (has && qw.cur == kPNone) {
                     if (shade_level(sc, f, ray, best_t, best_s, level, k, chain_key(f, pixel), qcs, kWideStride, base0, pixel, out,
                                     acc, (lane & 3) == 0)) {
@@ -1015,106 +839,12 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                         best_t = INFINITY;
                         best_s = -1;
                         pr = prune_off();
-                        qcont = CQ;
                     } else {
                         has = false;
                     }
                 }
-                if constexpr (CQ) {
-                    // quads whose ray starts its next level hand it to waiting
-                    // waves (quad-uniform decision; the wave keeps one ray)
-                    const uint64_t cm = __ballot(qcont && (lane & 3) == 0);
-                    if (cm) {
-                        const int lead = __builtin_ctzll(cm);
-                        uint32_t room = 0;
-                        if ((int)lane == lead) room = cq_room(cq);
-                        room = min((uint32_t)__builtin_amdgcn_readlane((int)room, lead),
-                                   (uint32_t)__popcll(__ballot(has && (lane & 3) == 0)) - 1u);
-                        const uint32_t qb = lane & ~3u;
-                        const uint32_t qrank = (uint32_t)__popcll(qb ? cm & ((1ull << qb) - 1) : 0ull);
-                        if (qcont && qrank < room) {
-                            if ((lane & 3) == 0) cq_push(cq, ray, pixel, k, base0, level, qcs, kWideStride);
-                            has = false;
-                            qw.cur = kPNone;
-                        }
-                    }
-                }
             }
         }
-    }
-    if constexpr (CQ) {
-        // this wave's own chains are done: no more pushes from it; wait for
-        // records while any wave may still push, walking each with the whole wave
-        const uint32_t lane = threadIdx.x & 63;
-        uint32_t* wst = wstack + (threadIdx.x & ~63u);
-        uint32_t* wcs = cstack + (threadIdx.x & ~63u);
-        // one waiting wave per consumer workgroup (about one per CU): enough
-        // to take the tail's chains, few enough that their polling does not
-        // crowd the L2 lines every wave's walk goes through
-        const bool consumer = MIRT_CQ_VARIANT != 3 && blockIdx.x < cq.consumers && threadIdx.x < 64;
-        if (lane == 0) {
-            if (consumer) atomicAdd(cq.ctl + kCqWaiters, 1u);
-            cq_complete();                          // this wave's pushes are published first
-            atomicAdd(cq.ctl + kCqPushers, ~0u);
-        }
-        uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        for (; consumer;) {
-            constexpr uint32_t kNone = ~0u, kExit = ~1u;
-            uint32_t got = kNone;
-            if (lane == 0) {
-                const uint32_t t = cq_load(cq.ctl + kCqTail), h = cq_load(cq.ctl + kCqHead);
-                if (t < h) {
-                    if (atomicCAS(cq.ctl + kCqTail, t, t + 1u) == t) got = t;
-                } else if (cq_load(cq.ctl + kCqPushers) == 0u &&
-                           cq_load(cq.ctl + kCqTail) >= cq_load(cq.ctl + kCqHead)) {
-                    got = kExit;
-                } else if (__builtin_amdgcn_s_memrealtime() - t0 > 25 * kContSpinTicks) {
-                    atomicOr(cq.ctl + kCqError, 2u);   // no pusher ever finished: give up
-                    got = kExit;
-                }
-            }
-            got = (uint32_t)__builtin_amdgcn_readfirstlane((int)got);
-            if (got == kExit) break;
-            if (got == kNone) {
-                __builtin_amdgcn_s_sleep(32);
-                continue;
-            }
-            const uint32_t slot = got % cq.cap, epoch = got / cq.cap + 1u;
-            uint32_t ok = 1;
-            if (lane == 0) {
-                const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
-                atomicAdd(cq.ctl + kCqWaiters, ~0u);
-                while (cq_load(cq.flag + slot) != epoch) {
-                    if (__builtin_amdgcn_s_memrealtime() - w0 > kContSpinTicks) {
-                        atomicOr(cq.ctl + kCqError, 4u);
-                        ok = 0;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-            }
-            ok = (uint32_t)__builtin_amdgcn_readfirstlane((int)ok);
-            if (!ok) break;
-            const uint32_t word = lane < 16 ? cq_load((const uint32_t*)(cq.rec + slot) + lane) : 0u;
-            cq_complete();                          // the record is read before its slot is freed
-            __builtin_amdgcn_wave_barrier();
-            if (lane == 0) cq_store(cq.flag + slot, 0u);
-            auto wd = [&](int i) { return (uint32_t)__builtin_amdgcn_readlane((int)word, i); };
-            const Ray cr{__uint_as_float(wd(0)), __uint_as_float(wd(1)), __uint_as_float(wd(2)),
-                         __uint_as_float(wd(3)), __uint_as_float(wd(4)), __uint_as_float(wd(5))};
-            const int clevel = (int)wd(9);
-            // the colour stack rows into column 0 (this wave's columns are free)
-            const uint32_t colw = (uint32_t)__shfl((int)word, min(10 + (int)lane, 63));
-            if (lane < 6 && (int)lane < clevel - 1) wcs[lane * kWideStride] = colw;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            solo_chain<FAST>(sc, f, 0, cr, INFINITY, -1, prune_off(), QuadWalk{sc.wide_root, 0u, 0u}, clevel, wd(7),
-                             wd(6), wd(8), 0u, wst, wcs, out, acc, (lds_uint4*)hcache, hc_n);
-            if (lane == 0) atomicAdd(cq.ctl + kCqWaiters, 1u);
-            t0 = __builtin_amdgcn_s_memrealtime();
-        }
-        if (consumer && lane == 0) atomicAdd(cq.ctl + kCqWaiters, ~0u);
     }
     if (DIAG) {
         for (int o = 32; o; o >>= 1) {
@@ -1206,7 +936,7 @@ __global__ __launch_bounds__(256) void brute_chunk_kernel(DevScene sc, const mir
     const int s1 = min(s0 + chunk, sc.num_spheres);
     float best_t = INFINITY;
     int best_s = -1;
-    if (FAST && MIRT_BRUTE_PACKED && s0 < s1 && __ballot(active)) {
+    if (FAST && s0 < s1 && __ballot(active)) {
         brute_range_packed(sc, sp, active, s0, s1, best_t, best_s);
     } else if (s0 < s1 && __ballot(active)) {
         float4 g = load_geo_uniform(sc.geo, s0);
@@ -1523,7 +1253,7 @@ struct AccumShare {
     size_t pixels = 0;       // pixels of the running accumulation (0: none yet)
     hipEvent_t folded = nullptr;
     bool has_fold = false;   // `folded` was recorded at least once
-    // Lazy fold (round 5, MIRT_LAZY_FOLD): the display slab of the last FRESH
+    // Lazy fold (round 5): the display slab of the last FRESH
     // frame issued on the share and not yet folded into d_acc. A fresh
     // frame's accumulation state is its colours / 255 (main.c:368-370), which
     // its slab holds exactly, so it is folded only when a frame or a read
@@ -1534,33 +1264,12 @@ struct AccumShare {
     mirt_ctx* pend_ctx = nullptr;   // the ctx that rendered it (its slab must outlive the read)
     hipEvent_t pend_ev = nullptr;   // recorded after that frame's render
 };
-#ifndef MIRT_LAZY_FOLD
-#define MIRT_LAZY_FOLD 1
-#endif
-// The same for a launch of several fresh frames (mirt_multi at N >= 4): off --
-// there the ordered fold per launch keeps the lanes finishing in the order the
-// caller rotates through them; left pending, the slowest shard of an 8-way
-// split ran 2-4% slower (four interleaved rounds, profiles/r05_logs/r05bc/),
-// where a one-frame launch gains (N = 1 +1.8%, depth 1 +4.7%, r05ax/)
-#ifndef MIRT_LAZY_FOLD_BATCH
-#define MIRT_LAZY_FOLD_BATCH 0
-#endif
+// (A launch of several fresh frames, mirt_multi at N >= 4, keeps its ordered
+// fold: the lanes then finish in the order the caller rotates through them;
+// its last display left pending ran the slowest shard of an 8-way split 2-4%
+// slower, profiles/r05_logs/r05bc/.)
 
-#ifndef MIRT_PRIMARY_DEPTH1
-#define MIRT_PRIMARY_DEPTH1 1
-#endif
-#ifndef MIRT_QUAD_BATCH_DEFAULT
-#define MIRT_QUAD_BATCH_DEFAULT 1
-#endif
-#ifndef MIRT_LEAF_BATCH_DEFAULT
-#define MIRT_LEAF_BATCH_DEFAULT 2
-#endif
 
-// Measured: the blocking call 1.22 -> 3.07 ms with the
-// queue (waiting waves alone +0.3 ms, the hand-overs +1.5 ms): off by default
-#ifndef MIRT_CONT_QUEUE_DEFAULT
-#define MIRT_CONT_QUEUE_DEFAULT 0
-#endif
 
 struct mirt_ctx {
     int device = 0;
@@ -1579,7 +1288,7 @@ struct mirt_ctx {
     // the frame scratch (queue, deferral list, phase events) is per ctx: a
     // launch on another stream than the previous one waits for it
     hipEvent_t done = nullptr;
-    // MIRT_LAZY_FOLD: another stream read this ctx's display slab for the
+    // Lazy fold: another stream read this ctx's display slab for the
     // share's pending fold; the ctx's next write to it waits for `slab_free`
     hipEvent_t slab_free = nullptr;
     bool slab_guard = false;
@@ -1623,9 +1332,8 @@ struct mirt_ctx {
     int bounce_blocks = 0;      // wavefront: persistent workgroups (set in mirt_create)
     int bounce_blocks_opt = 0;  // MIRT_OPT_BOUNCE_BLOCKS override (0: occupancy x CUs)
     int quad_drain = 1;         // four-wide bounce walk: finish the drain four lanes per ray
-    int quad_batch = MIRT_QUAD_BATCH_DEFAULT;  // small BVH batches one ray per quad (intersect_quad_kernel)
-    int primary_depth1 = MIRT_PRIMARY_DEPTH1;  // depth-1 frames through the camera-packet kernel alone
-    int leaf_batch_opt = MIRT_LEAF_BATCH_DEFAULT;  // MIRT_OPT_LEAF_BATCH: 0 off, 1 on, 2 auto (leaf_big)
+    int quad_batch = 1;                          // small BVH batches one ray per quad (intersect_quad_kernel)
+    int leaf_batch_opt = 2;                        // MIRT_OPT_LEAF_BATCH: 0 off, 1 on, 2 auto (leaf_big)
     int zero_copy = 1;          // MIRT_OPT_ZERO_COPY: blocking frames into page-locked memory written in place
     bool leaf_big = false;      // the four-wide tree (HNodes + LeafRecs) exceeds the chip's L2
     void* d_queue = nullptr;    // wavefront: {count, head} + bounce records
@@ -1638,9 +1346,6 @@ struct mirt_ctx {
     size_t keys_cap = 0;
     int num_cus = 0;
     int debug_stall_ms = 0;     // MIRT_OPT_DEBUG_STALL_MS: test hook, each frame starts behind a bounded wait
-    int cont_queue = MIRT_CONT_QUEUE_DEFAULT;  // MIRT_OPT_CONT_QUEUE: 0 off, 1 lone frames, 2 every frame
-    void* d_cq = nullptr;       // continuation queue: control words, records, slot flags
-    size_t cq_bytes = 0;
 };
 
 namespace {
@@ -1800,18 +1505,6 @@ bool build_pnodes(const mirt_node* nd, int nn, const mirt_sphere* sp, int ns, st
                 ref = kPNone;
             } else {
                 ref = kPLeaf | (uint32_t)n.sphere;
-                // the box is exactly the sphere's (bvh.c:26-35, float, no
-                // contraction: this file is built -ffp-contract=off): store
-                // the sphere, the walk recomputes the box bit for bit
-                const mirt_sphere& q = sp[n.sphere];
-                const float lo[3] = {q.center.x - q.radius, q.center.y - q.radius, q.center.z - q.radius};
-                const float hi[3] = {q.center.x + q.radius, q.center.y + q.radius, q.center.z + q.radius};
-                if (MIRT_PNODE_INLINE && std::memcmp(lo, n.bmin, sizeof lo) == 0 &&
-                    std::memcmp(hi, n.bmax, sizeof hi) == 0) {
-                    const float g[6] = {q.center.x, q.center.y, q.center.z, q.radius, 0.0f, 0.0f};
-                    std::memcpy(slot, g, sizeof g);
-                    ref |= kPInline;
-                }
             }
         }
         (k ? p.ref1 : p.ref0) = ref;
@@ -2033,7 +1726,7 @@ int accum_materialize(AccumShare* a, hipStream_t s)
     return MIRT_OK;
 }
 
-// A fresh frame's display left pending on its share (MIRT_LAZY_FOLD): the
+// A fresh frame's display left pending on its share (the lazy fold): the
 // newest fresh frame supersedes any earlier one.
 int accum_set_pending(AccumShare* a, mirt_ctx* c, const uint32_t* disp, hipStream_t s)
 {
@@ -2146,12 +1839,12 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
     // fold into a shared buffer, whichever stream enqueued it)
     float* const d_fold = f.samples > 1 || chain ? d_acc : nullptr;
     if (d_fold) d_acc = nullptr;
-    // MIRT_LAZY_FOLD: a fresh one-sample frame on a share leaves its display
+    // Lazy fold: a fresh one-sample frame on a share leaves its display
     // pending instead of folding it; any other frame that folds first takes
     // the pending one (an accumulating frame needs it in d_acc) or drops it (a
     // fresh multi-sample fold overwrites d_acc whole)
-    const bool lazy = MIRT_LAZY_FOLD && chain && d_fold && !f.accumulate && f.samples == 1;
-    if (MIRT_LAZY_FOLD && chain && d_fold && !lazy) {
+    const bool lazy = chain && d_fold && !f.accumulate && f.samples == 1;
+    if (chain && d_fold && !lazy) {
         if (f.accumulate) {
             if (int rc = accum_materialize(chain, s)) return rc;   // before this frame's render can touch a slab
         } else {
@@ -2176,7 +1869,7 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
     // depth 1 (camera rays and their shading only): the camera-packet kernel
     // alone, at its 8 waves per SIMD, where the tree admits the ordered walk
     const bool primary_only = c->trav == kTravWavefront && f.use_bvh && f.depth == 1 && !d_counts && c->fast_slab &&
-                              c->primary_depth1 && dev_scene(c).ordered;
+                              dev_scene(c).ordered;
     const int dbw = wavefront || primary_only ? 4 : bw;  // the wavefront kernels use 256-thread workgroups
     Deferred dfr{nullptr, nullptr, 0};
     c->phases_valid = wavefront;
@@ -2238,26 +1931,7 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
             primary_kernel<false, false><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl, octant_queue(c));
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ph1[ps], s));
-        // the continuation queue for a frame alone on the chip
-        const bool cq_on = sc.wide && c->fast_slab && c->quad_drain && !d_bdiag &&
-                           (c->cont_queue == 2 || (c->cont_queue == 1 && c->lone_frame));
-        ContQ cq{};
-        if (cq_on) {
-            cq.cap = (uint32_t)bblocks * 256u;
-            cq.consumers = (uint32_t)std::max(1, c->num_cus);
-            const size_t need = kCqCtlBytes + sizeof(ContRec) * cq.cap + 4 * (size_t)cq.cap;
-            if (int rc2 = ensure(&c->d_cq, &c->cq_bytes, need)) return rc2;
-            cq.ctl = (uint32_t*)c->d_cq;
-            cq.rec = (ContRec*)((char*)c->d_cq + kCqCtlBytes);
-            cq.flag = (uint32_t*)((char*)cq.rec + sizeof(ContRec) * cq.cap);
-            HIP_TRY(hipMemsetAsync(cq.ctl, 0, kCqCtlBytes, s));
-            HIP_TRY(hipMemsetAsync(cq.flag, 0, 4 * (size_t)cq.cap, s));
-        }
-        if (cq_on && leaf_batch(c))
-            bounce_kernel<true, 4, false, true><<<bblocks, 256, blds, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, nullptr, cq);
-        else if (cq_on)
-            bounce_kernel<true, 2, false, true><<<bblocks, 256, blds, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, nullptr, cq);
-        else if (d_bdiag && sc.wide)
+        if (d_bdiag && sc.wide)
             bounce_kernel<true, 2, true><<<bblocks, 256, blds, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, d_bdiag);
         else if (d_bdiag)
             bounce_kernel<true, 0, true><<<bblocks, 256, blds, s>>>(sc, f, d_out, d_acc, queue, qctl, c->bounce_threshold, c->quad_drain, d_bdiag);
@@ -2389,7 +2063,7 @@ void mirt_destroy(mirt_ctx* c)
     if (c->slab_guard) (void)hipEventSynchronize(c->slab_free);   // another stream's read of the slab
     accum_release(c->acc);
     for (void* p : {(void*)c->d_nodes, (void*)c->d_nodes32, (void*)c->d_geo, (void*)c->d_color, (void*)c->d_out,
-                    c->d_in, c->d_res, (void*)c->d_counts, (void*)c->d_defer, c->d_queue, c->d_cq, (void*)c->d_keys, (void*)c->d_pnodes,
+                    c->d_in, c->d_res, (void*)c->d_counts, (void*)c->d_defer, c->d_queue, (void*)c->d_keys, (void*)c->d_pnodes,
                     (void*)c->d_hnodes, (void*)c->d_haux, (void*)c->d_leaves, (void*)c->d_ndepth,
                     (void*)c->d_overlay})
         if (p) (void)hipFree(p);
@@ -2585,12 +2259,6 @@ int enqueue_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_desc* fd
         f1.samples = 1;
         f1.accumulate = 0;
         AccumShare* chain = accum_chain(c);
-        if (MIRT_LAZY_FOLD_BATCH && chain) {
-            // fresh frames: the last one's display left pending on the share
-            if (int rc2 = accum_set_pending(chain, c, *d_display, c->stream)) return rc2;
-            HIP_TRY(hipEventRecord(c->done, c->stream));
-            return MIRT_OK;
-        }
         if (chain) {   // this fold is newer than a pending fresh display: that one is dropped
             chain->pend = nullptr;
             chain->pend_ctx = nullptr;
@@ -2620,7 +2288,7 @@ int enqueue_host_frame(mirt_ctx* c, const mirt_camera* cam, const mirt_frame_des
     if (int rc = enqueue_frame(c, cam, fd, nullptr, &disp, fn)) return rc;
     // as a 2D copy (rows x width): the runtime takes a DMA engine for it, where a
     // 1D copy of the same bytes often runs as a blit kernel on this stream's
-    // compute queue (multi.hip MIRT_D2H_2D)
+    // compute queue (as multi.hip does)
     const size_t row = (size_t)fd->width * 4;
     HIP_TRY(hipMemcpy2DAsync(out, row, disp, row, row, (size_t)shard_row_count(fd), hipMemcpyDeviceToHost, c->stream));
     return MIRT_OK;
@@ -3221,21 +2889,6 @@ int mirt_phase_log(mirt_ctx* c, float* out, int max)
     return n;
 }
 
-// Diagnostics of the last frame that used the continuation queue: {records
-// pushed, records taken, pushers left, waiters left, error bits}.
-int mirt_cont_queue_stats(mirt_ctx* c, uint32_t* out, int n)
-{
-    if (!ctx_ok(c, false, "mirt_cont_queue_stats") || !out || n <= 0) return MIRT_E_INVALID;
-    if (!c->d_cq) return 0;
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    uint32_t w[kCqCtlBytes / 4];
-    HIP_TRY(hipMemcpy(w, c->d_cq, kCqCtlBytes, hipMemcpyDeviceToHost));
-    const uint32_t v[5] = {w[kCqHead], w[kCqTail], w[kCqPushers], w[kCqWaiters], w[kCqError]};
-    const int k = std::min(n, 5);
-    std::memcpy(out, v, sizeof(uint32_t) * k);
-    return k;
-}
-
 int mirt_set_option(mirt_ctx* c, int option, int value)
 {
     if (!c) return MIRT_E_INVALID;
@@ -3277,10 +2930,6 @@ int mirt_set_option(mirt_ctx* c, int option, int value)
         if (value < 0 || value > 2) break;
         c->zero_copy = value;
         return MIRT_OK;
-    case MIRT_OPT_CONT_QUEUE:
-        if (value < 0 || value > 2) break;
-        c->cont_queue = value;
-        return MIRT_OK;
     case MIRT_OPT_DEBUG_STALL_MS:
         if (value < 0 || value > 10000) break;
         c->debug_stall_ms = value;
@@ -3320,7 +2969,6 @@ int mirt_get_option(mirt_ctx* c, int option)
     if (option == MIRT_OPT_ZERO_COPY) return c->zero_copy;
     if (option == MIRT_OPT_QUEUE_ORDER) return c->queue_order;
     if (option == MIRT_OPT_DEBUG_STALL_MS) return c->debug_stall_ms;
-    if (option == MIRT_OPT_CONT_QUEUE) return c->cont_queue;
     if (option == MIRT_OPT_LEAF_BATCH) return leaf_batch(c) ? 1 : 0;  // in effect for the uploaded scene
     set_error("mirt_get_option: bad option %d", option);
     return MIRT_E_INVALID;

@@ -50,19 +50,7 @@ static_assert(sizeof(DNode) == 64, "device node is 64 B");
 // without a stack.
 constexpr uint32_t kPLeaf = 0x80000000u;
 constexpr uint32_t kPNone = 0xffffffffu;
-// MIRT_PNODE_INLINE: a leaf slot whose box is exactly its one sphere's
-// fl(c -+ r) (bvh.c:26-35 create_aabb_from_sphere; every 1-sphere leaf of the
-// reference's builds) holds the SPHERE instead (c.x, c.y, c.z, r) and its ref
-// carries kPInline: the walk recomputes the box with the same roundings and
-// has the sphere without a second dependent load.
-// Measured round 5: no faster -- the recomputed box's VALU costs
-// what the saved scalar load did (the sphere load mostly hits the scalar
-// cache or overlaps); off by default, kept as a build switch.
-#ifndef MIRT_PNODE_INLINE
-#define MIRT_PNODE_INLINE 0
-#endif
-constexpr uint32_t kPInline = 0x40000000u;
-constexpr uint32_t kPIndex = 0x3fffffffu;
+constexpr uint32_t kPIndex = 0x7fffffffu;
 struct __attribute__((aligned(64))) PNode {
     float c0[6];
     float c1[6];
@@ -475,39 +463,20 @@ __device__ __forceinline__ bool slab_cons(const SlabRay& r, const Prune& p, floa
 }
 
 // Per-ray constants of ray_sphere_intersect: a = d.d, 4a and 2a (hit.c:22-28).
-// MIRT_SPHRAY_LAZY (round 3): recomputed from d at each sphere test (eight
-// VALU) instead of held for the whole walk (four VGPRs fewer in every walk
-// loop: registers, not VALU, limit the walks); the same IEEE expressions, so
-// the same bits; 1/(2a) -- only the estimate's scale -- from v_rcp_f32
-// (1 ulp, well inside sphere_t's 2^-18 margin).
-#ifndef MIRT_SPHRAY_LAZY
-#define MIRT_SPHRAY_LAZY 1
-#endif
+// Recomputed from d at each sphere test (eight VALU) instead of held for the
+// whole walk (round 3: four VGPRs fewer in every walk loop -- registers, not
+// VALU, limit the walks); the same IEEE expressions, so the same bits; 1/(2a)
+// -- only the estimate's scale -- from v_rcp_f32 (1 ulp, well inside
+// sphere_t's 2^-18 margin).
 struct SphRay {
     float ox, oy, oz, dx, dy, dz;
-#if MIRT_SPHRAY_LAZY
     __device__ __forceinline__ float a() const { return dot3(dx, dy, dz, dx, dy, dz); }
     __device__ __forceinline__ float a4() const { return 4.0f * a(); }  // hit.c:25: (4 * a) * c
     __device__ __forceinline__ float inv2a() const { return __builtin_amdgcn_rcpf(2.0f * a()); }
     __device__ __forceinline__ double a2() const { return (double)(2.0f * a()); }
-#else
-    float a4_, inv2a_;
-    double a2_;
-    __device__ __forceinline__ float a4() const { return a4_; }
-    __device__ __forceinline__ float inv2a() const { return inv2a_; }
-    __device__ __forceinline__ double a2() const { return a2_; }
-#endif
 };
 
-__device__ __forceinline__ SphRay sph_ray(const Ray& r)
-{
-#if MIRT_SPHRAY_LAZY
-    return {r.ox, r.oy, r.oz, r.dx, r.dy, r.dz};
-#else
-    const float a = dot3(r.dx, r.dy, r.dz, r.dx, r.dy, r.dz);
-    return {r.ox, r.oy, r.oz, r.dx, r.dy, r.dz, 4.0f * a, 1.0f / (2.0f * a), (double)(2.0f * a)};
-#endif
-}
+__device__ __forceinline__ SphRay sph_ray(const Ray& r) { return {r.ox, r.oy, r.oz, r.dx, r.dy, r.dz}; }
 
 // hit.c:19-39 without point/normal (computed once for the winner): the t a
 // hit would record if it could still become the closest (t <= best, the
@@ -830,14 +799,7 @@ __device__ __forceinline__ bool visit_child(const DevScene& sc, const SlabRay& s
     if (ref & kPLeaf) {
         if (COUNT) cnt.nodes++;
         const int si = (int)(ref & kPIndex);
-        if (MIRT_PNODE_INLINE && (ref & kPInline)) {
-            // the sphere inline: its box as bvh.c:26-35 computes it
-            if (slab_box<FAST>(sr, pr, s0 - s3, s1 - s3, s2 - s3, s0 + s3, s1 + s3, s2 + s3, near)) {
-                if (COUNT) cnt.spheres++;
-                consider_sphere<FAST>(sc, sp, pr, sr.ox, sr.oy, sr.oz, si, make_float4(s0, s1, s2, s3), best_t,
-                                      best_s);
-            }
-        } else if (slab_box<FAST>(sr, pr, s0, s1, s2, s3, s4, s5, near)) {
+        if (slab_box<FAST>(sr, pr, s0, s1, s2, s3, s4, s5, near)) {
             if (COUNT) cnt.spheres++;
             consider_sphere<FAST>(sc, sp, pr, sr.ox, sr.oy, sr.oz, si, sc.geo[si], best_t, best_s);
         }
@@ -847,95 +809,6 @@ __device__ __forceinline__ bool visit_child(const DevScene& sc, const SlabRay& s
     // an inner box needs only a conservative test: the reference's test is
     // monotone under containment, so a ray that passes any leaf box below
     // passes this one too, and every leaf is still gated exactly
-    if (FAST) return slab_cons(sr, pr, s0, s1, s2, s3, s4, s5, near);
-    return slab_box<FAST>(sr, pr, s0, s1, s2, s3, s4, s5, near);
-}
-
-// MIRT_PACKET_PREFETCH (round 5): the packet walk's next
-// data requested through the VECTOR memory path at the start of each step,
-// while the step's box tests run. One global_load_dword per step, lanes
-// [16k, 16k + 16) loading target k's 64 B: k = 0 / 1 the node's two children
-// (an inner child's PNode, a leaf child's sphere), k = 2 the PNode on top of
-// the packet's stack (the target of a pop). Whatever the step decides --
-// descend into either child, pop, or gate a leaf -- its data is then in
-// flight already, so a step waits for ONE load issued before its tests
-// instead of a chain of scalar loads (node, then the leaf's sphere, then the
-// next node) each behind its own s_waitcnt; the values reach the scalar unit
-// by v_readlane. The vector path is nearly idle in this kernel (TD 9% busy).
-// Measured (profiles/r05_logs/r05p/): byte-identical, but the
-// packet launch alone 0.328 -> 0.452 ms at 8 waves per SIMD (13 VGPRs and 19
-// SGPRs spilled) and 0.455 at 7 (no VGPR spills): a vector round trip plus
-// the v_readlane chain is longer than the scalar loads it replaces, which
-// mostly hit the scalar cache. Off by default, kept as a build switch.
-#ifndef MIRT_PACKET_PREFETCH
-#define MIRT_PACKET_PREFETCH 0
-#endif
-
-__device__ __forceinline__ uint32_t readlane_u(uint32_t v, uint32_t l)
-{
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
-}
-
-__device__ __forceinline__ PNodeV pnode_from_lanes(uint32_t v, uint32_t b)
-{
-    PNodeV n;
-    n.a0 = __uint_as_float(readlane_u(v, b + 0));
-    n.a1 = __uint_as_float(readlane_u(v, b + 1));
-    n.a2 = __uint_as_float(readlane_u(v, b + 2));
-    n.a3 = __uint_as_float(readlane_u(v, b + 3));
-    n.a4 = __uint_as_float(readlane_u(v, b + 4));
-    n.a5 = __uint_as_float(readlane_u(v, b + 5));
-    n.b0 = __uint_as_float(readlane_u(v, b + 6));
-    n.b1 = __uint_as_float(readlane_u(v, b + 7));
-    n.b2 = __uint_as_float(readlane_u(v, b + 8));
-    n.b3 = __uint_as_float(readlane_u(v, b + 9));
-    n.b4 = __uint_as_float(readlane_u(v, b + 10));
-    n.b5 = __uint_as_float(readlane_u(v, b + 11));
-    n.r0 = readlane_u(v, b + 12);
-    n.r1 = readlane_u(v, b + 13);
-    n.flat = readlane_u(v, b + 14);
-    n.end = readlane_u(v, b + 15);
-    return n;
-}
-
-// The dword lane `w` (0..15) of a prefetch target loads: an inner child's
-// PNode word w, a leaf child's sphere word w & 3, nothing useful for kPNone
-// (a valid address all the same).
-__device__ __forceinline__ const uint32_t* prefetch_word(const DevScene& sc, uint32_t ref, uint32_t w)
-{
-    if (ref == kPNone) return (const uint32_t*)sc.pnodes + w;
-    if (ref & kPLeaf) return (const uint32_t*)(sc.geo + (ref & kPIndex)) + (w & 3u);
-    return (const uint32_t*)(sc.pnodes + ref) + w;
-}
-
-// visit_child with the leaf's sphere taken from the prefetch register
-// (lanes b .. b + 3) instead of a load of its own.
-template <bool FAST, bool COUNT>
-__device__ __forceinline__ bool visit_child_pf(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
-                                               uint32_t ref, float s0, float s1, float s2, float s3, float s4,
-                                               float s5, uint32_t pf, uint32_t b, float& near, float& best_t,
-                                               int& best_s, Counters& cnt)
-{
-    if (ref == kPNone) return false;
-    if (ref & kPLeaf) {
-        if (COUNT) cnt.nodes++;
-        const int si = (int)(ref & kPIndex);
-        if (MIRT_PNODE_INLINE && (ref & kPInline)) {
-            if (slab_box<FAST>(sr, pr, s0 - s3, s1 - s3, s2 - s3, s0 + s3, s1 + s3, s2 + s3, near)) {
-                if (COUNT) cnt.spheres++;
-                consider_sphere<FAST>(sc, sp, pr, sr.ox, sr.oy, sr.oz, si, make_float4(s0, s1, s2, s3), best_t,
-                                      best_s);
-            }
-        } else if (slab_box<FAST>(sr, pr, s0, s1, s2, s3, s4, s5, near)) {
-            if (COUNT) cnt.spheres++;
-            const float4 g = make_float4(__uint_as_float(readlane_u(pf, b)), __uint_as_float(readlane_u(pf, b + 1)),
-                                         __uint_as_float(readlane_u(pf, b + 2)),
-                                         __uint_as_float(readlane_u(pf, b + 3)));
-            consider_sphere<FAST>(sc, sp, pr, sr.ox, sr.oy, sr.oz, si, g, best_t, best_s);
-        }
-        return false;
-    }
-    if (COUNT) cnt.nodes++;
     if (FAST) return slab_cons(sr, pr, s0, s1, s2, s3, s4, s5, near);
     return slab_box<FAST>(sr, pr, s0, s1, s2, s3, s4, s5, near);
 }
@@ -964,67 +837,6 @@ __device__ __forceinline__ void closest_packet_ordered(const DevScene& sc, const
     uint32_t cur = 0;
     uint32_t top = 0;
     uint32_t st_node = 0, st_lo = 0, st_hi = 0;
-#if MIRT_PACKET_PREFETCH
-    (void)cur;
-    // the current node lives in lanes [cb, cb + 16) of the VGPR `nv` (one
-    // register instead of 16 SGPRs); its words are read where they are used
-    uint32_t nv = *((const uint32_t*)sc.pnodes + (lane & 15u));
-    uint32_t cb = 0;
-    const uint32_t seg = lane >> 4, w = lane & 15u;
-    while (mask) {
-        if (COUNT) cnt.steps++;
-        const uint32_t r0 = readlane_u(nv, cb + 12), r1 = readlane_u(nv, cb + 13);
-        // this step's possible next data: both children, and the stack's top
-        const uint32_t pop_node = top > 0 ? readlane_u(st_node, top - 1) : kPNone;
-        const uint32_t tgt = seg == 0 ? r0 : (seg == 1 ? r1 : pop_node);
-        uint32_t pf = 0;
-        if (seg < 3) pf = *prefetch_word(sc, tgt, w);
-        const bool in = (mask >> lane) & 1;
-        float e0 = 0.0f, e1 = 0.0f;
-        bool h0 = false, h1 = false;
-        if (in) {
-            h0 = visit_child_pf<FAST, COUNT>(sc, sr, sp, pr, r0, __uint_as_float(readlane_u(nv, cb + 0)),
-                                             __uint_as_float(readlane_u(nv, cb + 1)),
-                                             __uint_as_float(readlane_u(nv, cb + 2)),
-                                             __uint_as_float(readlane_u(nv, cb + 3)),
-                                             __uint_as_float(readlane_u(nv, cb + 4)),
-                                             __uint_as_float(readlane_u(nv, cb + 5)), pf, 0u, e0, best_t, best_s, cnt);
-            h1 = visit_child_pf<FAST, COUNT>(sc, sr, sp, pr, r1, __uint_as_float(readlane_u(nv, cb + 6)),
-                                             __uint_as_float(readlane_u(nv, cb + 7)),
-                                             __uint_as_float(readlane_u(nv, cb + 8)),
-                                             __uint_as_float(readlane_u(nv, cb + 9)),
-                                             __uint_as_float(readlane_u(nv, cb + 10)),
-                                             __uint_as_float(readlane_u(nv, cb + 11)), pf, 16u, e1, best_t, best_s,
-                                             cnt);
-        }
-        const uint64_t m0 = __ballot(h0), m1 = __ballot(h1);
-        if (m0 && m1) {
-            const uint64_t both = m0 & m1;
-            const uint64_t v = __ballot(((both >> lane) & 1) && e1 < e0);
-            const bool swap = 2 * __popcll(v) > __popcll(both);
-            const uint32_t second = swap ? r0 : r1;
-            const uint64_t sm = swap ? m0 : m1;
-            if (lane == top) {
-                st_node = second;
-                st_lo = (uint32_t)sm;
-                st_hi = (uint32_t)(sm >> 32);
-            }
-            top++;
-            mask = swap ? m1 : m0;
-            cb = swap ? 16u : 0u;
-        } else if (m0 | m1) {
-            mask = m0 | m1;
-            cb = m0 ? 0u : 16u;
-        } else if (top > 0) {
-            top--;
-            mask = ((uint64_t)readlane_u(st_hi, top) << 32) | (uint64_t)readlane_u(st_lo, top);
-            cb = 32u;
-        } else {
-            break;
-        }
-        nv = pf;
-    }
-#else
     while (mask) {
         if (COUNT) cnt.steps++;
         const PNodeV nd = load_pnode_uniform(sc.pnodes, cur);
@@ -1065,93 +877,6 @@ __device__ __forceinline__ void closest_packet_ordered(const DevScene& sc, const
             break;
         }
     }
-#endif
-}
-
-// MIRT_PACKET_HALVES (round 5, VERDICT r4 item 5's second form): the wave
-// walks TWO packets, its lower and upper 32 lanes (an 8x8 tile's rows 0-3 and
-// 4-7; with four frames per packet, frames 0-1 and 2-3 of the same pixels),
-// each with its own node, vote, lane mask and stack. Both halves' PNodes are
-// requested together each step, so one scalar wait covers two independent
-// loads where closest_packet_ordered has one load per wait; each lane takes
-// its half's node words by a per-lane select. A half that has finished
-// re-reads the other's node. Stack of half h: entry k in lane 32h + (k & 31)
-// of the register pair k >> 5 (depth <= 64 as above). The result is the
-// order-independent closest hit of consider_sphere, so byte-identical.
-#ifndef MIRT_PACKET_HALVES
-#define MIRT_PACKET_HALVES 0
-#endif
-template <bool FAST, bool COUNT>
-__device__ __forceinline__ void closest_packet_halves(const DevScene& sc, const Ray& ray, bool active, float& best_t,
-                                                      int& best_s, Counters& cnt)
-{
-    const SlabRay sr = slab_ray(ray);
-    const SphRay sp = sph_ray(ray);
-    Prune pr = prune_start(sc, ray.ox, ray.oy, ray.oz);
-    best_t = INFINITY;
-    best_s = -1;
-    const uint32_t lane = threadIdx.x & 63;
-    const bool hi = lane >= 32;
-    constexpr uint64_t kLo = 0xffffffffull, kHi = ~0xffffffffull;
-    uint64_t mask = __ballot(active);
-    uint32_t cur0 = 0, cur1 = 0, top0 = 0, top1 = 0;
-    uint32_t sn_a = 0, sm_a = 0, sn_b = 0, sm_b = 0;
-    while (mask) {
-        if (COUNT) cnt.steps++;
-        const uint32_t c0 = (mask & kLo) ? cur0 : cur1;
-        const uint32_t c1 = (mask & kHi) ? cur1 : cur0;
-        const PNodeV n0 = load_pnode_uniform(sc.pnodes, c0);
-        const PNodeV n1 = load_pnode_uniform(sc.pnodes, c1);
-        const bool in = (mask >> lane) & 1;
-        float e0 = 0.0f, e1 = 0.0f;
-        bool h0 = false, h1 = false;
-        if (in) {
-            h0 = visit_child<FAST, COUNT>(sc, sr, sp, pr, hi ? n1.r0 : n0.r0, hi ? n1.a0 : n0.a0,
-                                          hi ? n1.a1 : n0.a1, hi ? n1.a2 : n0.a2, hi ? n1.a3 : n0.a3,
-                                          hi ? n1.a4 : n0.a4, hi ? n1.a5 : n0.a5, e0, best_t, best_s, cnt);
-            h1 = visit_child<FAST, COUNT>(sc, sr, sp, pr, hi ? n1.r1 : n0.r1, hi ? n1.b0 : n0.b0,
-                                          hi ? n1.b1 : n0.b1, hi ? n1.b2 : n0.b2, hi ? n1.b3 : n0.b3,
-                                          hi ? n1.b4 : n0.b4, hi ? n1.b5 : n0.b5, e1, best_t, best_s, cnt);
-        }
-        const uint64_t m0 = __ballot(h0), m1 = __ballot(h1);
-        const uint64_t v = __ballot(h0 && h1 && e1 < e0);
-        // one half's step of closest_packet_ordered: descend (pushing the
-        // other child when both are entered), or pop, or finish (0)
-        auto step = [&](uint64_t H, uint32_t h, const PNodeV& nd, uint32_t& cur, uint32_t& top) -> uint64_t {
-            const uint64_t a = m0 & H, b = m1 & H;
-            if (a && b) {
-                const bool swap = 2 * __popcll(v & H) > __popcll(a & b);
-                const uint32_t slot = 32u * h + (top & 31u);
-                const uint32_t second = swap ? nd.r0 : nd.r1;
-                const uint32_t sm = (uint32_t)((swap ? a : b) >> (32u * h));
-                if (lane == slot) {
-                    if (top < 32) {
-                        sn_a = second;
-                        sm_a = sm;
-                    } else {
-                        sn_b = second;
-                        sm_b = sm;
-                    }
-                }
-                top++;
-                cur = swap ? nd.r1 : nd.r0;
-                return swap ? b : a;
-            }
-            if (a | b) {
-                cur = a ? nd.r0 : nd.r1;
-                return a | b;
-            }
-            if (top > 0) {
-                top--;
-                const uint32_t slot = 32u * h + (top & 31u);
-                cur = top < 32 ? readlane_u(sn_a, slot) : readlane_u(sn_b, slot);
-                const uint32_t sm = top < 32 ? readlane_u(sm_a, slot) : readlane_u(sm_b, slot);
-                return (uint64_t)sm << (32u * h);
-            }
-            return 0;
-        };
-        mask = step(kLo, 0u, n0, cur0, top0) | step(kHi, 1u, n1, cur1, top1);
-    }
 }
 
 // Per-lane DFS walk (any tree, the reference order): `cur` is the next flat
@@ -1168,9 +893,6 @@ struct DfsWalk {
 // node's whole subtree is walked as a DFS segment instead.
 #ifndef MIRT_WIDE_STACK
 #define MIRT_WIDE_STACK 20
-#endif
-#ifndef MIRT_EXTRA_NODE_LOAD
-#define MIRT_EXTRA_NODE_LOAD 0
 #endif
 constexpr int kWideStack = MIRT_WIDE_STACK;
 constexpr int kWideStride = 256;  // threads per workgroup of the bounce kernel
@@ -1299,19 +1021,6 @@ __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay
             s1 = p[1];
             s2 = p[2];
             s3 = p[3];
-#if MIRT_EXTRA_NODE_LOAD
-            // sensitivity probe (pricing a three-load node format):
-            // one more load instruction per visit, 1 = a word of the same
-            // node, 2 = a word of the neighbouring HNode (another 64-B line)
-            {
-                uint32_t z;   // an offset of 0 the compiler cannot see, so the load is not merged
-                asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-                const uint32_t* xp =
-                    (const uint32_t*)(sc.hnodes + (MIRT_EXTRA_NODE_LOAD == 2 ? (w.cur ^ 1u) : w.cur)) + z;
-                const uint32_t x = *xp;
-                asm volatile("" ::"v"(x));
-            }
-#endif
         }
         auto test = [&](const uint4& q, float& e) {
             if (COUNT && q.w != kPNone) cnt.nodes++;
@@ -1713,9 +1422,6 @@ __device__ __forceinline__ void closest_hit(const DevScene& sc, const Ray& ray, 
 
 // Spheres [s0, s1) against this lane's ray, in array order (the first of
 // equal t wins: renderer.c:39's strict `<`), into best_t / best_s.
-#ifndef MIRT_BRUTE_PACKED
-#define MIRT_BRUTE_PACKED 1
-#endif
 __device__ __forceinline__ void brute_range_packed(const DevScene& sc, const SphRay& sp, bool active, int s0, int s1,
                                                    float& best_t, int& best_s)
 {
@@ -1788,7 +1494,7 @@ __device__ __forceinline__ void closest_brute(const DevScene& sc, const Ray& ray
     best_t = INFINITY;
     best_s = -1;
     if (!__ballot(active) || sc.num_spheres == 0) return;
-    if (FAST && !COUNT && MIRT_BRUTE_PACKED) {
+    if (FAST && !COUNT) {
         brute_range_packed(sc, sp, active, 0, sc.num_spheres, best_t, best_s);
         return;
     }

@@ -554,3 +554,18 @@ class MultiRenderer:
 
     def wait(self):
         check(self.L.mirt_multi_wait(self.h), "mirt_multi_wait")
+
+    def stats(self):
+        """mirt_multi_get_stats as a dict (RCCL calls issued, copies, launches)."""
+        st = abi.MultiStats()
+        check(self.L.mirt_multi_get_stats(self.h, C.byref(st)), "mirt_multi_get_stats")
+        return {k: int(getattr(st, k)) for k, _ in abi.MultiStats._fields_}
+
+    def read_gathered(self, shard, rows, width, frame=0, lane=-1):
+        """Test hook: shard `shard`'s compact rows (rows x width RGBA8) of
+        frame `frame` as they arrived in device 0's gather buffer in the last
+        launch (lane -1) or lane `lane`'s."""
+        out = np.zeros((rows, width, 4), np.uint8)
+        check(self.L.mirt_multi_read_gathered(self.h, lane, shard, frame, ptr(out), out.nbytes),
+              "mirt_multi_read_gathered")
+        return out

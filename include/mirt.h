@@ -424,26 +424,18 @@ enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3,
                                        mirt_render_frame (a frame alone on the chip), grouped by
                                        direction octant per workgroup for frames in flight;
                                        1 = always grouped; 2 = always tile order. Speed only. */
-       MIRT_OPT_DEBUG_STALL_MS = 19, /* test hook: every frame of this context starts behind a
+       MIRT_OPT_DEBUG_STALL_MS = 19 /* test hook: every frame of this context starts behind a
                                        kernel that waits this many ms (0..10000, default 0), then
                                        exits -- a frame that overruns a caller's deadline
-                                       (mirt_multi's MIRT_MULTI_OPT_TIMEOUT_MS) without a hang */
-       MIRT_OPT_CONT_QUEUE = 20     /* wavefront, four-wide bounce walk: once a frame's bounce queue is
-                                       dry, waves out of chains wait and take chains starting their
-                                       next level from waves that still hold several, walking each
-                                       with the whole wave -- 1 for a frame alone on the chip (the
-                                       blocking mirt_render_frame), 2 for every frame, 0 (default)
-                                       never: measured slower. Speed only. */ };
+                                       (mirt_multi's MIRT_MULTI_OPT_TIMEOUT_MS) without a hang */ };
 /* Traversal ids keep their first-release values (mirt 0.1: TILE 0, WAVEFRONT 5).
    ABI note: the mirt 0.2 header numbered WAVEFRONT 1; mirt_set_option accepts
    1 as a deprecated alias of MIRT_TRAV_WAVEFRONT (mirt_get_option reads back
    5), to be dropped in 1.0. The retired ids 2-4 (chunked / DFS-only schedules
-   of mirt 0.1) and the retired option ids 8, 10, 12, 13 return MIRT_E_INVALID. */
+   of mirt 0.1) and the retired option ids 8, 10, 12, 13, 20 (20: the bounce
+   pass's continuation queue of mirt 0.5, measured slower and removed) return
+   MIRT_E_INVALID. */
 enum { MIRT_TRAV_TILE = 0, MIRT_TRAV_WAVEFRONT = 5, MIRT_TRAV_WAVEFRONT_V02 = 1 /* deprecated alias */ };
-/* Diagnostics of the last frame run with MIRT_OPT_CONT_QUEUE: up to n words of
-   {records pushed, records taken, pushers left, waiters left, error bits};
-   returns the words written (0: no such frame yet). Waits for the ctx. */
-int mirt_cont_queue_stats(mirt_ctx *ctx, uint32_t *out, int n);
 int mirt_set_option(mirt_ctx *ctx, int option, int value);
 int mirt_get_option(mirt_ctx *ctx, int option);
 

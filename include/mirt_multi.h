@@ -41,10 +41,14 @@
  * every call returns MIRT_E_DEVICE and mirt_multi_destroy releases only host
  * memory (device buffers of a possibly stuck GPU are left to process exit).
  *
- * Verification status: the RCCL gather has run with n = 1 (one device) only;
- * the n-GPU gather (sends from n devices' streams into rank 0) has not run on
- * a multi-GPU node yet. Copy mode with n same-device ranks exercises the same
- * geometry, strides and de-interleave.
+ * Verification status: on one GPU the RCCL gather runs end to end with
+ * MIRT_MULTI_OPT_GATHER_SELF (rank 0's slabs sent to itself) and in the
+ * per-shard emulation (rank k > 0's send, rank 0's receives, as self
+ * send/receive groups); tests/test_multi.py checks the received slabs and the
+ * frames against the reference's golden frame and mirt_multi_get_stats'
+ * counters. The n-GPU gather (sends from n devices' streams into rank 0) has
+ * not run on a multi-GPU node yet. Copy mode with n same-device ranks
+ * exercises the same geometry, strides and de-interleave.
  */
 #ifndef MIRT_MULTI_H
 #define MIRT_MULTI_H
@@ -94,13 +98,28 @@ enum {
     MIRT_MULTI_OPT_DIRECT_COPY = 259,    /* MIRT_MULTI_HOST_DIRECT: each rank's blocks of a frame as one strided
                                             copy (hipMemcpy2DAsync, 0, default), one copy per row block (1), or
                                             a kernel storing them into the mapped page-locked frame (2) */
-    MIRT_MULTI_OPT_COPY_STREAM = 260     /* MIRT_MULTI_QUEUE_AHEAD: a launch's copies on its context's stream
+    MIRT_MULTI_OPT_COPY_STREAM = 260,    /* MIRT_MULTI_QUEUE_AHEAD: a launch's copies on its context's stream
                                             behind its kernels (0, default) or on the context's copy stream (1);
                                             2: on the copy stream, and a launch is enqueued only once the
                                             kernels of the launch in its contexts' other slot have finished
                                             (one launch's kernels per context at a time; its copies still
                                             running). DESIGN §8 has the measurements */
+    MIRT_MULTI_OPT_GATHER_SELF = 261     /* gather delivery: 1 = rank 0's own slabs travel through the gather
+                                            too (an RCCL send to itself, or a device copy in copy mode) instead
+                                            of being read in place, so every slab of the frame takes one path
+                                            -- with one GPU, the RCCL gather path end to end. 0 = off (default) */
 };
+
+/* Counters of what the object issued since it was created (mirt_multi_get_stats). */
+typedef struct mirt_multi_stats {
+    uint64_t launches;      /* launches enqueued (mirt_multi_render_frames_async calls that succeeded) */
+    uint64_t comm_inits;    /* ncclCommInitAll calls that succeeded (0 or 1) */
+    uint64_t rccl_groups;   /* ncclGroupStart / ncclGroupEnd groups issued on rank 0 (one per gathered launch) */
+    uint64_t rccl_sends;    /* ncclSend calls issued (every rank) */
+    uint64_t rccl_recvs;    /* ncclRecv calls issued (rank 0) */
+    uint64_t rccl_bytes;    /* bytes those receives carry */
+    uint64_t device_copies; /* copy-mode gather copies (hipMemcpyAsync / hipMemcpyPeerAsync) */
+} mirt_multi_stats;
 
 /* n ranks on devices[0..n-1] (NULL: devices 0..n-1; n <= 64), `lanes` launches in
    flight (>= 1), flags MIRT_MULTI_*. With distinct devices and no
@@ -152,6 +171,16 @@ int mirt_multi_render_frame_async(mirt_multi *m, const mirt_camera *cam, const m
 /* Block until every launch on every lane has delivered its frames (bounded
    by MIRT_MULTI_OPT_TIMEOUT_MS). */
 int mirt_multi_wait(mirt_multi *m);
+
+/* The object's counters (struct above). */
+int mirt_multi_get_stats(const mirt_multi *m, mirt_multi_stats *out);
+/* Test hook (gather delivery, a frame split over > 1 shards or
+   MIRT_MULTI_OPT_GATHER_SELF): after waiting for lane `lane` (-1: the lane of
+   the last launch), copy shard `shard`'s display slab of frame `frame` of that
+   launch, as it arrived in device 0's gather buffer -- the shard's compact rows
+   (its row blocks in image order, width pixels each) -- into host `out`
+   (`bytes` at least rows x width x 4). Blocking. */
+int mirt_multi_read_gathered(mirt_multi *m, int lane, int shard, int frame, mirt_rgba8 *out, size_t bytes);
 
 #ifdef __cplusplus
 }

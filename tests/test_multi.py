@@ -3,12 +3,15 @@
 slabs gathered to rank 0 over RCCL, de-interleaved there).
 
 The frame of n ranks must equal the one-GPU frame byte for byte (the RNG
-contract keys on the full-frame pixel index). On the one-GPU box: n = 1 runs
-the real RCCL path (ncclCommInitAll over one device, every slab through an
-ncclSend/ncclRecv group), and n = 2 / 3 / 8 ranks on the same device run the
-copy-mode gather (RCCL refuses two ranks on one device) -- the same shard
-geometry, slab strides and de-interleave as n GPUs. CPU: the entry points
-fail loudly without a GPU."""
+contract keys on the full-frame pixel index). On the one-GPU box the RCCL
+gather runs for real in two ways: n = 1 with MIRT_MULTI_OPT_GATHER_SELF (rank
+0's slab sent to itself through ncclCommInitAll's communicator), and the
+per-shard emulation (rank k > 0's send, rank 0's world - 1 receives, as
+ncclSend/ncclRecv groups on the one device), each checked against the
+reference's golden frame and the library's RCCL call counters. n = 2 / 3 / 8
+ranks on the same device run the copy-mode gather (RCCL refuses two ranks on
+one device) -- the same shard geometry, slab strides and de-interleave as n
+GPUs. CPU: the entry points fail loudly without a GPU."""
 import hashlib
 
 import numpy as np
@@ -35,17 +38,141 @@ def scene10k(mirt):
     return s, mirt.build_bvh(s)
 
 
+def shard_rows(H, world, k, rb=8):
+    """Image rows of shard k, in its compact slab's order (row block b goes to
+    shard b % world: host_scene.cpp shard_row_count's geometry)."""
+    return np.array([y for y in range(H) if (y // rb) % world == k])
+
+
+@pytest.fixture(scope="module")
+def golden_frame(gpu, mirt, golden, scene10k):
+    """The 1080p / 10k depth-5 frame from one context, pinned to the
+    reference's SHA-256 (tests/golden/golden.json)."""
+    s, b = scene10k
+    gpu.upload(s, b)
+    img = gpu.render_frame(mirt.default_camera(), 1920, 1080, depth=5, seed=1)
+    assert sha(img) == golden["frames"][GOLD]["sha"]
+    return img
+
+
 @pytest.mark.gpu
-def test_multi_rccl_one_gpu_golden(mirt, golden, scene10k):
-    """n = 1 through RCCL: the golden 1080p / 10k depth-5 frame."""
+def test_multi_one_rank_reads_its_slab_in_place(mirt, golden, scene10k):
+    """n = 1 on the RCCL backend without an exchange: the golden frame, and
+    the counters show that no RCCL call was made (one rank's slab is its frame)."""
     s, b = scene10k
     with mirt.MultiRenderer([0]) as m:
         assert m.backend == "rccl" and m.size == 1
         m.upload(s, b)
         img = m.render_frame(mirt.default_camera(), 1920, 1080, depth=5, seed=1)
         assert sha(img) == golden["frames"][GOLD]["sha"]
-        img2 = m.render_frame(mirt.default_camera(), 1920, 1080, depth=5, seed=1)
-        assert sha(img2) == golden["frames"][GOLD]["sha"]
+        st = m.stats()
+        assert st["launches"] == 1 and st["comm_inits"] == 0 and st["rccl_sends"] == 0 and st["rccl_recvs"] == 0
+
+
+@pytest.mark.gpu
+def test_multi_rccl_gather_self_golden(mirt, golden, scene10k):
+    """n = 1 through the RCCL gather end to end (MIRT_MULTI_OPT_GATHER_SELF:
+    rank 0's slab goes through ncclCommInitAll's communicator as an
+    ncclSend/ncclRecv group to itself, the frame is read from the gather
+    buffer): the golden 1080p / 10k depth-5 frame, twice, with the RCCL calls
+    counted (main.c:356-374's frame, multi.hip's gather group)."""
+    s, b = scene10k
+    W, H = 1920, 1080
+    with mirt.MultiRenderer([0]) as m:
+        assert m.backend == "rccl" and m.delivery == "gather"
+        m.set_option(mirt.abi.MULTI_OPT_GATHER_SELF, 1)
+        assert m.get_option(mirt.abi.MULTI_OPT_GATHER_SELF) == 1
+        m.upload(s, b)
+        for k in range(2):
+            img = m.render_frame(mirt.default_camera(), W, H, depth=5, seed=1)
+            assert sha(img) == golden["frames"][GOLD]["sha"], k
+            assert sha(m.read_gathered(0, H, W)) == golden["frames"][GOLD]["sha"], k
+        st = m.stats()
+        print("rccl stats", st)
+        assert st["comm_inits"] == 1
+        assert st["rccl_groups"] == 2 and st["rccl_sends"] == 2 and st["rccl_recvs"] == 2
+        assert st["rccl_bytes"] == 2 * W * H * 4 and st["device_copies"] == 0
+        # a batched launch through the same path: two frames in one receive
+        hb = [mirt.HostBuffer((H, W, 4)) for _ in range(2)]
+        try:
+            m.render_frames_async(mirt.default_camera(), mirt.frame_desc(W, H, depth=5, seed=1, sample=0), hb)
+            m.wait()
+            assert sha(hb[0].array) == golden["frames"][GOLD]["sha"]
+        finally:
+            for x in hb:
+                x.close()
+        assert m.stats()["rccl_recvs"] == 3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 8])
+def test_multi_rccl_emulated_gather_golden_rows(mirt, golden_frame, scene10k, world):
+    """The N-GPU gather's RCCL path on one GPU, shard by shard
+    (MIRT_MULTI_OPT_EMULATE_WORLD / _RANK, gather delivery): rank k > 0
+    renders its row blocks and sends them (an ncclSend/ncclRecv group to
+    itself); what arrives in the gather buffer is exactly the golden frame's
+    rows of shard k. Rank 0 renders its blocks, receives world - 1 slabs
+    through RCCL (its own slab standing in for each), de-interleaves and
+    delivers the frame: its own rows equal the golden frame's, and every
+    received slab equals what was sent. Every RCCL call is counted."""
+    s, b = scene10k
+    W, H = 1920, 1080
+    full = golden_frame
+    cam = mirt.default_camera()
+    hb = mirt.HostBuffer((H, W, 4))
+    try:
+        with mirt.MultiRenderer([0], lanes=2) as m:
+            assert m.backend == "rccl" and m.delivery == "gather"
+            m.upload(s, b)
+            sends = recvs = 0
+            for k in list(range(1, world)) + [0]:
+                m.emulate(world, k)
+                hb.array[:] = 7
+                m.render_frame_async(cam, mirt.frame_desc(W, H, depth=5, seed=1), hb)
+                m.wait()
+                mine = shard_rows(H, world, k)
+                if k > 0:
+                    # rank k's slab as rank 0 received it; rank k delivers nothing itself
+                    assert (m.read_gathered(k, len(mine), W) == full[mine]).all(), k
+                    assert (hb.array == 7).all(), k
+                    sends, recvs = sends + 1, recvs + 1
+                else:
+                    assert (hb.array[mine] == full[mine]).all()
+                    for q in range(1, world):
+                        rq = len(shard_rows(H, world, q))
+                        assert (m.read_gathered(q, rq, W) == full[mine][:rq]).all(), q
+                    sends, recvs = sends + world - 1, recvs + world - 1
+                st = m.stats()
+                assert st["rccl_sends"] == sends and st["rccl_recvs"] == recvs, (k, st)
+            assert st["comm_inits"] == 1 and st["device_copies"] == 0
+            print("rccl stats", st)
+    finally:
+        hb.close()
+
+
+@pytest.mark.gpu
+def test_multi_queue_ahead_close_after_fresh_frame(mirt, scene10k):
+    """Closing a QUEUE_AHEAD renderer right after a fresh one-frame launch on
+    a context-owning slot (its display left pending on the shared
+    accumulation buffer, in that slot's own slab): the pending fold is taken
+    before any slab is freed, and the device stays usable."""
+    s, b = scene10k
+    W, H = 320, 180
+    cam = mirt.default_camera()
+    hb = [mirt.HostBuffer((H, W, 4)) for _ in range(3)]
+    try:
+        m = mirt.MultiRenderer([0, 0], lanes=2, queue_ahead=True)
+        m.upload(s, b)
+        m.render_frames_async(cam, mirt.frame_desc(W, H, depth=5, seed=2, sample=0), hb[:2])   # slot 0
+        m.render_frame_async(cam, mirt.frame_desc(W, H, depth=5, seed=2, sample=2), hb[2])     # slot 1: fresh, lazy
+        m.close()
+        with mirt.Renderer(0) as r:
+            r.upload(s, b)
+            want = r.render_frame(cam, W, H, depth=5, seed=2, sample=2)
+        assert (hb[2].array == want).all()
+    finally:
+        for x in hb:
+            x.close()
 
 
 @pytest.mark.gpu
