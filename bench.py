@@ -611,11 +611,13 @@ def frame_desc_for(f0, n, depth, accumulate):
                            jitter=JITTER)
 
 
-def plan(f0, steps, per):
-    """(first frame, frames) of the launches covering `steps` frames from f0"""
+def plan(f0, steps, per, ramp=0):
+    """(first frame, frames) of the launches covering `steps` frames from f0;
+    `ramp`: the first `ramp` launches carry one frame each (their frames are
+    done, and their delivery starts, before a full launch's would be)"""
     out, f, end = [], f0, f0 + steps
     while f < end:
-        k = min(per, end - f)
+        k = min(1 if len(out) < ramp else per, end - f)
         out.append((f, k))
         f += k
     return out
@@ -686,12 +688,12 @@ def devices_for(n):
 def open_multi(n, lanes, host_direct, spheres, bvh, blocks, opts, timeout_ms=120000, ahead=False):
     m = mirt.MultiRenderer(devices_for(n), lanes=lanes, host_direct=host_direct, queue_ahead=ahead)
     m.set_option(mirt.abi.MULTI_OPT_TIMEOUT_MS, timeout_ms)
+    for ov in opts:   # before the upload: some options (MIRT_OPT_NODE_ORDER) shape the scene's layout
+        o, v = (int(t) for t in ov.split("="))
+        m.set_option(o, v)
     m.upload(spheres, bvh)
     if blocks >= 0:
         m.set_option(mirt.abi.OPT_BOUNCE_BLOCKS, blocks)
-    for ov in opts:
-        o, v = (int(t) for t in ov.split("="))
-        m.set_option(o, v)
     return m
 
 
@@ -771,8 +773,13 @@ def measure(args):
         if k_lane:
             phases += m.phase_log(lane, 0, min(k_lane, 64))
     primary_ms, bounce_ms = (float(v) for v in np.mean(np.array(phases), axis=0)) if phases else (0.0, 0.0)
-    # depth 1 (camera rays and their shading only), frames to host memory
+    # depth 1 (camera rays and their shading only), frames to host memory, and
+    # (one GPU) the same loop with the frames left on the device
     el_d1 = timed_loop(m, cam, plan(0, 2, per), plan(args.warmup, args.steps, per), bufs, 1, False, tail)
+    el_d1_dev = None
+    if n == 1:
+        el_d1_dev = timed_loop(m, cam, plan(0, 2, per), plan(args.warmup, args.steps, per), bufs, 1, False, tail,
+                               device_only=True)
     # the same loop with the frames left on the device(s): N = 1 in the
     # rank's slabs; N > 1 gathered on GPU 0 over RCCL (below)
     el_dev = None
@@ -826,6 +833,10 @@ def measure(args):
                                  "the same launches with every frame gathered on GPU 0 over RCCL and "
                                  "de-interleaved there (no D2H)"),
         "depth1_mrays_s": round(W * H * SPP * args.steps / el_d1 / 1e6, 3),
+        "depth1_device_resident_mrays_s": round(W * H * SPP * args.steps / el_d1_dev / 1e6, 3) if el_d1_dev else None,
+        "depth1_note": "depth 1 through the same loop: frames delivered to page-locked host memory (depth1_mrays_s; "
+                       "a 1080p frame's D2H is 0.155 ms at the link's 53.5 GB/s) and left in HBM "
+                       "(depth1_device_resident_mrays_s)",
         "bvh_build_s": round(build_s, 4),
         "frame_sha_last": frame_sha(last_frame),
         "last_frame_equals_one_context": same,

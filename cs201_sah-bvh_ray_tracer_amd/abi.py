@@ -205,7 +205,7 @@ SIGNATURES = [
 OPT_TRAVERSAL, OPT_FAST_SLAB, OPT_BLOCK_WAVES, OPT_DEFER, OPT_BOUNCE_THRESHOLD, OPT_PRUNE, OPT_ORDERED = (
     1, 2, 3, 4, 5, 6, 7)
 OPT_BOUNCE_BLOCKS, OPT_QUAD_DRAIN, OPT_LEAF_BATCH, OPT_QUAD_BATCH, OPT_ZERO_COPY = 9, 11, 14, 15, 17
-OPT_QUEUE_ORDER, OPT_DEBUG_STALL_MS = 18, 19
+OPT_QUEUE_ORDER, OPT_DEBUG_STALL_MS, OPT_NODE_ORDER, OPT_PRIMARY_WALK = 18, 19, 21, 22
 TRAV_TILE, TRAV_WAVEFRONT = 0, 5
 MULTI_COPY, MULTI_HOST_DIRECT, MULTI_QUEUE_AHEAD = 1, 2, 4
 MULTI_FULL_GRID = 1

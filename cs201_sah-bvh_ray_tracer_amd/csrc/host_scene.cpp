@@ -62,7 +62,7 @@ int shard_row_count(const mirt_frame_desc* fd)
 
 extern "C" {
 
-const char* mirt_version(void) { return "mirt 0.5 (gfx950)"; }
+const char* mirt_version(void) { return "mirt 0.6 (gfx950)"; }
 const char* mirt_last_error(void) { return mirt::g_err; }
 
 // ------------------------------------------------------------------ rand

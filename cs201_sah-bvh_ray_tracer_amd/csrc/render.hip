@@ -344,25 +344,36 @@ struct BounceRec {
 // ORD: the tree admits the ordered packet walk (DevScene::ordered), which
 // also takes zero-component rays -- that build has no deferred waves and no
 // other walk, so it keeps the register budget of the packet walk alone.
-template <bool FAST, bool ORD>
+// LANE (MIRT_OPT_PRIMARY_WALK 1, ordered four-wide trees only): each camera ray
+// walks the four-wide tree on its own (the bounce kernel's walk, an LDS stack
+// column per lane) instead of in its wave's packet -- for deep trees, where
+// an 8x8 tile's rays part ways early and a packet step tests every lane
+// against nodes that few of them reach. The same closest hit (least t, a
+// tie to the larger sphere index), so the same frame.
+template <bool FAST, bool ORD, bool LANE = false>
 // Register budget of the ordered camera-packet kernel (ORD): 8 waves per SIMD (64 VGPRs, no
 // scratch; 67 and 7 waves without the attribute). With four frames in flight
 // its waves share the CUs with the bounce passes, and the eighth wave hides
 // more of the packet walk's scalar-load latency (1080p/10k +0.3-1.1%,
 // 1080p/100k +3.7%, profiles/r02_ab/r02ax_primary_waves8_*).
+#ifndef MIRT_BOUNCE_WAVES
+#define MIRT_BOUNCE_WAVES 5
+#endif
 #ifndef MIRT_PRIMARY_WAVES
 #define MIRT_PRIMARY_WAVES 8
 #endif
 // (Round 3: the ordered kernel groups each workgroup's first bounces by
 // direction octant in the queue -- scripts/tree_quality.cpp's lockstep model:
 // distinct nodes per lane-step -9%, busy lanes per step +13%; measured +1.8%.)
-#define MIRT_PRIMARY_ATTR __attribute__((amdgpu_waves_per_eu(ORD ? MIRT_PRIMARY_WAVES : 1)))
+#define MIRT_PRIMARY_ATTR __attribute__((amdgpu_waves_per_eu(LANE ? MIRT_BOUNCE_WAVES : ORD ? MIRT_PRIMARY_WAVES : 1)))
 __global__ __launch_bounds__(256) MIRT_PRIMARY_ATTR void primary_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
                                                       float* __restrict__ acc, Deferred dfr,
                                                       BounceRec* __restrict__ queue, uint32_t* __restrict__ qctl,
                                                       int octants = 1)
 {
+    static_assert(!LANE || ORD, "the per-lane camera walk needs the ordered four-wide tree");
     __shared__ uint32_t cstack[ORD ? 1 : kMaxDepth * 256];
+    __shared__ uint32_t wstack[LANE ? kWideStack * kWideStride : 1];
     Counters cnt{0, 0, 0, 0, 0};
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
@@ -411,7 +422,9 @@ __global__ __launch_bounds__(256) MIRT_PRIMARY_ATTR void primary_kernel(DevScene
     if (!ORD && dfr.blocks > 0 && alive && slab_ray(ray).generic) alive = false;  // traced by a deferred wave
     float t;
     int s;
-    if constexpr (ORD) {
+    if constexpr (LANE) {
+        closest_hit<false, FAST, false>(sc, ray, alive, t, s, cnt, wstack + threadIdx.x);
+    } else if constexpr (ORD) {
         closest_packet_ordered<FAST, false>(sc, ray, alive, t, s, cnt);
     } else
         closest_hit<true, FAST, false>(sc, ray, alive, t, s, cnt);
@@ -640,9 +653,6 @@ __device__ __forceinline__ void solo_chain(const DevScene& sc, const FrameConst&
 // Register budget of the bounce kernel: 5 waves per SIMD (<= 96 VGPRs; 4
 // without the attribute, at 114). The pipelined frames gain most: the
 // co-running primary pass gets the issue slots the fifth wave hides.
-#ifndef MIRT_BOUNCE_WAVES
-#define MIRT_BOUNCE_WAVES 5
-#endif
 #define MIRT_BOUNCE_ATTR __attribute__((amdgpu_waves_per_eu(MIRT_BOUNCE_WAVES)))
 template <bool FAST, int WALK, bool DIAG = false>
 __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
@@ -1321,7 +1331,8 @@ struct mirt_ctx {
     int ordered = 1;            // ordered (nearer-child-first) walks where the tree admits them
     HNode* d_hnodes = nullptr;  // four-wide layout (per-lane walks)
     HAux* d_haux = nullptr;
-    LeafRec* d_leaves = nullptr;
+    char* d_leaves = nullptr;   // leaf spheres (float4 each), then at leaf_box_off the leaf boxes (LeafBox each)
+    size_t leaf_box_off = 0;
     uint32_t num_hnodes = 0;
     uint32_t wide_root = 0;     // HNode a four-wide walk starts at (DevScene::wide_root)
     uint8_t* d_ndepth = nullptr;  // depth of every flat node (BVH overlay colours)
@@ -1335,11 +1346,13 @@ struct mirt_ctx {
     int quad_batch = 1;                          // small BVH batches one ray per quad (intersect_quad_kernel)
     int leaf_batch_opt = 2;                        // MIRT_OPT_LEAF_BATCH: 0 off, 1 on, 2 auto (leaf_big)
     int zero_copy = 1;          // MIRT_OPT_ZERO_COPY: blocking frames into page-locked memory written in place
-    bool leaf_big = false;      // the four-wide tree (HNodes + LeafRecs) exceeds the chip's L2
+    bool leaf_big = false;      // the four-wide tree (HNodes + leaves) exceeds the chip's L2
     void* d_queue = nullptr;    // wavefront: {count, head} + bounce records
     size_t queue_cap = 0;
     bool lone_frame = false;    // mirt_render_frame's frame: the first bounces queued in tile order
     int queue_order = 0;        // MIRT_OPT_QUEUE_ORDER: 0 auto (tile order for lone_frame), 1 octants, 2 tile order
+    int node_order = 0;         // MIRT_OPT_NODE_ORDER: HNode numbering at the next upload (order_hnodes)
+    int primary_walk = 0;       // MIRT_OPT_PRIMARY_WALK: camera rays as packets (0) or per lane, four-wide (1)
     uint32_t* d_defer = nullptr;  // [count, list...]
     size_t defer_cap = 0;
     unsigned long long* d_keys = nullptr;  // chunked brute force: per-ray (t, index) keys
@@ -1565,15 +1578,15 @@ uint16_t half_up(float v)
 
 // HNode layout (trace.h) of a validated flat tree: HNode 0 holds the root;
 // an HNode for each inner node that is some HNode's slot holds that node's
-// grandchildren (a leaf child standing in for its own); one LeafRec per
-// leaf slot. Used only when the PNode conditions hold and the boxes nest.
+// grandchildren (a leaf child standing in for its own); one leaf (sphere +
+// exact box) per leaf slot. Used only when the PNode conditions hold and the boxes nest.
 void build_hnodes(const mirt_node* nd, int nn, const mirt_sphere* sp, int ns, std::vector<HNode>& hn,
-                  std::vector<HAux>& aux, std::vector<LeafRec>& leaves, std::vector<uint32_t>& src)
+                  std::vector<HAux>& aux, std::vector<float4>& lgeo, std::vector<LeafBox>& lbox)
 {
     hn.assign(1, HNode{});
-    src.assign(4, kPNone);  // src[4 h + k]: the flat node slot k of HNode h stands for
     aux.assign(1, HAux{0xffffffffu, (uint32_t)nn});  // flat + 1 == 0: the whole tree
-    leaves.clear();
+    lgeo.clear();
+    lbox.clear();
     std::vector<uint32_t> todo;  // inner nodes waiting for their HNode: HNode 1 + i is todo[i]
     auto fill = [&](size_t hi, int k, uint32_t c) {
         HNode& h = hn[hi];
@@ -1592,14 +1605,14 @@ void build_hnodes(const mirt_node* nd, int nn, const mirt_sphere* sp, int ns, st
             if (n.sphere >= ns) {
                 ref = kPNone;
             } else {
-                LeafRec l{};
+                LeafBox l{};
                 std::memcpy(l.lo, n.bmin, sizeof l.lo);
                 std::memcpy(l.hi, n.bmax, sizeof l.hi);
                 l.sphere = n.sphere;
                 const mirt_sphere& s = sp[n.sphere];
-                l.geo = make_float4(s.center.x, s.center.y, s.center.z, s.radius);
-                ref = kPLeaf | (uint32_t)leaves.size();
-                leaves.push_back(l);
+                ref = kPLeaf | (uint32_t)lbox.size();
+                lbox.push_back(l);
+                lgeo.push_back(make_float4(s.center.x, s.center.y, s.center.z, s.radius));
             }
         } else {
             todo.push_back(ci);
@@ -1615,7 +1628,6 @@ void build_hnodes(const mirt_node* nd, int nn, const mirt_sphere* sp, int ns, st
         HNode h{};
         for (int k = 0; k < 4; k++) h.slot[k].ref = kPNone;
         hn.push_back(h);
-        src.resize(4 * hn.size(), kPNone);
         aux.push_back(HAux{y, nd[y].skip & MIRT_SKIP_MASK});
         // the four slots: y's live children, then the inner slot with the
         // largest box replaced by its two live children while a slot is
@@ -1651,6 +1663,73 @@ void build_hnodes(const mirt_node* nd, int nn, const mirt_sphere* sp, int ns, st
     }
 }
 
+// MIRT_OPT_NODE_ORDER 1: renumber the HNodes (and the leaves) for locality
+// of the walks' accesses: the first `keep` HNodes (the top levels every walk
+// starts in, staged in LDS by the bounce kernel) keep their breadth-first
+// numbers; below them the tree is laid out depth first with every node's
+// inner children as one contiguous group (siblings share lines, as
+// breadth-first order gives, and a subtree's nodes -- what one ray's walk
+// below that level touches -- lie together instead of spread over every
+// level of the whole tree). Each HNode's leaves are renumbered in the new
+// node order, so a subtree's spheres lie together too. Only the numbering
+// changes: every visit, test and tie is the same.
+void order_hnodes(std::vector<HNode>& hn, std::vector<HAux>& aux, std::vector<float4>& lgeo,
+                  std::vector<LeafBox>& lbox, size_t keep)
+{
+    const size_t nh = hn.size();
+    keep = std::min(keep, nh);
+    std::vector<uint32_t> nid(nh, kPNone), order;
+    order.reserve(nh);
+    auto emit = [&](uint32_t h) {
+        nid[h] = (uint32_t)order.size();
+        order.push_back(h);
+    };
+    for (size_t h = 0; h < keep; h++) emit((uint32_t)h);
+    std::vector<uint32_t> stack;
+    for (size_t h = keep; h-- > 0;) stack.push_back((uint32_t)h);
+    while (!stack.empty()) {
+        const uint32_t h = stack.back();
+        stack.pop_back();
+        uint32_t kids[4];
+        int nk = 0;
+        for (int k = 0; k < 4; k++) {
+            const uint32_t r = hn[h].slot[k].ref;
+            if (r != kPNone && !(r & kPLeaf) && r < nh && nid[r] == kPNone) kids[nk++] = r;
+        }
+        for (int k = 0; k < nk; k++) emit(kids[k]);
+        for (int k = nk; k-- > 0;) stack.push_back(kids[k]);
+    }
+    for (size_t h = 0; h < nh; h++)   // unreachable nodes (none in a built tree) keep a slot
+        if (nid[h] == kPNone) emit((uint32_t)h);
+    std::vector<HNode> h2(nh);
+    std::vector<HAux> a2(nh);
+    std::vector<float4> g2;
+    std::vector<LeafBox> b2;
+    g2.reserve(lgeo.size());
+    b2.reserve(lbox.size());
+    for (size_t i = 0; i < nh; i++) {
+        HNode n = hn[order[i]];
+        for (int k = 0; k < 4; k++) {
+            uint32_t& r = n.slot[k].ref;
+            if (r == kPNone) continue;
+            if (r & kPLeaf) {
+                const uint32_t l = r & ~kPLeaf;
+                r = kPLeaf | (uint32_t)b2.size();
+                g2.push_back(lgeo[l]);
+                b2.push_back(lbox[l]);
+            } else {
+                r = nid[r];
+            }
+        }
+        h2[i] = n;
+        a2[i] = aux[order[i]];
+    }
+    hn.swap(h2);
+    aux.swap(a2);
+    lgeo.swap(g2);
+    lbox.swap(b2);
+}
+
 // MIRT_OPT_LEAF_BATCH: the bounce walk loads a step's passing leaf spheres
 // together (bounce_kernel WALK 4) -- by default when the four-wide tree is
 // larger than the chip's L2 (32 MiB over the 8 XCDs), where the leaf loads
@@ -1665,7 +1744,8 @@ DevScene dev_scene(const mirt_ctx* c)
     const bool prune = c->prune && c->prune_ok;
     const bool ordered = prune && c->ordered && c->ordered_ok && c->fast_slab;
     return DevScene{c->d_nodes, c->d_nodes32, c->d_geo, c->d_color, (uint32_t)c->num_nodes, c->num_spheres,
-                    prune, c->r_max, c->c_max, c->d_pnodes, ordered, c->d_hnodes, c->d_haux, c->d_leaves, ordered,
+                    prune, c->r_max, c->c_max, c->d_pnodes, ordered, c->d_hnodes, c->d_haux,
+                    (const float4*)c->d_leaves, (const LeafBox*)(c->d_leaves + c->leaf_box_off), ordered,
                     ordered ? c->num_hnodes : 0u, c->wide_root};
 }
 
@@ -1902,7 +1982,10 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
         BounceRec* queue = (BounceRec*)((char*)c->d_queue + kQCtlBytes);
         const int ptiles = f.samples >= 4 ? ((f.width + 3) / 4) * ((f.shard_rows + 3) / 4) * ((f.samples + 3) / 4)
                                           : tiles;
-        primary_kernel<true, true><<<(ptiles + 3) / 4, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
+        if (c->primary_walk == 1 && sc.wide)
+            primary_kernel<true, true, true><<<(ptiles + 3) / 4, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
+        else
+            primary_kernel<true, true><<<(ptiles + 3) / 4, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
         HIP_TRY(hipGetLastError());
         if (int rc2 = fold()) return rc2;
         if (timed) HIP_TRY(hipEventRecord(c->ev1, s));
@@ -1923,7 +2006,10 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
         const int pblocks = (ptiles + 3) / 4 + dfr.blocks;
         const int bblocks = c->bounce_blocks_opt ? c->bounce_blocks_opt : c->bounce_blocks;
         const size_t blds = bounce_lds_bytes(f.depth);
-        if (c->fast_slab && sc.ordered)
+        if (c->fast_slab && sc.ordered && sc.wide && c->primary_walk == 1)
+            primary_kernel<true, true, true><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl,
+                                                                   octant_queue(c));
+        else if (c->fast_slab && sc.ordered)
             primary_kernel<true, true><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl, octant_queue(c));
         else if (c->fast_slab)
             primary_kernel<true, false><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl, octant_queue(c));
@@ -2136,15 +2222,21 @@ try {
     HIP_TRY(hipMemcpy(c->d_pnodes, pn.data(), sizeof(PNode) * pn.size(), hipMemcpyHostToDevice));
     std::vector<HNode> hn;
     std::vector<HAux> hx;
-    std::vector<LeafRec> lr;
-    std::vector<uint32_t> src;
-    build_hnodes(nodes, nn, spheres, ns, hn, hx, lr, src);
+    std::vector<float4> lgeo;
+    std::vector<LeafBox> lbox;
+    build_hnodes(nodes, nn, spheres, ns, hn, hx, lgeo, lbox);
+    if (c->node_order == 1) order_hnodes(hn, hx, lgeo, lbox, kHCache);
+    const size_t nl = lbox.size();
+    const size_t box_off = (sizeof(float4) * nl + 255) & ~(size_t)255;
     HIP_TRY(hipMalloc((void**)&c->d_hnodes, sizeof(HNode) * hn.size()));
     HIP_TRY(hipMalloc((void**)&c->d_haux, sizeof(HAux) * hx.size()));
-    HIP_TRY(hipMalloc((void**)&c->d_leaves, sizeof(LeafRec) * std::max<size_t>(lr.size(), 1)));
+    HIP_TRY(hipMalloc((void**)&c->d_leaves, box_off + sizeof(LeafBox) * std::max<size_t>(nl, 1)));
     HIP_TRY(hipMemcpy(c->d_hnodes, hn.data(), sizeof(HNode) * hn.size(), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_haux, hx.data(), sizeof(HAux) * hx.size(), hipMemcpyHostToDevice));
-    if (!lr.empty()) HIP_TRY(hipMemcpy(c->d_leaves, lr.data(), sizeof(LeafRec) * lr.size(), hipMemcpyHostToDevice));
+    if (nl) {
+        HIP_TRY(hipMemcpy(c->d_leaves, lgeo.data(), sizeof(float4) * nl, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(c->d_leaves + box_off, lbox.data(), sizeof(LeafBox) * nl, hipMemcpyHostToDevice));
+    }
     // node depths (pre-order: the children of inner node i are i + 1 and the
     // left subtree's skip), clamped to 255 -- the overlay's colour key
     std::vector<uint8_t> ndepth((size_t)std::max(nn, 1), 0);
@@ -2159,7 +2251,8 @@ try {
     c->num_nodes = nn;
     c->num_spheres = ns;
     c->num_hnodes = (uint32_t)hn.size();
-    c->leaf_big = sizeof(HNode) * hn.size() + sizeof(LeafRec) * lr.size() > ((size_t)32 << 20);
+    c->leaf_box_off = box_off;
+    c->leaf_big = sizeof(HNode) * hn.size() + (sizeof(float4) + sizeof(LeafBox)) * nl > ((size_t)32 << 20);
     {
         const uint32_t r = hn[0].slot[0].ref;
         c->wide_root = (r != kPNone && !(r & kPLeaf)) ? r : 0u;
@@ -2934,6 +3027,14 @@ int mirt_set_option(mirt_ctx* c, int option, int value)
         if (value < 0 || value > 10000) break;
         c->debug_stall_ms = value;
         return MIRT_OK;
+    case MIRT_OPT_NODE_ORDER:
+        if (value < 0 || value > 1) break;
+        c->node_order = value;
+        return MIRT_OK;
+    case MIRT_OPT_PRIMARY_WALK:
+        if (value < 0 || value > 1) break;
+        c->primary_walk = value;
+        return MIRT_OK;
     case MIRT_OPT_QUEUE_ORDER:
         if (value < 0 || value > 2) break;
         c->queue_order = value;
@@ -2969,6 +3070,8 @@ int mirt_get_option(mirt_ctx* c, int option)
     if (option == MIRT_OPT_ZERO_COPY) return c->zero_copy;
     if (option == MIRT_OPT_QUEUE_ORDER) return c->queue_order;
     if (option == MIRT_OPT_DEBUG_STALL_MS) return c->debug_stall_ms;
+    if (option == MIRT_OPT_NODE_ORDER) return c->node_order;
+    if (option == MIRT_OPT_PRIMARY_WALK) return c->primary_walk;
     if (option == MIRT_OPT_LEAF_BATCH) return leaf_batch(c) ? 1 : 0;  // in effect for the uploaded scene
     set_error("mirt_get_option: bad option %d", option);
     return MIRT_E_INVALID;

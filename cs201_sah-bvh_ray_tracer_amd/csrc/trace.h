@@ -71,11 +71,14 @@ static_assert(sizeof(PNode) == 64, "ordered node is 64 B");
 // stored in fp16 rounded outward (a superset) and tested with a fast test
 // that passes when undecided -- entering an inner node too eagerly costs
 // work, never a result, because every leaf is still gated by its exact box.
-// A leaf slot's exact box and its sphere live in a LeafRec fetched when the
-// fp16 box passes. 64 B per node = the bytes of two fp32 boxes: divergent
+// A leaf slot's sphere and its exact box live in two arrays (structure of
+// arrays, round 6): the gate reads the 16-B sphere first and the 32-B box only
+// for a hit that could win, so the spheres the walks read are packed eight to
+// a 128-B line (a 48-B record per leaf held 2.7) and the hot part of a large
+// tree -- HNodes + spheres -- is two thirds of the bytes it was. 64 B per node = the bytes of two fp32 boxes: divergent
 // per-lane loads are bound by the bytes the texture path returns.
 // HNode 0 is a virtual node whose only slot is the root; slot references: an
-// inner HNode index, kPLeaf | LeafRec index, or kPNone. HAux holds the
+// inner HNode index, kPLeaf | leaf index, or kPNone. HAux holds the
 // node's flat DFS segment [flat + 1, end), read only when the stack is full.
 struct __attribute__((aligned(64))) HNode {
     struct Slot {
@@ -87,13 +90,12 @@ static_assert(sizeof(HNode) == 64, "wide node is 64 B");
 struct HAux {
     uint32_t flat, end;
 };
-struct __attribute__((aligned(16))) LeafRec {
+struct __attribute__((aligned(32))) LeafBox {
     float lo[3], hi[3];  // the leaf's exact box (bvh.c bounds)
     int32_t sphere;
     uint32_t pad;
-    float4 geo;          // the sphere: centre, radius
 };
-static_assert(sizeof(LeafRec) == 48, "leaf record is 48 B");
+static_assert(sizeof(LeafBox) == 32, "leaf box is 32 B");
 
 // Read-only scene in HBM (L2 / Infinity-Cache resident at the BASELINE sizes).
 struct DevScene {
@@ -116,7 +118,8 @@ struct DevScene {
     // four-wide per-lane walks (HNode): ordered trees whose boxes nest
     const HNode* hnodes;
     const HAux* haux;
-    const LeafRec* leaves;
+    const float4* leaf_geo;   // per leaf: its sphere (centre, radius)
+    const LeafBox* leaf_box;  // per leaf: its exact box and sphere index
     int wide;
     uint32_t num_hnodes;  // HNodes, numbered breadth-first: the first ones are the top levels
     // where a four-wide walk starts: the root's own HNode (1) -- HNode 0's
@@ -943,16 +946,17 @@ template <bool FAST, bool COUNT>
 __device__ __forceinline__ void wide_leaf(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
                                           uint32_t ref, float& best_t, int& best_s, Counters& cnt)
 {
-    const float4* lp = (const float4*)(sc.leaves + (ref & ~kPLeaf));
+    const uint32_t li = ref & ~kPLeaf;
+    const float4* lp = (const float4*)(sc.leaf_box + li);
     float e;
     if constexpr (COUNT) {
-        const float4 l0 = lp[0], l1 = lp[1], g = lp[2];
+        const float4 l0 = lp[0], l1 = lp[1], g = sc.leaf_geo[li];
         if (slab_box<FAST>(sr, pr, l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, e)) {
             cnt.spheres++;
             consider_sphere<FAST>(sc, sp, pr, sr.ox, sr.oy, sr.oz, __float_as_int(l1.z), g, best_t, best_s);
         }
     } else {
-        const float t = sphere_t<FAST>(sp, lp[2], best_t);
+        const float t = sphere_t<FAST>(sp, sc.leaf_geo[li], best_t);
         if (t > 0.0f) {
             const float4 l0 = lp[0], l1 = lp[1];
             const int si = __float_as_int(l1.z);
@@ -972,7 +976,7 @@ __device__ __forceinline__ void leaf_gate(const DevScene& sc, const SlabRay& sr,
 {
     const float t = sphere_t<true>(sp, g, best_t);
     if (t > 0.0f) {
-        const float4* lp = (const float4*)(sc.leaves + (ref & ~kPLeaf));
+        const float4* lp = (const float4*)(sc.leaf_box + (ref & ~kPLeaf));
         const float4 l0 = lp[0], l1 = lp[1];
         const int si = __float_as_int(l1.z);
         float e;
@@ -1081,10 +1085,10 @@ __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay
         // than the round trips they save
         if (__ballot(lm != 0)) {
             float4 g0, g1, g2, g3;
-            if (lm & 1) g0 = sc.leaves[q3.x & ~kPLeaf].geo;
-            if (lm & 2) g1 = sc.leaves[q3.y & ~kPLeaf].geo;
-            if (lm & 4) g2 = sc.leaves[q3.z & ~kPLeaf].geo;
-            if (lm & 8) g3 = sc.leaves[q3.w & ~kPLeaf].geo;
+            if (lm & 1) g0 = sc.leaf_geo[q3.x & ~kPLeaf];
+            if (lm & 2) g1 = sc.leaf_geo[q3.y & ~kPLeaf];
+            if (lm & 4) g2 = sc.leaf_geo[q3.z & ~kPLeaf];
+            if (lm & 8) g3 = sc.leaf_geo[q3.w & ~kPLeaf];
             if (lm & 1) leaf_gate(sc, sr, sp, pr, q3.x, g0, best_t, best_s);
             if (lm & 2) leaf_gate(sc, sr, sp, pr, q3.y, g1, best_t, best_s);
             if (lm & 4) leaf_gate(sc, sr, sp, pr, q3.z, g2, best_t, best_s);
@@ -1175,8 +1179,8 @@ __device__ __forceinline__ void quad_step(const DevScene& sc, const SlabRay& sr,
     float ct = INFINITY;
     int cs = -1;
     if (pass && (q.w & kPLeaf)) {  // sphere first, the exact box only for a hit (wide_leaf)
-        const float4* lp = (const float4*)(sc.leaves + (q.w & ~kPLeaf));
-        const float t = sphere_t<FAST>(sp, lp[2], best_t);
+        const float4* lp = (const float4*)(sc.leaf_box + (q.w & ~kPLeaf));
+        const float t = sphere_t<FAST>(sp, sc.leaf_geo[q.w & ~kPLeaf], best_t);
         if (t > 0.0f) {
             const float4 l0 = lp[0], l1 = lp[1];
             float ee;
@@ -1301,8 +1305,8 @@ __device__ __forceinline__ bool solo_step(const DevScene& sc, const SlabRay& sr,
         const bool pass = slab_cons(sr, pr, h_lo(q.x), h_lo(q.y), h_lo(q.z), h_hi(q.x), h_hi(q.y), h_hi(q.z), e) &
                           (q.w != kPNone);
         if (pass && (q.w & kPLeaf)) {  // sphere first, the exact box only for a hit (wide_leaf)
-            const float4* lp = (const float4*)(sc.leaves + (q.w & ~kPLeaf));
-            const float t = sphere_t<FAST>(sp, lp[2], best_t);
+            const float4* lp = (const float4*)(sc.leaf_box + (q.w & ~kPLeaf));
+            const float t = sphere_t<FAST>(sp, sc.leaf_geo[q.w & ~kPLeaf], best_t);
             if (t > 0.0f) {
                 const float4 l0 = lp[0], l1 = lp[1];
                 float ee;

@@ -424,10 +424,19 @@ enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3,
                                        mirt_render_frame (a frame alone on the chip), grouped by
                                        direction octant per workgroup for frames in flight;
                                        1 = always grouped; 2 = always tile order. Speed only. */
-       MIRT_OPT_DEBUG_STALL_MS = 19 /* test hook: every frame of this context starts behind a
+       MIRT_OPT_DEBUG_STALL_MS = 19, /* test hook: every frame of this context starts behind a
                                        kernel that waits this many ms (0..10000, default 0), then
                                        exits -- a frame that overruns a caller's deadline
-                                       (mirt_multi's MIRT_MULTI_OPT_TIMEOUT_MS) without a hang */ };
+                                       (mirt_multi's MIRT_MULTI_OPT_TIMEOUT_MS) without a hang */
+       MIRT_OPT_NODE_ORDER = 21,    /* layout of the four-wide tree built at the NEXT scene upload:
+                                       0 (default) = nodes numbered breadth first; 1 = the top levels
+                                       breadth first, then depth first with each node's children
+                                       contiguous, leaves renumbered to follow (locality of large
+                                       trees). Speed only: the walks' visits and results do not
+                                       change. */
+       MIRT_OPT_PRIMARY_WALK = 22   /* wavefront, ordered four-wide tree: camera rays walked as 8x8
+                                       packets (0, default) or each on its own, four-wide, like the
+                                       bounce rays (1). Speed only. */ };
 /* Traversal ids keep their first-release values (mirt 0.1: TILE 0, WAVEFRONT 5).
    ABI note: the mirt 0.2 header numbered WAVEFRONT 1; mirt_set_option accepts
    1 as a deprecated alias of MIRT_TRAV_WAVEFRONT (mirt_get_option reads back

@@ -2,6 +2,7 @@
 the golden 1080p depth-5 frame must match, then bench.py's device numbers.
 
     python scripts/ab_libs.py ab/libmirt_base.so ab/libmirt_x.so [--workload 1080p_10k] [--rounds 2]
+    python scripts/ab_libs.py ab/libmirt_x.so ab/libmirt_x.so@21=1 ...   (LIB@OPT=VAL[,OPT=VAL]: bench.py --opt)
 
 Each library runs in its own process (MIRT_LIB), rounds interleaved.
 """
@@ -33,7 +34,8 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     a = ap.parse_args()
     res = {lib: [] for lib in a.libs}
-    for lib in a.libs:
+    for spec in dict.fromkeys(x.split("@")[0] for x in a.libs):
+        lib = spec
         env = dict(os.environ, MIRT_LIB=os.path.abspath(lib))
         p = subprocess.run([sys.executable, "-c", CHECK % (ROOT, os.path.join(ROOT, "tests/golden/golden.json"))],
                            env=env, capture_output=True, text=True, timeout=300)
@@ -42,10 +44,12 @@ def main():
             sys.exit(p.returncode)
     for _ in range(a.rounds):
         for lib in a.libs:
-            env = dict(os.environ, MIRT_LIB=os.path.abspath(lib))
+            path, _, opts = lib.partition("@")
+            env = dict(os.environ, MIRT_LIB=os.path.abspath(path))
+            extra = [x for o in opts.split(",") if o for x in ("--opt", o)]
             p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu", "--no-host",
-                                "--workload", a.workload, "--steps", str(a.steps)], env=env, capture_output=True,
-                               text=True, timeout=600)
+                                "--workload", a.workload, "--steps", str(a.steps)] + extra, env=env,
+                               capture_output=True, text=True, timeout=600)
             if p.returncode:
                 print(lib, "bench failed", p.stderr[-1000:])
                 sys.exit(p.returncode)

@@ -37,9 +37,12 @@ def main():
     ap.add_argument("--delivery", default="gather", choices=("gather", "host-direct"))
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--rounds", type=int, default=2, help="repeat every shard's measurement (its best round counts)")
+    ap.add_argument("--rounds", type=int, default=5,
+                    help="measure every shard this many times, rounds interleaved across the shards")
+    ap.add_argument("--ranks", default="", help="only these shards (comma list; default every shard)")
     ap.add_argument("--pipeline", type=int, default=0)
     ap.add_argument("--batch", type=int, default=0)
+    ap.add_argument("--ramp", type=int, default=0, help="the timed region's first RAMP launches carry one frame each")
     ap.add_argument("--tail-grid", type=int, default=-1)
     ap.add_argument("--bounce-blocks", type=int, default=-1)
     ap.add_argument("--accumulate", action="store_true")
@@ -71,31 +74,40 @@ def main():
         m.set_option(mirt.abi.MULTI_OPT_DIRECT_COPY, a.direct_copy)
         bufs = bench.host_bufs(m.lanes, per)
         bench.prime(m, cam, bufs, per)
-        timed = bench.plan(a.warmup, a.steps, per)
+        timed = bench.plan(a.warmup, a.steps, per, a.ramp)
         tail = bench.tail_of(timed, tail_n, lanes, blocks)
-        per_rank, enq = [], []
-        for k in range(world):
-            m.emulate(world, k)
-            best = None
-            for _ in range(a.rounds):
+        ranks = [int(k) for k in a.ranks.split(",")] if a.ranks else list(range(world))
+        runs, enq = {k: [] for k in ranks}, []
+        for _ in range(a.rounds):          # rounds interleaved across the shards
+            for k in ranks:
+                m.emulate(world, k)
                 el = bench.timed_loop(m, cam, bench.plan(0, a.warmup, per), timed, bufs, bench.DEPTH, a.accumulate,
                                       tail, device_only=a.device_only)
-                best = el if best is None else min(best, el)
+                runs[k].append(el)
                 enq += bench.ENQUEUE
-            per_rank.append(best)
+        st = m.stats()
         m.close()
         bench.close_bufs(bufs)
+        med = {k: sorted(v)[len(v) // 2] for k, v in runs.items()}
+        per_rank = [med[k] for k in ranks]
         slow = max(per_rank)
+        best_slow = max(min(v) for v in runs.values())
         print(json.dumps({
             "workload": a.workload, "delivery": "device-only" if a.device_only else a.delivery,
             "direct_copy": a.direct_copy, "world": world, "steps": a.steps, "warmup": a.warmup,
-            "lanes": lanes, "queue_ahead": ahead, "row_block": a.row_block, "frames_per_launch": per, "tail_grid": len(tail),
+            "lanes": lanes, "queue_ahead": ahead, "row_block": a.row_block, "frames_per_launch": per, "ramp": a.ramp, "tail_grid": len(tail),
             "bounce_blocks": blocks,
             "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+            "ranks": ranks, "rounds": a.rounds,
             "rank_ms_per_frame": [round(t / a.steps * 1e3, 4) for t in per_rank],
-            "slowest_rank": per_rank.index(slow),
+            "rank_ms_per_frame_runs": {k: [round(t / a.steps * 1e3, 4) for t in v] for k, v in runs.items()},
+            "slowest_rank": ranks[per_rank.index(slow)],
             "enqueue_ms_per_launch_median": round(sorted(enq)[len(enq) // 2] * 1e3, 4) if enq else None,
-            "pred_job_mrays_s": round(W * H * SPP * a.steps / slow / 1e6, 1)}), flush=True)
+            "estimator": "N x the slowest shard's MEDIAN over the rounds (pred_job_mrays_s); "
+                         "pred_job_mrays_s_best: the slowest shard's best round",
+            "pred_job_mrays_s": round(W * H * SPP * a.steps / slow / 1e6, 1),
+            "pred_job_mrays_s_best": round(W * H * SPP * a.steps / best_slow / 1e6, 1),
+            "rccl": {k: st[k] for k in ("comm_inits", "rccl_sends", "rccl_recvs")}}), flush=True)
     return 0
 
 
