@@ -688,7 +688,7 @@ def devices_for(n):
 def open_multi(n, lanes, host_direct, spheres, bvh, blocks, opts, timeout_ms=120000, ahead=False):
     m = mirt.MultiRenderer(devices_for(n), lanes=lanes, host_direct=host_direct, queue_ahead=ahead)
     m.set_option(mirt.abi.MULTI_OPT_TIMEOUT_MS, timeout_ms)
-    for ov in opts:   # before the upload: some options (MIRT_OPT_NODE_ORDER) shape the scene's layout
+    for ov in opts:   # before the upload (an option may shape the layout the upload builds)
         o, v = (int(t) for t in ov.split("="))
         m.set_option(o, v)
     m.upload(spheres, bvh)

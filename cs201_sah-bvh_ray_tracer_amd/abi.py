@@ -76,7 +76,7 @@ class FrameDesc(C.Structure):
                 ("use_bvh", C.c_int32), ("seed", C.c_uint64), ("sample", C.c_uint32),
                 ("accumulate", C.c_int32), ("frames", C.c_int32), ("row_block", C.c_int32),
                 ("shard", C.c_int32), ("num_shards", C.c_int32), ("samples", C.c_int32),
-                ("jitter", C.c_int32)]
+                ("jitter", C.c_int32), ("lead_skip", C.c_int32)]
 
 
 class Counts(C.Structure):
@@ -205,10 +205,10 @@ SIGNATURES = [
 OPT_TRAVERSAL, OPT_FAST_SLAB, OPT_BLOCK_WAVES, OPT_DEFER, OPT_BOUNCE_THRESHOLD, OPT_PRUNE, OPT_ORDERED = (
     1, 2, 3, 4, 5, 6, 7)
 OPT_BOUNCE_BLOCKS, OPT_QUAD_DRAIN, OPT_LEAF_BATCH, OPT_QUAD_BATCH, OPT_ZERO_COPY = 9, 11, 14, 15, 17
-OPT_QUEUE_ORDER, OPT_DEBUG_STALL_MS, OPT_NODE_ORDER, OPT_PRIMARY_WALK = 18, 19, 21, 22
+OPT_QUEUE_ORDER, OPT_DEBUG_STALL_MS = 18, 19
 TRAV_TILE, TRAV_WAVEFRONT = 0, 5
 MULTI_COPY, MULTI_HOST_DIRECT, MULTI_QUEUE_AHEAD = 1, 2, 4
 MULTI_FULL_GRID = 1
 MULTI_OPT_TIMEOUT_MS, MULTI_OPT_EMULATE_WORLD, MULTI_OPT_EMULATE_RANK, MULTI_OPT_DIRECT_COPY = 256, 257, 258, 259
 MULTI_OPT_COPY_STREAM = 260
-MULTI_OPT_GATHER_SELF = 261
+MULTI_OPT_GATHER_SELF, MULTI_OPT_LEAD_SKIP = 261, 262

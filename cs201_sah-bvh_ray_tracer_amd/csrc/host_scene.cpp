@@ -7,7 +7,10 @@
 #include <cstdint>
 #include <cstring>
 
+#include <algorithm>
+
 #include "internal.h"
+#include "shard.h"
 
 static_assert(sizeof(mirt_vec3) == 12, "Vec3 is 12 B (vec3.h:3-7)");
 static_assert(sizeof(mirt_sphere) == 20, "Sphere is 20 B (sphere.h:7-11)");
@@ -42,20 +45,20 @@ bool frame_desc_valid(const mirt_frame_desc* fd)
     if (fd->row_block <= 0 || fd->num_shards <= 0 || fd->shard < 0 || fd->shard >= fd->num_shards) return false;
     if (fd->accumulate && fd->frames <= 0) return false;
     if (fd->samples < 0 || fd->samples > 64) return false;
+    if (fd->lead_skip < 0 || fd->lead_skip >= kLeadRounds || (fd->lead_skip > 0 && fd->num_shards < 2)) return false;
     const int64_t samples = fd->samples > 1 ? fd->samples : 1;
     return (int64_t)fd->width * fd->height * samples <= (int64_t)1 << 31;
 }
 
 int shard_row_count(const mirt_frame_desc* fd)
 {
-    const int rb = fd->row_block, g = fd->num_shards;
+    const int rb = fd->row_block, n = fd->num_shards, d = fd->lead_skip;
     const int blocks = (fd->height + rb - 1) / rb;
-    int rows = 0;
-    for (int b = fd->shard; b < blocks; b += g) {
-        const int y0 = b * rb;
-        rows += (fd->height - y0 < rb) ? fd->height - y0 : rb;
-    }
-    return rows;
+    const int c = shard_block_count(fd->shard, blocks, n, d);
+    if (c == 0) return 0;
+    // every block is full but the image's last one, if it is this shard's
+    const int last = shard_block(fd->shard, c - 1, n, d);
+    return (c - 1) * rb + std::min(rb, fd->height - last * rb);
 }
 
 }  // namespace mirt
@@ -214,10 +217,9 @@ int mirt_shard_rows(const mirt_frame_desc* fd, int32_t* rows)
     }
     const int n = mirt::shard_row_count(fd);
     if (rows) {
-        const int rb = fd->row_block, g = fd->num_shards;
-        int k = 0;
-        for (int b = fd->shard; b * rb < fd->height; b += g)
-            for (int y = b * rb; y < (b + 1) * rb && y < fd->height; y++) rows[k++] = y;
+        const int rb = fd->row_block;
+        for (int r = 0; r < n; r++)
+            rows[r] = mirt::shard_block(fd->shard, r / rb, fd->num_shards, fd->lead_skip) * rb + r % rb;
     }
     return n;
 }

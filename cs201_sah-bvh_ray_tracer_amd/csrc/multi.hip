@@ -32,6 +32,7 @@
 
 #include "../../include/mirt_multi.h"
 #include "internal.h"
+#include "shard.h"
 
 using namespace mirt;
 
@@ -55,36 +56,36 @@ struct ShardSrc {
 };
 
 // The shards' slabs -> the row-major frames. Image row y lies in row block
-// b = y / rb, which shard b % n rendered as its compact row (b / n) * rb +
-// y % rb (host_scene.cpp shard_row_count's geometry). One thread per pixel,
-// rows across blockIdx.y, frames across blockIdx.z: both sides are coalesced
-// row segments.
+// b = y / rb, which its owner shard s rendered as compact row c * rb + y % rb
+// (shard.h block_owner: b % n, or the lead-skip weighting). One thread per
+// pixel, rows across blockIdx.y, frames across blockIdx.z: both sides are
+// coalesced row segments.
 __global__ void __launch_bounds__(256) deinterleave_kernel(ShardSrc src, uint32_t* __restrict__ frames, int width,
-                                                           int height, int rb, int n)
+                                                           int height, int rb, int n, int lead_skip)
 {
     const int x = blockIdx.x * 256 + threadIdx.x;
     const int y = blockIdx.y;
     const int j = blockIdx.z;
     if (x >= width || y >= height) return;
-    const int b = y / rb;
-    const int s = b % n;
-    const size_t row = (size_t)(b / n) * rb + y % rb;
+    int s, c;
+    block_owner(y / rb, n, lead_skip, s, c);
+    const size_t row = (size_t)c * rb + y % rb;
     frames[((size_t)j * height + y) * width + x] = src.p[s][((size_t)j * src.rows[s] + row) * width + x];
 }
 
 // MIRT_MULTI_OPT_DIRECT_COPY 2: shard s's compact rows straight into the
 // row-major host frame (device-visible address of page-locked memory) by a
 // kernel, 16 B per thread, instead of a strided DMA: compact row r is image
-// row (r / rb * world + s) * rb + r % rb (host_scene.cpp shard_row_count's
-// geometry; the image's short last block lies at the slab's end).
+// row shard_block(s, r / rb) * rb + r % rb (shard.h; the image's short last
+// block lies at the slab's end).
 __global__ void __launch_bounds__(256) scatter_rows_kernel(const uint32_t* __restrict__ slab,
                                                            uint32_t* __restrict__ frame, int width, int rows,
-                                                           int rb, int world, int s)
+                                                           int rb, int world, int s, int lead_skip)
 {
     const int r = blockIdx.y;
     const int x = (int)(blockIdx.x * 256 + threadIdx.x) * 4;
     if (r >= rows || x >= width) return;
-    const int y = (r / rb * world + s) * rb + r % rb;
+    const int y = shard_block(s, r / rb, world, lead_skip) * rb + r % rb;
     const uint32_t* src = slab + (size_t)r * width + x;
     uint32_t* dst = frame + (size_t)y * width + x;
     if (x + 4 <= width && (((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
@@ -218,6 +219,7 @@ struct mirt_multi {
     int timeout_ms = 60000;           // MIRT_MULTI_OPT_TIMEOUT_MS (0: unbounded)
     int emu_world = 0, emu_rank = 0;  // MIRT_MULTI_OPT_EMULATE_*: this one rank plays shard emu_rank of emu_world
     int direct_copy = 0;              // MIRT_MULTI_OPT_DIRECT_COPY: 0 one strided copy per frame, 1 one per row block
+    int lead_skip = 0;                // MIRT_MULTI_OPT_LEAD_SKIP: shard 0's lighter share (shard.h)
     bool gather_self = false;         // MIRT_MULTI_OPT_GATHER_SELF: rank 0's own slabs travel through the gather too
     int last_lane = -1;               // lane of the last launch enqueued
     // a wait timed out or a device call failed: every call returns fail_msg;
@@ -404,14 +406,17 @@ int prepare(mirt_multi* m, Lane& L, const mirt_camera* cam, const mirt_frame_des
     J.sd.row_block = fd->row_block > 0 ? fd->row_block : 8;
     J.sd.num_shards = J.world;
     J.sd.samples = spp * nframes;
+    J.sd.lead_skip = J.world > 1 ? m->lead_skip : 0;
     J.rb = J.sd.row_block;
     J.sr = ShardSrc{};
     mirt_frame_desc g = J.sd;
+    int most = 0;
     for (int s = 0; s < J.world; s++) {
         g.shard = s;
         J.sr.rows[s] = shard_row_count(&g);
+        most = std::max(most, J.sr.rows[s]);
     }
-    J.shard_stride = (size_t)J.sr.rows[0] * J.W * nframes;   // shard 0 holds the most rows
+    J.shard_stride = (size_t)most * J.W * nframes;   // every shard's slot in the gather buffer
     J.frame_elems = (size_t)J.W * J.H;
     J.gather = !m->direct;                                     // frames to device 0
     J.rank0_assembles = J.gather && (!J.emu || m->emu_rank == 0);
@@ -608,7 +613,7 @@ int issue_rank_body(mirt_multi* m, Lane& L, int r)
                 const uint32_t* frames = self ? L.gathered + (size_t)s * J.shard_stride : src;
                 if (J.world > 1) {
                     const dim3 grid((J.W + 255) / 256, J.H, J.nframes);
-                    deinterleave_kernel<<<grid, 256, 0, st>>>(sr, L.frame, J.W, J.H, J.rb, J.world);
+                    deinterleave_kernel<<<grid, 256, 0, st>>>(sr, L.frame, J.W, J.H, J.rb, J.world, J.sd.lead_skip);
                     MHIP(hipGetLastError());
                     frames = L.frame;
                 }
@@ -622,15 +627,22 @@ int issue_rank_body(mirt_multi* m, Lane& L, int r)
         }
     } else if (J.deliver) {
         // host-direct: this rank's row blocks of frame j straight into its
-        // host frame: its full blocks b = s, s + world, ... as one strided
-        // copy (rows of rb * W pixels, the destination pitch world * rb
-        // rows), the image's short last block (if it is this shard's) after it
-        const int W = J.W, H = J.H, rb = J.rb, world = J.world;
+        // host frame as strided copies (rows of rb * W pixels): with plain
+        // interleaving (lead_skip 0) its full blocks b = s, s + world, ... are
+        // ONE copy (destination pitch world * rb rows); with the lead-skip
+        // weighting one copy per position k of a period (destination pitch
+        // P * rb rows, source pitch w * rb rows); the image's short last block
+        // (if it is this shard's) after them
+        const int W = J.W, H = J.H, rb = J.rb, world = J.world, d = J.sd.lead_skip;
         const int blocks = (H + rb - 1) / rb;
         const int last = blocks - 1;
-        const int nb = s < blocks ? (last - s) / world + 1 : 0;     // this shard's blocks
-        const bool has_short = H % rb != 0 && nb > 0 && last % world == s;
+        const int nb = shard_block_count(s, blocks, world, d);     // this shard's blocks
+        int owner_last = 0, c_last = 0;
+        block_owner(last, world, d, owner_last, c_last);
+        const bool has_short = H % rb != 0 && owner_last == s;
         const int nfull = nb - (has_short ? 1 : 0);
+        const int P = shard_period(world, d), w = shard_period_blocks(s, d);
+        const int last_full = H % rb != 0 ? last - 1 : last;        // the image's last full block
         st = copy_stream(m, L, r);   // the copies (with QUEUE_AHEAD on the lane's copy stream)
         for (int j = 0; j < J.nframes; j++) {
             const uint32_t* sj = src + (size_t)j * elems;
@@ -643,22 +655,34 @@ int issue_rank_body(mirt_multi* m, Lane& L, int r)
                     return MIRT_E_INVALID;
                 }
                 const dim3 grid((unsigned)((W + 1023) / 1024), (unsigned)J.sr.rows[s]);
-                scatter_rows_kernel<<<grid, 256, 0, st>>>(sj, dd, W, J.sr.rows[s], rb, world, s);
+                scatter_rows_kernel<<<grid, 256, 0, st>>>(sj, dd, W, J.sr.rows[s], rb, world, s, d);
                 MHIP(hipGetLastError());
                 continue;
             }
-            if (nfull > 0 && m->direct_copy == 0)
-                MHIP(hipMemcpy2DAsync(dj + (size_t)s * rb * W, (size_t)world * rb * W * 4, sj, (size_t)rb * W * 4,
-                                      (size_t)rb * W * 4, nfull, hipMemcpyDeviceToHost, st));
-            for (int i = 0; m->direct_copy == 1 && i < nfull; i++)   // one copy per row block
-                MHIP(hipMemcpyAsync(dj + ((size_t)i * world + s) * rb * W, sj + (size_t)i * rb * W,
-                                    (size_t)rb * W * 4, hipMemcpyDeviceToHost, st));
+            if (m->direct_copy == 1) {   // one copy per row block
+                for (int i = 0; i < nfull; i++)
+                    MHIP(hipMemcpyAsync(dj + (size_t)shard_block(s, i, world, d) * rb * W, sj + (size_t)i * rb * W,
+                                        (size_t)rb * W * 4, hipMemcpyDeviceToHost, st));
+            } else if (d == 0) {
+                if (nfull > 0)
+                    MHIP(hipMemcpy2DAsync(dj + (size_t)s * rb * W, (size_t)world * rb * W * 4, sj, (size_t)rb * W * 4,
+                                          (size_t)rb * W * 4, nfull, hipMemcpyDeviceToHost, st));
+            } else {
+                for (int k = 0; k < w; k++) {
+                    const int pos = shard_block_pos(s, k, world, d);
+                    const int cnt = last_full >= pos ? (last_full - pos) / P + 1 : 0;   // full blocks at pos
+                    if (cnt > 0)
+                        MHIP(hipMemcpy2DAsync(dj + (size_t)pos * rb * W, (size_t)P * rb * W * 4,
+                                              sj + (size_t)k * rb * W, (size_t)w * rb * W * 4, (size_t)rb * W * 4,
+                                              cnt, hipMemcpyDeviceToHost, st));
+                }
+            }
             // the short block as a one-row 2D copy too: a 1D copy after the strided one on the
             // same stream cost a rank ~0.5 ms per frame (N = 2, 16-row blocks: profiles/r05_logs/r05at/),
             // the runtime moving between its copy paths
             if (has_short) {
                 const size_t sb = (size_t)(H - last * rb) * W * 4;
-                MHIP(hipMemcpy2DAsync(dj + (size_t)last * rb * W, sb, sj + (size_t)nfull * rb * W, sb, sb, 1,
+                MHIP(hipMemcpy2DAsync(dj + (size_t)last * rb * W, sb, sj + (size_t)c_last * rb * W, sb, sb, 1,
                                       hipMemcpyDeviceToHost, st));
             }
         }
@@ -746,8 +770,9 @@ int check_frame(const mirt_multi* m, const mirt_camera* cam, const mirt_frame_de
                 mirt_rgba8* const* outs, const char* fn)
 {
     if (!cam || !fd || fd->shard != 0 || fd->num_shards > 1 || fd->num_shards < 0 || fd->row_block < 0 ||
-        nframes < 1) {
-        set_error("%s: invalid arguments (fd describes the whole frame: shard 0, num_shards 0 or 1)", fn);
+        fd->lead_skip != 0 || nframes < 1) {
+        set_error("%s: invalid arguments (fd describes the whole frame: shard 0, num_shards 0 or 1, lead_skip 0 "
+                  "-- the weighting is MIRT_MULTI_OPT_LEAD_SKIP)", fn);
         return MIRT_E_INVALID;
     }
     if (nframes > 1 && fd->samples > 1) {
@@ -764,6 +789,7 @@ int check_frame(const mirt_multi* m, const mirt_camera* cam, const mirt_frame_de
     whole.num_shards = m->emu_world > 1 ? m->emu_world : m->n;
     whole.row_block = fd->row_block > 0 ? fd->row_block : 8;
     whole.samples = std::max(1, fd->samples) * nframes;
+    whole.lead_skip = whole.num_shards > 1 ? m->lead_skip : 0;
     if (!frame_desc_valid(&whole) || whole.num_shards > kMaxShards) {
         set_error("%s: invalid frame descriptor (or more than 64 frames / samples per launch)", fn);
         return MIRT_E_INVALID;
@@ -994,6 +1020,10 @@ int mirt_multi_set_option(mirt_multi* m, int option, int value)
         if (value < 0 || value > 1) break;
         m->gather_self = value == 1;
         return MIRT_OK;
+    case MIRT_MULTI_OPT_LEAD_SKIP:
+        if (value < 0 || value >= kLeadRounds) break;
+        m->lead_skip = value;
+        return MIRT_OK;
     default:
         for (Lane& L : m->lanes)
             if (L.owns_ctx)
@@ -1014,6 +1044,7 @@ int mirt_multi_get_option(mirt_multi* m, int option)
     if (option == MIRT_MULTI_OPT_DIRECT_COPY) return m->direct_copy;
     if (option == MIRT_MULTI_OPT_COPY_STREAM) return m->ahead_copy_stream;
     if (option == MIRT_MULTI_OPT_GATHER_SELF) return m->gather_self ? 1 : 0;
+    if (option == MIRT_MULTI_OPT_LEAD_SKIP) return m->lead_skip;
     return mirt_get_option(m->lanes[0].ctx[0], option);
 }
 

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "internal.h"
+#include "shard.h"
 #include "trace.h"
 
 using namespace mirt;
@@ -36,7 +37,7 @@ struct FrameConst {
     uint32_t sample;
     int accumulate;
     float frames;
-    int row_block, shard, num_shards;
+    int row_block, shard, num_shards, lead_skip;
     int jitter;        // sub-pixel jitter of camera rays from the RNG contract (camera_ray)
     int num_rows;      // rows of this launch: shard_rows x samples (frame j's rows follow frame j-1's)
     int shard_rows;    // rows of one frame of this shard
@@ -69,6 +70,7 @@ FrameConst make_frame_const(const mirt_camera* cam, const mirt_frame_desc* fd)
     f.row_block = fd->row_block;
     f.shard = fd->shard;
     f.num_shards = fd->num_shards;
+    f.lead_skip = fd->lead_skip;
     f.shard_rows = shard_row_count(fd);
     f.samples = fd->samples > 1 ? fd->samples : 1;
     f.jitter = fd->jitter != 0;
@@ -81,7 +83,7 @@ __device__ __forceinline__ int shard_row_to_y(const FrameConst& f, int r)
 {
     if (f.samples > 1) r %= f.shard_rows;
     const int blk = r / f.row_block;
-    return (blk * f.num_shards + f.shard) * f.row_block + (r - blk * f.row_block);
+    return shard_block(f.shard, blk, f.num_shards, f.lead_skip) * f.row_block + (r - blk * f.row_block);
 }
 
 // RNG contract sample of launch row r (one sample per frame).
@@ -344,13 +346,7 @@ struct BounceRec {
 // ORD: the tree admits the ordered packet walk (DevScene::ordered), which
 // also takes zero-component rays -- that build has no deferred waves and no
 // other walk, so it keeps the register budget of the packet walk alone.
-// LANE (MIRT_OPT_PRIMARY_WALK 1, ordered four-wide trees only): each camera ray
-// walks the four-wide tree on its own (the bounce kernel's walk, an LDS stack
-// column per lane) instead of in its wave's packet -- for deep trees, where
-// an 8x8 tile's rays part ways early and a packet step tests every lane
-// against nodes that few of them reach. The same closest hit (least t, a
-// tie to the larger sphere index), so the same frame.
-template <bool FAST, bool ORD, bool LANE = false>
+template <bool FAST, bool ORD>
 // Register budget of the ordered camera-packet kernel (ORD): 8 waves per SIMD (64 VGPRs, no
 // scratch; 67 and 7 waves without the attribute). With four frames in flight
 // its waves share the CUs with the bounce passes, and the eighth wave hides
@@ -365,15 +361,13 @@ template <bool FAST, bool ORD, bool LANE = false>
 // (Round 3: the ordered kernel groups each workgroup's first bounces by
 // direction octant in the queue -- scripts/tree_quality.cpp's lockstep model:
 // distinct nodes per lane-step -9%, busy lanes per step +13%; measured +1.8%.)
-#define MIRT_PRIMARY_ATTR __attribute__((amdgpu_waves_per_eu(LANE ? MIRT_BOUNCE_WAVES : ORD ? MIRT_PRIMARY_WAVES : 1)))
+#define MIRT_PRIMARY_ATTR __attribute__((amdgpu_waves_per_eu(ORD ? MIRT_PRIMARY_WAVES : 1)))
 __global__ __launch_bounds__(256) MIRT_PRIMARY_ATTR void primary_kernel(DevScene sc, FrameConst f, uint32_t* __restrict__ out,
                                                       float* __restrict__ acc, Deferred dfr,
                                                       BounceRec* __restrict__ queue, uint32_t* __restrict__ qctl,
                                                       int octants = 1)
 {
-    static_assert(!LANE || ORD, "the per-lane camera walk needs the ordered four-wide tree");
     __shared__ uint32_t cstack[ORD ? 1 : kMaxDepth * 256];
-    __shared__ uint32_t wstack[LANE ? kWideStack * kWideStride : 1];
     Counters cnt{0, 0, 0, 0, 0};
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
@@ -422,9 +416,7 @@ __global__ __launch_bounds__(256) MIRT_PRIMARY_ATTR void primary_kernel(DevScene
     if (!ORD && dfr.blocks > 0 && alive && slab_ray(ray).generic) alive = false;  // traced by a deferred wave
     float t;
     int s;
-    if constexpr (LANE) {
-        closest_hit<false, FAST, false>(sc, ray, alive, t, s, cnt, wstack + threadIdx.x);
-    } else if constexpr (ORD) {
+    if constexpr (ORD) {
         closest_packet_ordered<FAST, false>(sc, ray, alive, t, s, cnt);
     } else
         closest_hit<true, FAST, false>(sc, ray, alive, t, s, cnt);
@@ -1351,8 +1343,6 @@ struct mirt_ctx {
     size_t queue_cap = 0;
     bool lone_frame = false;    // mirt_render_frame's frame: the first bounces queued in tile order
     int queue_order = 0;        // MIRT_OPT_QUEUE_ORDER: 0 auto (tile order for lone_frame), 1 octants, 2 tile order
-    int node_order = 0;         // MIRT_OPT_NODE_ORDER: HNode numbering at the next upload (order_hnodes)
-    int primary_walk = 0;       // MIRT_OPT_PRIMARY_WALK: camera rays as packets (0) or per lane, four-wide (1)
     uint32_t* d_defer = nullptr;  // [count, list...]
     size_t defer_cap = 0;
     unsigned long long* d_keys = nullptr;  // chunked brute force: per-ray (t, index) keys
@@ -1663,73 +1653,6 @@ void build_hnodes(const mirt_node* nd, int nn, const mirt_sphere* sp, int ns, st
     }
 }
 
-// MIRT_OPT_NODE_ORDER 1: renumber the HNodes (and the leaves) for locality
-// of the walks' accesses: the first `keep` HNodes (the top levels every walk
-// starts in, staged in LDS by the bounce kernel) keep their breadth-first
-// numbers; below them the tree is laid out depth first with every node's
-// inner children as one contiguous group (siblings share lines, as
-// breadth-first order gives, and a subtree's nodes -- what one ray's walk
-// below that level touches -- lie together instead of spread over every
-// level of the whole tree). Each HNode's leaves are renumbered in the new
-// node order, so a subtree's spheres lie together too. Only the numbering
-// changes: every visit, test and tie is the same.
-void order_hnodes(std::vector<HNode>& hn, std::vector<HAux>& aux, std::vector<float4>& lgeo,
-                  std::vector<LeafBox>& lbox, size_t keep)
-{
-    const size_t nh = hn.size();
-    keep = std::min(keep, nh);
-    std::vector<uint32_t> nid(nh, kPNone), order;
-    order.reserve(nh);
-    auto emit = [&](uint32_t h) {
-        nid[h] = (uint32_t)order.size();
-        order.push_back(h);
-    };
-    for (size_t h = 0; h < keep; h++) emit((uint32_t)h);
-    std::vector<uint32_t> stack;
-    for (size_t h = keep; h-- > 0;) stack.push_back((uint32_t)h);
-    while (!stack.empty()) {
-        const uint32_t h = stack.back();
-        stack.pop_back();
-        uint32_t kids[4];
-        int nk = 0;
-        for (int k = 0; k < 4; k++) {
-            const uint32_t r = hn[h].slot[k].ref;
-            if (r != kPNone && !(r & kPLeaf) && r < nh && nid[r] == kPNone) kids[nk++] = r;
-        }
-        for (int k = 0; k < nk; k++) emit(kids[k]);
-        for (int k = nk; k-- > 0;) stack.push_back(kids[k]);
-    }
-    for (size_t h = 0; h < nh; h++)   // unreachable nodes (none in a built tree) keep a slot
-        if (nid[h] == kPNone) emit((uint32_t)h);
-    std::vector<HNode> h2(nh);
-    std::vector<HAux> a2(nh);
-    std::vector<float4> g2;
-    std::vector<LeafBox> b2;
-    g2.reserve(lgeo.size());
-    b2.reserve(lbox.size());
-    for (size_t i = 0; i < nh; i++) {
-        HNode n = hn[order[i]];
-        for (int k = 0; k < 4; k++) {
-            uint32_t& r = n.slot[k].ref;
-            if (r == kPNone) continue;
-            if (r & kPLeaf) {
-                const uint32_t l = r & ~kPLeaf;
-                r = kPLeaf | (uint32_t)b2.size();
-                g2.push_back(lgeo[l]);
-                b2.push_back(lbox[l]);
-            } else {
-                r = nid[r];
-            }
-        }
-        h2[i] = n;
-        a2[i] = aux[order[i]];
-    }
-    hn.swap(h2);
-    aux.swap(a2);
-    lgeo.swap(g2);
-    lbox.swap(b2);
-}
-
 // MIRT_OPT_LEAF_BATCH: the bounce walk loads a step's passing leaf spheres
 // together (bounce_kernel WALK 4) -- by default when the four-wide tree is
 // larger than the chip's L2 (32 MiB over the 8 XCDs), where the leaf loads
@@ -1982,10 +1905,7 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
         BounceRec* queue = (BounceRec*)((char*)c->d_queue + kQCtlBytes);
         const int ptiles = f.samples >= 4 ? ((f.width + 3) / 4) * ((f.shard_rows + 3) / 4) * ((f.samples + 3) / 4)
                                           : tiles;
-        if (c->primary_walk == 1 && sc.wide)
-            primary_kernel<true, true, true><<<(ptiles + 3) / 4, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
-        else
-            primary_kernel<true, true><<<(ptiles + 3) / 4, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
+        primary_kernel<true, true><<<(ptiles + 3) / 4, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
         HIP_TRY(hipGetLastError());
         if (int rc2 = fold()) return rc2;
         if (timed) HIP_TRY(hipEventRecord(c->ev1, s));
@@ -2006,10 +1926,7 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
         const int pblocks = (ptiles + 3) / 4 + dfr.blocks;
         const int bblocks = c->bounce_blocks_opt ? c->bounce_blocks_opt : c->bounce_blocks;
         const size_t blds = bounce_lds_bytes(f.depth);
-        if (c->fast_slab && sc.ordered && sc.wide && c->primary_walk == 1)
-            primary_kernel<true, true, true><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl,
-                                                                   octant_queue(c));
-        else if (c->fast_slab && sc.ordered)
+        if (c->fast_slab && sc.ordered)
             primary_kernel<true, true><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl, octant_queue(c));
         else if (c->fast_slab)
             primary_kernel<true, false><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl, octant_queue(c));
@@ -2225,7 +2142,6 @@ try {
     std::vector<float4> lgeo;
     std::vector<LeafBox> lbox;
     build_hnodes(nodes, nn, spheres, ns, hn, hx, lgeo, lbox);
-    if (c->node_order == 1) order_hnodes(hn, hx, lgeo, lbox, kHCache);
     const size_t nl = lbox.size();
     const size_t box_off = (sizeof(float4) * nl + 255) & ~(size_t)255;
     HIP_TRY(hipMalloc((void**)&c->d_hnodes, sizeof(HNode) * hn.size()));
@@ -3027,14 +2943,6 @@ int mirt_set_option(mirt_ctx* c, int option, int value)
         if (value < 0 || value > 10000) break;
         c->debug_stall_ms = value;
         return MIRT_OK;
-    case MIRT_OPT_NODE_ORDER:
-        if (value < 0 || value > 1) break;
-        c->node_order = value;
-        return MIRT_OK;
-    case MIRT_OPT_PRIMARY_WALK:
-        if (value < 0 || value > 1) break;
-        c->primary_walk = value;
-        return MIRT_OK;
     case MIRT_OPT_QUEUE_ORDER:
         if (value < 0 || value > 2) break;
         c->queue_order = value;
@@ -3070,8 +2978,6 @@ int mirt_get_option(mirt_ctx* c, int option)
     if (option == MIRT_OPT_ZERO_COPY) return c->zero_copy;
     if (option == MIRT_OPT_QUEUE_ORDER) return c->queue_order;
     if (option == MIRT_OPT_DEBUG_STALL_MS) return c->debug_stall_ms;
-    if (option == MIRT_OPT_NODE_ORDER) return c->node_order;
-    if (option == MIRT_OPT_PRIMARY_WALK) return c->primary_walk;
     if (option == MIRT_OPT_LEAF_BATCH) return leaf_batch(c) ? 1 : 0;  // in effect for the uploaded scene
     set_error("mirt_get_option: bad option %d", option);
     return MIRT_E_INVALID;

@@ -11,7 +11,8 @@
 #pragma once
 #include <cstdint>
 
-#if defined(__HIPCC__)
+#if defined(__HIP__)
+#include <hip/hip_runtime.h>
 #define MIRT_HD __host__ __device__ __forceinline__
 #else
 #define MIRT_HD inline

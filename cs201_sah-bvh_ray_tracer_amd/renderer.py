@@ -158,13 +158,14 @@ def flatten_bvh(root, spheres):
 
 
 def frame_desc(width, height, depth=5, use_bvh=True, seed=1, sample=0, accumulate=False, frames=1,
-               row_block=8, shard=0, num_shards=1, samples=1, jitter=False):
+               row_block=8, shard=0, num_shards=1, samples=1, jitter=False, lead_skip=0):
     fd = abi.FrameDesc()
     fd.width, fd.height, fd.max_depth, fd.use_bvh = width, height, depth, int(use_bvh)
     fd.seed, fd.sample, fd.accumulate, fd.frames = seed, sample, int(accumulate), frames
     fd.row_block, fd.shard, fd.num_shards = row_block, shard, num_shards
     fd.samples = samples
     fd.jitter = int(jitter)
+    fd.lead_skip = lead_skip
     return fd
 
 

@@ -112,6 +112,11 @@ typedef struct mirt_frame_desc {
     int32_t jitter;          /* 1: camera rays through (x + jx, y + jy), j in [0, 1)^2 from the pixel's
                                 RNG contract stream (rng.h; BASELINE configs[4] "4 spp jittered" --
                                 the reference samples pixel corners only); 0: main.c:362-363 */
+    int32_t lead_skip;       /* shard weighting (mirt 0.6; 0 = none): blocks are dealt in periods of 8
+                                rounds, one block per shard per round, and shard 0 sits out the first
+                                lead_skip (0..7) rounds of every period -- so shard 0 renders
+                                (8 - lead_skip) / (8 num_shards - lead_skip) of the frame
+                                (csrc/shard.h). 0 = block b to shard b % num_shards. num_shards >= 2 */
 } mirt_frame_desc;
 
 /* Work counters of the walk as configured; with MIRT_OPT_PRUNE = 0 they are
@@ -427,16 +432,7 @@ enum { MIRT_OPT_TRAVERSAL = 1, MIRT_OPT_FAST_SLAB = 2, MIRT_OPT_BLOCK_WAVES = 3,
        MIRT_OPT_DEBUG_STALL_MS = 19, /* test hook: every frame of this context starts behind a
                                        kernel that waits this many ms (0..10000, default 0), then
                                        exits -- a frame that overruns a caller's deadline
-                                       (mirt_multi's MIRT_MULTI_OPT_TIMEOUT_MS) without a hang */
-       MIRT_OPT_NODE_ORDER = 21,    /* layout of the four-wide tree built at the NEXT scene upload:
-                                       0 (default) = nodes numbered breadth first; 1 = the top levels
-                                       breadth first, then depth first with each node's children
-                                       contiguous, leaves renumbered to follow (locality of large
-                                       trees). Speed only: the walks' visits and results do not
-                                       change. */
-       MIRT_OPT_PRIMARY_WALK = 22   /* wavefront, ordered four-wide tree: camera rays walked as 8x8
-                                       packets (0, default) or each on its own, four-wide, like the
-                                       bounce rays (1). Speed only. */ };
+                                       (mirt_multi's MIRT_MULTI_OPT_TIMEOUT_MS) without a hang */ };
 /* Traversal ids keep their first-release values (mirt 0.1: TILE 0, WAVEFRONT 5).
    ABI note: the mirt 0.2 header numbered WAVEFRONT 1; mirt_set_option accepts
    1 as a deprecated alias of MIRT_TRAV_WAVEFRONT (mirt_get_option reads back

@@ -104,10 +104,15 @@ enum {
                                             kernels of the launch in its contexts' other slot have finished
                                             (one launch's kernels per context at a time; its copies still
                                             running). DESIGN §8 has the measurements */
-    MIRT_MULTI_OPT_GATHER_SELF = 261     /* gather delivery: 1 = rank 0's own slabs travel through the gather
+    MIRT_MULTI_OPT_GATHER_SELF = 261,    /* gather delivery: 1 = rank 0's own slabs travel through the gather
                                             too (an RCCL send to itself, or a device copy in copy mode) instead
                                             of being read in place, so every slab of the frame takes one path
                                             -- with one GPU, the RCCL gather path end to end. 0 = off (default) */
+    MIRT_MULTI_OPT_LEAD_SKIP = 262       /* 0..7: rank 0 renders a lighter share of every frame (it also
+                                            receives, de-interleaves and delivers it in the gather): row blocks
+                                            are dealt 8 rounds at a time, one per rank per round, and rank 0
+                                            sits out this many rounds of every 8 (mirt_frame_desc.lead_skip).
+                                            0 (default) = block b to rank b % n. Frames are the same bytes */
 };
 
 /* Counters of what the object issued since it was created (mirt_multi_get_stats). */

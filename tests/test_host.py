@@ -93,24 +93,43 @@ def test_degenerate_builds(mirt, oracle):
         assert got.nodes.tobytes() == ref.tobytes()
 
 
-@pytest.mark.parametrize("H,rb,world", [(1080, 8, 1), (1080, 8, 2), (1080, 8, 8), (1080, 8, 3), (90, 8, 7),
-                                        (13, 4, 5), (2160, 16, 8)])
-def test_shard_rows_partition(mirt, H, rb, world):
+@pytest.mark.parametrize("H,rb,world,d", [(1080, 8, 1, 0), (1080, 8, 2, 0), (1080, 8, 8, 0), (1080, 8, 3, 0),
+                                          (90, 8, 7, 0), (13, 4, 5, 0), (2160, 16, 8, 0), (1080, 8, 8, 2),
+                                          (1080, 8, 2, 7), (1080, 8, 3, 1), (90, 8, 7, 3), (13, 4, 5, 5),
+                                          (187, 8, 8, 4), (7, 8, 3, 2), (2160, 16, 8, 6)])
+def test_shard_rows_partition(mirt, H, rb, world, d):
+    """Every row in exactly one shard, compact rows in image order; the C
+    geometry (mirt_shard_rows, csrc/shard.h) equals shard.py's. d: the
+    lead-skip weighting (shard 0 sits out d of every 8 rounds)."""
     from importlib import import_module
     shard = import_module("cs201_sah-bvh_ray_tracer_amd.shard")
     seen = []
+    src_shard, pos = shard.row_sources(H, rb, world, d)
     for s in range(world):
-        fd = mirt.frame_desc(64, H, row_block=rb, shard=s, num_shards=world)
+        fd = mirt.frame_desc(64, H, row_block=rb, shard=s, num_shards=world, lead_skip=d)
         rows = mirt.shard_rows(fd)
-        assert len(rows) == shard.shard_row_count(H, rb, world, s)
+        assert len(rows) == shard.shard_row_count(H, rb, world, s, d)
+        assert (rows == shard.shard_rows_of(H, rb, world, s, d)).all()
         assert (np.diff(rows) > 0).all()
-        assert all((y // rb) % world == s for y in rows)
+        if d == 0:
+            assert all((y // rb) % world == s for y in rows)
         seen.extend(rows.tolist())
-        src_shard, pos = shard.row_sources(H, rb, world)
         for k, y in enumerate(rows):
             assert int(src_shard[y]) == s and int(pos[y]) == k
     assert sorted(seen) == list(range(H))
-    assert shard.slab_rows(H, rb, world) == max(shard.shard_row_count(H, rb, world, s) for s in range(world))
+    assert shard.slab_rows(H, rb, world, d) == max(shard.shard_row_count(H, rb, world, s, d) for s in range(world))
+    if d and H >= 8 * rb * world:
+        # shard 0 renders (8 - d) blocks of every 8 world - d
+        share = shard.shard_row_count(H, rb, world, 0, d) / H
+        assert abs(share - (8 - d) / (8 * world - d)) < 0.05
+
+
+def test_lead_skip_needs_shards(mirt):
+    """lead_skip in 0..7, and only for a frame split over two shards or more."""
+    for fd in (mirt.frame_desc(64, 64, lead_skip=1), mirt.frame_desc(64, 64, num_shards=2, lead_skip=8),
+               mirt.frame_desc(64, 64, num_shards=2, lead_skip=-1)):
+        with pytest.raises(mirt.MirtError):
+            mirt.shard_rows(fd)
 
 
 def test_invalid_frame_desc_raises(mirt):
@@ -345,9 +364,10 @@ def test_phantom_leaves_are_covered(mirt, kind, n, start, end, depth):
     assert pointed - tested <= {start + ns}, sorted(pointed - tested)[:5]
 
 
-@pytest.mark.parametrize("H,rb,world", [(1080, 8, 1), (1080, 8, 8), (45, 8, 3), (90, 8, 7), (13, 4, 5),
-                                        (187, 8, 8), (7, 8, 3)])
-def test_delivery_index_math_restated(H, rb, world):
+@pytest.mark.parametrize("H,rb,world,d", [(1080, 8, 1, 0), (1080, 8, 8, 0), (45, 8, 3, 0), (90, 8, 7, 0),
+                                          (13, 4, 5, 0), (187, 8, 8, 0), (7, 8, 3, 0), (1080, 8, 8, 2),
+                                          (187, 8, 8, 5), (45, 8, 3, 1), (90, 8, 7, 7), (13, 4, 5, 3)])
+def test_delivery_index_math_restated(H, rb, world, d):
     """shard.py's restatements of multi.hip's two deliveries (the gather's
     deinterleave_kernel and host-direct's strided copies, short last block
     included) rebuild a frame from its shards' compact slabs."""
@@ -355,9 +375,9 @@ def test_delivery_index_math_restated(H, rb, world):
     shard = import_module("cs201_sah-bvh_ray_tracer_amd.shard")
     rng = np.random.default_rng(H * 31 + world)
     full = rng.integers(0, 1 << 31, size=(2, H, 11), dtype=np.int64)
-    src, _ = shard.row_sources(H, rb, world)
+    src, _ = shard.row_sources(H, rb, world, d)
     slabs = [full[:, [y for y in range(H) if src[y] == s]] for s in range(world)]
     for s in range(world):
-        assert slabs[s].shape[1] == shard.shard_row_count(H, rb, world, s)
-    assert (shard.assemble_gather(slabs, H, rb) == full).all()
-    assert (shard.assemble_direct(slabs, H, rb) == full).all()
+        assert slabs[s].shape[1] == shard.shard_row_count(H, rb, world, s, d)
+    assert (shard.assemble_gather(slabs, H, rb, d) == full).all()
+    assert (shard.assemble_direct(slabs, H, rb, d) == full).all()

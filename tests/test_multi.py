@@ -38,10 +38,12 @@ def scene10k(mirt):
     return s, mirt.build_bvh(s)
 
 
-def shard_rows(H, world, k, rb=8):
+def shard_rows(H, world, k, rb=8, d=0):
     """Image rows of shard k, in its compact slab's order (row block b goes to
-    shard b % world: host_scene.cpp shard_row_count's geometry)."""
-    return np.array([y for y in range(H) if (y // rb) % world == k])
+    shard b % world, or with the lead-skip weighting d as csrc/shard.h deals
+    them: shard.py restates it)."""
+    from importlib import import_module
+    return import_module("cs201_sah-bvh_ray_tracer_amd.shard").shard_rows_of(H, rb, world, k, d)
 
 
 @pytest.fixture(scope="module")
@@ -105,8 +107,8 @@ def test_multi_rccl_gather_self_golden(mirt, golden, scene10k):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 8])
-def test_multi_rccl_emulated_gather_golden_rows(mirt, golden_frame, scene10k, world):
+@pytest.mark.parametrize("world,d", [(2, 0), (8, 0), (8, 3)])
+def test_multi_rccl_emulated_gather_golden_rows(mirt, golden_frame, scene10k, world, d):
     """The N-GPU gather's RCCL path on one GPU, shard by shard
     (MIRT_MULTI_OPT_EMULATE_WORLD / _RANK, gather delivery): rank k > 0
     renders its row blocks and sends them (an ncclSend/ncclRecv group to
@@ -114,7 +116,8 @@ def test_multi_rccl_emulated_gather_golden_rows(mirt, golden_frame, scene10k, wo
     rows of shard k. Rank 0 renders its blocks, receives world - 1 slabs
     through RCCL (its own slab standing in for each), de-interleaves and
     delivers the frame: its own rows equal the golden frame's, and every
-    received slab equals what was sent. Every RCCL call is counted."""
+    received slab equals what was sent. Every RCCL call is counted. d: the
+    lead-skip weighting (MIRT_MULTI_OPT_LEAD_SKIP), rank 0's lighter share."""
     s, b = scene10k
     W, H = 1920, 1080
     full = golden_frame
@@ -123,6 +126,8 @@ def test_multi_rccl_emulated_gather_golden_rows(mirt, golden_frame, scene10k, wo
     try:
         with mirt.MultiRenderer([0], lanes=2) as m:
             assert m.backend == "rccl" and m.delivery == "gather"
+            m.set_option(mirt.abi.MULTI_OPT_LEAD_SKIP, d)
+            assert m.get_option(mirt.abi.MULTI_OPT_LEAD_SKIP) == d
             m.upload(s, b)
             sends = recvs = 0
             for k in list(range(1, world)) + [0]:
@@ -130,7 +135,7 @@ def test_multi_rccl_emulated_gather_golden_rows(mirt, golden_frame, scene10k, wo
                 hb.array[:] = 7
                 m.render_frame_async(cam, mirt.frame_desc(W, H, depth=5, seed=1), hb)
                 m.wait()
-                mine = shard_rows(H, world, k)
+                mine = shard_rows(H, world, k, d=d)
                 if k > 0:
                     # rank k's slab as rank 0 received it; rank k delivers nothing itself
                     assert (m.read_gathered(k, len(mine), W) == full[mine]).all(), k
@@ -139,7 +144,7 @@ def test_multi_rccl_emulated_gather_golden_rows(mirt, golden_frame, scene10k, wo
                 else:
                     assert (hb.array[mine] == full[mine]).all()
                     for q in range(1, world):
-                        rq = len(shard_rows(H, world, q))
+                        rq = len(shard_rows(H, world, q, d=d))
                         assert (m.read_gathered(q, rq, W) == full[mine][:rq]).all(), q
                     sends, recvs = sends + world - 1, recvs + world - 1
                 st = m.stats()
@@ -176,20 +181,23 @@ def test_multi_queue_ahead_close_after_fresh_frame(mirt, scene10k):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [2, 3, 8])
-def test_multi_same_device_golden(mirt, golden, scene10k, n):
-    """n shards on one GPU, copy-mode gather + de-interleave: the golden frame."""
+@pytest.mark.parametrize("n,d", [(2, 0), (3, 0), (8, 0), (2, 7), (3, 2), (8, 3)])
+def test_multi_same_device_golden(mirt, golden, scene10k, n, d):
+    """n shards on one GPU, copy-mode gather + de-interleave: the golden
+    frame, also with rank 0's lighter share (lead skip d)."""
     s, b = scene10k
     with mirt.MultiRenderer([0] * n) as m:
         assert m.backend == "copy" and m.size == n
+        m.set_option(mirt.abi.MULTI_OPT_LEAD_SKIP, d)
         m.upload(s, b)
         img = m.render_frame(mirt.default_camera(), 1920, 1080, depth=5, seed=1)
         assert sha(img) == golden["frames"][GOLD]["sha"]
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,rb", [(3, 8), (5, 16), (4, 1)])
-def test_multi_ragged_frames_equal_one_gpu(gpu, mirt, n, rb):
+@pytest.mark.parametrize("n,rb,d,direct", [(3, 8, 0, False), (5, 16, 0, False), (4, 1, 0, False), (3, 8, 3, False),
+                                           (5, 16, 1, True), (4, 1, 6, True), (8, 8, 2, True)])
+def test_multi_ragged_frames_equal_one_gpu(gpu, mirt, n, rb, d, direct):
     """Ragged sizes (77 x 45: the last block short, some ranks one block
     fewer) and other interleave blocks equal one ctx's frame, depth 1 and 5,
     brute force too."""
@@ -197,7 +205,8 @@ def test_multi_ragged_frames_equal_one_gpu(gpu, mirt, n, rb):
     b = mirt.build_bvh(s)
     gpu.upload(s, b)
     cam = mirt.default_camera()
-    with mirt.MultiRenderer([0] * n) as m:
+    with mirt.MultiRenderer([0] * n, host_direct=direct) as m:
+        m.set_option(mirt.abi.MULTI_OPT_LEAD_SKIP, d)
         m.upload(s, b)
         for depth, bvh in ((1, True), (5, True), (5, False)):
             want = gpu.render_frame(cam, 77, 45, depth=depth, use_bvh=bvh, seed=3)
@@ -388,8 +397,9 @@ def test_multi_timeout_fails_with_status(mirt, scene10k):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("devices,dc", [([0, 0], 2), ([0, 0, 0], 2), ([0] * 8, 2), ([0, 0, 0], 1)])
-def test_multi_host_direct_copy_methods(gpu, mirt, scene10k, devices, dc):
+@pytest.mark.parametrize("devices,dc,d", [([0, 0], 2, 0), ([0, 0, 0], 2, 0), ([0] * 8, 2, 0), ([0, 0, 0], 1, 0),
+                                          ([0] * 8, 0, 3), ([0] * 8, 1, 3), ([0, 0, 0], 2, 5)])
+def test_multi_host_direct_copy_methods(gpu, mirt, scene10k, devices, dc, d):
     """MIRT_MULTI_OPT_DIRECT_COPY: the ranks' rows into the host frame by a
     copy kernel storing into the mapped page-locked frame (2) or one DMA per
     row block (1), into page-locked and pageable outputs, ragged frames
@@ -400,6 +410,7 @@ def test_multi_host_direct_copy_methods(gpu, mirt, scene10k, devices, dc):
     hb = [mirt.HostBuffer((H, W, 4)) for _ in range(4)]
     try:
         with mirt.MultiRenderer(devices, lanes=2, host_direct=True) as m:
+            m.set_option(mirt.abi.MULTI_OPT_LEAD_SKIP, d)
             m.set_option(mirt.abi.MULTI_OPT_DIRECT_COPY, dc)
             assert m.get_option(mirt.abi.MULTI_OPT_DIRECT_COPY) == dc
             m.upload(s, b)
