@@ -134,11 +134,11 @@ TAIL_GRID_MULTI = 0
 # current one on its stream (own slabs, copies on a copy stream), so no
 # context idles through its frame's D2H and the host's turnaround
 QUEUE_AHEAD, QUEUE_AHEAD_MULTI = False, False
-KERNEL = "bounce_kernel<true, 2, false, false>"   # dominant kernel of the default (wavefront, four-wide) schedule
+KERNEL = "bounce_kernel<true, 2, false>"   # dominant kernel of the default (wavefront, four-wide) schedule
 # the PMC-derived bound of the timed launch shape, per workload
 # (scripts/pmc_bench.sh over this script's own command + scripts/pmc_summary.py);
 # the newest round's file wins
-PMC_BOUND = {wl: [os.path.join(ROOT, "profiles", f"r0{r}_pmc_bound_{wl}.json") for r in (5, 4, 3)] for wl in WORKLOADS}
+PMC_BOUND = {wl: [os.path.join(ROOT, "profiles", f"r0{r}_pmc_bound_{wl}.json") for r in (6, 5, 4, 3)] for wl in WORKLOADS}
 # the chip's gather peak by access shape (scripts/td_probe.hip + its counter
 # passes, scripts/td_probe_summary.py): the roofline's denominator
 TD_PROBE = os.path.join(ROOT, "profiles", "r04_td_probe.json")
@@ -325,7 +325,9 @@ def gather_peak(probe, tcp_per_inst):
 def trace_check():
     """The same launch shape ALONE under rocprofv3 --kernel-trace --stats
     (committed summary): its mean duration must agree with kernel_ms."""
-    for path, stats in ((os.path.join(ROOT, "profiles", "r05_exclusive_bounce_trace.json"),
+    for path, stats in ((os.path.join(ROOT, "profiles", "r06_exclusive_bounce_trace.json"),
+                         "profiles/r06_logs/r06pmc/prof_exclusive_kernel_stats.csv"),
+                        (os.path.join(ROOT, "profiles", "r05_exclusive_bounce_trace.json"),
                          "profiles/r05_logs/r05z/prof_exclusive_kernel_stats.csv"),
                         (os.path.join(ROOT, "profiles", "r04q", "exclusive_bounce_trace.json"),
                          "profiles/r04q/prof_exclusive_kernel_stats.csv")):

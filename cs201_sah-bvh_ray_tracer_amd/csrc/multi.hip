@@ -219,7 +219,7 @@ struct mirt_multi {
     int timeout_ms = 60000;           // MIRT_MULTI_OPT_TIMEOUT_MS (0: unbounded)
     int emu_world = 0, emu_rank = 0;  // MIRT_MULTI_OPT_EMULATE_*: this one rank plays shard emu_rank of emu_world
     int direct_copy = 0;              // MIRT_MULTI_OPT_DIRECT_COPY: 0 one strided copy per frame, 1 one per row block
-    int lead_skip = 0;                // MIRT_MULTI_OPT_LEAD_SKIP: shard 0's lighter share (shard.h)
+    int lead_skip = -1;               // MIRT_MULTI_OPT_LEAD_SKIP: shard 0's lighter share (shard.h); -1 auto
     bool gather_self = false;         // MIRT_MULTI_OPT_GATHER_SELF: rank 0's own slabs travel through the gather too
     int last_lane = -1;               // lane of the last launch enqueued
     // a wait timed out or a device call failed: every call returns fail_msg;
@@ -238,6 +238,21 @@ struct mirt_multi {
 namespace {
 
 hipStream_t stream_of(mirt_ctx* c) { return (hipStream_t)mirt_ctx_stream(c); }
+
+// The lead-skip weighting of a frame split `world` ways (shard.h): the
+// option's value, or by default (-1) a lighter share for rank 0 in the gather
+// only -- it also receives, de-interleaves and delivers the frame. Measured at
+// N = 8 (per-shard emulation, frames gathered on GPU 0, MEASUREMENTS.md §D):
+// lead skip 0 / 2 / 3 / 4 -> 10.3 / 12.4 / 13.6 / 13.8 G rays/s, rank 1 the
+// slowest from 4 on; smaller N take the share that balances the same per-frame
+// cost of rank 0's exchange against a larger render share.
+int lead_skip_for(const mirt_multi* m, int world, bool gather)
+{
+    if (world <= 1) return 0;
+    if (m->lead_skip >= 0) return m->lead_skip;
+    if (!gather) return 0;
+    return world == 2 ? 1 : world <= 4 ? 2 : 4;
+}
 
 int failed_status(const mirt_multi* m, const char* fn)
 {
@@ -406,7 +421,7 @@ int prepare(mirt_multi* m, Lane& L, const mirt_camera* cam, const mirt_frame_des
     J.sd.row_block = fd->row_block > 0 ? fd->row_block : 8;
     J.sd.num_shards = J.world;
     J.sd.samples = spp * nframes;
-    J.sd.lead_skip = J.world > 1 ? m->lead_skip : 0;
+    J.sd.lead_skip = lead_skip_for(m, J.world, !m->direct);
     J.rb = J.sd.row_block;
     J.sr = ShardSrc{};
     mirt_frame_desc g = J.sd;
@@ -789,7 +804,7 @@ int check_frame(const mirt_multi* m, const mirt_camera* cam, const mirt_frame_de
     whole.num_shards = m->emu_world > 1 ? m->emu_world : m->n;
     whole.row_block = fd->row_block > 0 ? fd->row_block : 8;
     whole.samples = std::max(1, fd->samples) * nframes;
-    whole.lead_skip = whole.num_shards > 1 ? m->lead_skip : 0;
+    whole.lead_skip = lead_skip_for(m, whole.num_shards, !m->direct);
     if (!frame_desc_valid(&whole) || whole.num_shards > kMaxShards) {
         set_error("%s: invalid frame descriptor (or more than 64 frames / samples per launch)", fn);
         return MIRT_E_INVALID;
@@ -1021,7 +1036,7 @@ int mirt_multi_set_option(mirt_multi* m, int option, int value)
         m->gather_self = value == 1;
         return MIRT_OK;
     case MIRT_MULTI_OPT_LEAD_SKIP:
-        if (value < 0 || value >= kLeadRounds) break;
+        if (value < -1 || value >= kLeadRounds) break;
         m->lead_skip = value;
         return MIRT_OK;
     default:

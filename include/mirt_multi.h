@@ -111,8 +111,10 @@ enum {
     MIRT_MULTI_OPT_LEAD_SKIP = 262       /* 0..7: rank 0 renders a lighter share of every frame (it also
                                             receives, de-interleaves and delivers it in the gather): row blocks
                                             are dealt 8 rounds at a time, one per rank per round, and rank 0
-                                            sits out this many rounds of every 8 (mirt_frame_desc.lead_skip).
-                                            0 (default) = block b to rank b % n. Frames are the same bytes */
+                                            sits out this many rounds of every 8 (mirt_frame_desc.lead_skip);
+                                            0 = block b to rank b % n; -1 (default) = automatic: the gather
+                                            at n = 2 / 3-4 / 5+ ranks 1 / 2 / 4, host-direct 0. Frames are the
+                                            same bytes whatever the value */
 };
 
 /* Counters of what the object issued since it was created (mirt_multi_get_stats). */

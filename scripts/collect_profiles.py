@@ -18,7 +18,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-KERNEL = "bounce_kernel<true, 2, false, false>"
+KERNEL = "bounce_kernel<true, 2, false>"
 WORKLOAD = [1920, 1080, 10000, 5]
 
 

@@ -13,7 +13,7 @@ import csv
 import json
 import statistics
 
-BOUNCE = "bounce_kernel<true, 2, false, false>"
+BOUNCE = "bounce_kernel<true, 2, false>"
 
 
 def main():

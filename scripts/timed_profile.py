@@ -14,7 +14,7 @@ import argparse
 import csv
 import json
 
-BOUNCE = "bounce_kernel<true, 2, false, false>"   # <true, 4, false, false> on trees past the L2 (MIRT_OPT_LEAF_BATCH)
+BOUNCE = "bounce_kernel<true, 2, false>"   # <true, 4, false> on trees past the L2 (MIRT_OPT_LEAF_BATCH)
 PRIMARY = "primary_kernel<true, true>"
 
 
