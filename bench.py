@@ -825,8 +825,10 @@ def measure(args):
                             "accumulation buffer" if args.accumulate else "1 fresh frame (main.c:358-374)")
                            + f", {SPP} sample(s), {per} frame(s) per launch, launches rotating over {lanes} lanes, "
                              "every frame delivered to page-locked host memory",
-                   "parallelism": (f"row-block shard x{n}, one process: mirt_multi over ncclCommInitAll, "
-                                   + ("one D2H per frame" if n == 1 else "RCCL gather to GPU 0 + D2H"
+                   "parallelism": ("one GPU, one process: mirt_multi with one rank (no exchange: the rank's slab "
+                                   "is the frame), one D2H per frame" if n == 1 else
+                                   f"row-block shard x{n}, one process: mirt_multi, "
+                                   + ("RCCL gather to GPU 0 (ncclCommInitAll communicators) + D2H"
                                       if delivery == "gather" else "per-GPU strided D2H into the host frame"))},
         "timing": "one process drives all GPUs (include/mirt_multi.h); the timed region is bracketed by "
                   "mirt_multi_wait on both sides, so it ends when every frame is in host memory on every lane",
@@ -875,7 +877,8 @@ def measure(args):
             el2 = timed_loop(m2, cam, plan(0, args.warmup, per), tl2, bufs2, DEPTH, args.accumulate, tail)
             other_frame = last_delivered(m2, bufs2, tl2)
             other.update({"mrays_s": round(W * H * SPP * args.steps / el2 / 1e6, 3),
-                          "ms_per_step": round(el2 / args.steps * 1e3, 4), "backend": m2.backend})
+                          "ms_per_step": round(el2 / args.steps * 1e3, 4), "backend": m2.backend,
+                          "lead_skip_option": m2.get_option(mirt.abi.MULTI_OPT_LEAD_SKIP)})
             if od == "gather":
                 el_dev = timed_loop(m2, cam, plan(0, 2, per), plan(args.warmup, args.steps, per), bufs2, DEPTH,
                                     args.accumulate, tail, device_only=True)
@@ -890,6 +893,10 @@ def measure(args):
             print(f"bench.py: the {od} leg failed: {other['error']}", file=sys.stderr, flush=True)
         finally:
             if m2 is not None:
+                try:   # what the n-GPU exchange issued (mirt_multi_get_stats): RCCL calls, bytes, copies
+                    other["exchange_stats"] = m2.stats()
+                except Exception as e:   # noqa: BLE001
+                    other["exchange_stats_error"] = str(e)
                 m2.close()
             if bufs2 is not None:
                 close_bufs(bufs2)

@@ -113,8 +113,8 @@ enum {
                                             are dealt 8 rounds at a time, one per rank per round, and rank 0
                                             sits out this many rounds of every 8 (mirt_frame_desc.lead_skip);
                                             0 = block b to rank b % n; -1 (default) = automatic: the gather
-                                            at n = 2 / 3-4 / 5+ ranks 1 / 2 / 4, host-direct 0. Frames are the
-                                            same bytes whatever the value */
+                                            at n = 2 / 3-4 / 5-6 / 7+ ranks 0 / 1 / 2 / 3, host-direct 0.
+                                            Frames are the same bytes whatever the value */
 };
 
 /* Counters of what the object issued since it was created (mirt_multi_get_stats). */
