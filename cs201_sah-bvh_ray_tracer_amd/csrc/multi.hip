@@ -219,7 +219,7 @@ struct mirt_multi {
     int timeout_ms = 60000;           // MIRT_MULTI_OPT_TIMEOUT_MS (0: unbounded)
     int emu_world = 0, emu_rank = 0;  // MIRT_MULTI_OPT_EMULATE_*: this one rank plays shard emu_rank of emu_world
     int direct_copy = 0;              // MIRT_MULTI_OPT_DIRECT_COPY: 0 one strided copy per frame, 1 one per row block
-    int lead_skip = -1;               // MIRT_MULTI_OPT_LEAD_SKIP: shard 0's lighter share (shard.h); -1 auto
+    int lead_skip = kLeadRounds;      // MIRT_MULTI_OPT_LEAD_SKIP: shard 0's lighter share (shard.h); 8 automatic
     bool gather_self = false;         // MIRT_MULTI_OPT_GATHER_SELF: rank 0's own slabs travel through the gather too
     int last_lane = -1;               // lane of the last launch enqueued
     // a wait timed out or a device call failed: every call returns fail_msg;
@@ -251,7 +251,7 @@ hipStream_t stream_of(mirt_ctx* c) { return (hipStream_t)mirt_ctx_stream(c); }
 int lead_skip_for(const mirt_multi* m, int world, bool gather)
 {
     if (world <= 1) return 0;
-    if (m->lead_skip >= 0) return m->lead_skip;
+    if (m->lead_skip < kLeadRounds) return m->lead_skip;
     if (!gather) return 0;
     return world <= 2 ? 0 : world <= 4 ? 1 : world <= 6 ? 2 : 3;
 }
@@ -1038,7 +1038,7 @@ int mirt_multi_set_option(mirt_multi* m, int option, int value)
         m->gather_self = value == 1;
         return MIRT_OK;
     case MIRT_MULTI_OPT_LEAD_SKIP:
-        if (value < -1 || value >= kLeadRounds) break;
+        if (value < 0 || value > kLeadRounds) break;   // kLeadRounds: automatic
         m->lead_skip = value;
         return MIRT_OK;
     default:

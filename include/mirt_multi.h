@@ -112,7 +112,7 @@ enum {
                                             receives, de-interleaves and delivers it in the gather): row blocks
                                             are dealt 8 rounds at a time, one per rank per round, and rank 0
                                             sits out this many rounds of every 8 (mirt_frame_desc.lead_skip);
-                                            0 = block b to rank b % n; -1 (default) = automatic: the gather
+                                            0 = block b to rank b % n; 8 (default) = automatic: the gather
                                             at n = 2 / 3-4 / 5-6 / 7+ ranks 0 / 1 / 2 / 3, host-direct 0.
                                             Frames are the same bytes whatever the value */
 };

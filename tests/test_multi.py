@@ -126,6 +126,9 @@ def test_multi_rccl_emulated_gather_golden_rows(mirt, golden_frame, scene10k, wo
     try:
         with mirt.MultiRenderer([0], lanes=2) as m:
             assert m.backend == "rccl" and m.delivery == "gather"
+            assert m.get_option(mirt.abi.MULTI_OPT_LEAD_SKIP) == 8   # the default: automatic
+            with pytest.raises(mirt.MirtError):
+                m.set_option(mirt.abi.MULTI_OPT_LEAD_SKIP, -1)
             m.set_option(mirt.abi.MULTI_OPT_LEAD_SKIP, d)
             assert m.get_option(mirt.abi.MULTI_OPT_LEAD_SKIP) == d
             m.upload(s, b)
