@@ -77,7 +77,7 @@ def main():
         timed = bench.plan(a.warmup, a.steps, per, a.ramp)
         tail = bench.tail_of(timed, tail_n, lanes, blocks)
         ranks = [int(k) for k in a.ranks.split(",")] if a.ranks else list(range(world))
-        runs, enq = {k: [] for k in ranks}, []
+        runs, enq, enq_runs = {k: [] for k in ranks}, [], []
         for _ in range(a.rounds):          # rounds interleaved across the shards
             for k in ranks:
                 m.emulate(world, k)
@@ -85,6 +85,7 @@ def main():
                                       tail, device_only=a.device_only)
                 runs[k].append(el)
                 enq += bench.ENQUEUE
+                enq_runs.append([round(x * 1e3, 3) for x in bench.ENQUEUE])
         st = m.stats()
         m.close()
         bench.close_bufs(bufs)
@@ -103,6 +104,7 @@ def main():
             "rank_ms_per_frame_runs": {k: [round(t / a.steps * 1e3, 4) for t in v] for k, v in runs.items()},
             "slowest_rank": ranks[per_rank.index(slow)],
             "enqueue_ms_per_launch_median": round(sorted(enq)[len(enq) // 2] * 1e3, 4) if enq else None,
+            "enqueue_ms_first_runs": enq_runs[:3],   # each timed launch's host call, in order
             "estimator": "N x the slowest shard's MEDIAN over the rounds (pred_job_mrays_s); "
                          "pred_job_mrays_s_best: the slowest shard's best round",
             "pred_job_mrays_s": round(W * H * SPP * a.steps / slow / 1e6, 1),

@@ -362,7 +362,7 @@ def test_shared_accumulation_frames_in_flight(gpu, mirt, oracle, small, W, H, n)
 
 
 def test_lazy_fold_fresh_frames_in_flight(gpu, mirt):
-    """MIRT_LAZY_FOLD: fresh frames on four ctxs sharing one accumulation
+    """The lazy fold: fresh frames on four ctxs sharing one accumulation
     buffer leave their displays pending instead of folding in order. After
     six fresh frames in flight the shared buffer (read back) is the last
     frame's colours / 255; an accumulating frame on ANOTHER ctx then continues

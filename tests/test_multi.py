@@ -438,7 +438,7 @@ def test_multi_lazy_then_batch_then_accumulate(gpu, mirt, scene10k):
     """A one-frame fresh launch (its display left pending on the lanes'
     shared buffer), then a launch of two fresh frames (folded in order: it
     supersedes the pending one), then an accumulating frame: equal to one
-    context's sequence (MIRT_LAZY_FOLD with batched launches)."""
+    context's sequence (the lazy fold with batched launches)."""
     s, b = scene10k
     W, H = 320, 180
     cam = mirt.default_camera()
