@@ -240,14 +240,15 @@ namespace {
 hipStream_t stream_of(mirt_ctx* c) { return (hipStream_t)mirt_ctx_stream(c); }
 
 // The lead-skip weighting of a frame split `world` ways (shard.h): the
-// option's value, or by default (-1) a lighter share for rank 0 in the gather
-// only -- it also receives, de-interleaves and delivers the frame. Measured
-// (per-shard emulation, frames gathered on GPU 0, MEASUREMENTS.md §D): N = 8
-// lead skip 0 / 2 / 3 / 4 -> 10.3 / 12.4 / 13.6 / 13.8-15.1 G rays/s, at 4 rank
-// 0 already the lightest (0.087 vs 0.131-0.137 ms per frame); N = 4 with 2:
-// rank 0 0.218 vs 0.26 ms; N = 2 with 1: rank 1 0.49 vs rank 0 0.46 ms. Rank
-// 0's exchange costs about the same per frame at any N while the render share
-// shrinks with N, so the skip grows with N.
+// option's value, or by default (kLeadRounds: automatic) a lighter share for
+// rank 0 in the gather only -- it also receives, de-interleaves and delivers
+// the frame. Measured (per-shard emulation, frames gathered on GPU 0,
+// MEASUREMENTS.md §D): N = 8 lead skip 0 / 2 / 3 / 4 -> 10.3 / 12.4 / 15.7 /
+// 13.8-15.1 G rays/s (at 3 rank 0 0.10 ms per frame, ranks 1-7 0.126-0.132);
+// N = 4: skip 1 8.0 G (rank 0 0.240 vs 0.25-0.26 ms), skip 2 7.9 G; N = 2:
+// skip 0 4.3 G, skip 1 4.2 G. Rank 0's exchange costs about the same per
+// frame at any N while the render share shrinks with N, so the skip grows
+// with N.
 int lead_skip_for(const mirt_multi* m, int world, bool gather)
 {
     if (world <= 1) return 0;
