@@ -434,6 +434,40 @@ def test_multi_host_direct_copy_methods(gpu, mirt, scene10k, devices, dc, d):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("devices,ahead", [([0], False), ([0, 0], False), ([0], True)])
+def test_multi_pending_batches_then_accumulate(gpu, mirt, scene10k, devices, ahead):
+    """Launches of several fresh frames leave their last display pending on
+    the lanes' shared accumulation buffer (no fold behind them): a later batch
+    on the SAME context supersedes it (its kernels overwrite that slab), and
+    the accumulating frames after the batches fold the newest one. Every
+    frame equals one context's sequence."""
+    s, b = scene10k
+    W, H = 333, 187
+    cam = mirt.default_camera()
+    hb = [mirt.HostBuffer((H, W, 4)) for _ in range(8)]
+    try:
+        with mirt.MultiRenderer(devices, lanes=2, queue_ahead=ahead) as m:
+            m.upload(s, b)
+            for f0 in range(0, 6, 2):     # lanes 0, 1, 0 (slots 0, 1, 2 with QUEUE_AHEAD)
+                m.render_frames_async(cam, mirt.frame_desc(W, H, depth=5, seed=5, sample=f0), hb[f0:f0 + 2])
+            m.render_frame_async(cam, mirt.frame_desc(W, H, depth=5, seed=5, sample=6, accumulate=True, frames=2),
+                                 hb[6])
+            m.render_frame_async(cam, mirt.frame_desc(W, H, depth=5, seed=5, sample=7, accumulate=True, frames=3),
+                                 hb[7])
+            m.wait()
+            got = [x.array.copy() for x in hb]
+    finally:
+        for x in hb:
+            x.close()
+    gpu.upload(s, b)
+    want = [gpu.render_frame(cam, W, H, depth=5, seed=5, sample=k) for k in range(6)]
+    want.append(gpu.render_frame(cam, W, H, depth=5, seed=5, sample=6, accumulate=True, frames=2))
+    want.append(gpu.render_frame(cam, W, H, depth=5, seed=5, sample=7, accumulate=True, frames=3))
+    for j in range(8):
+        assert (got[j] == want[j]).all(), j
+
+
+@pytest.mark.gpu
 def test_multi_lazy_then_batch_then_accumulate(gpu, mirt, scene10k):
     """A one-frame fresh launch (its display left pending on the lanes'
     shared buffer), then a launch of two fresh frames (folded in order: it
