@@ -497,6 +497,20 @@ __global__ __launch_bounds__(256) MIRT_PRIMARY_ATTR void primary_kernel(DevScene
     }
 }
 
+// The bounce kernel's walks test the HNode slot boxes without
+// slab_cons_fast's margins (trace.h, BND): the boxes are grown by 2^-19
+// DevScene::o_bound at upload, and a bounce ray whose origin lies within that
+// bound -- a hit point in the scene -- needs no more; an origin beyond it (or
+// NaN) takes the exact test. Round 6: serial bounce pass 0.84-0.86 ->
+// 0.83 ms, 1080p/10k +1.5-3%, 1080p/100k +3.5% (MEASUREMENTS.md §D).
+constexpr bool kBoundedSlab = true;
+__device__ __forceinline__ SlabRay bounce_slab_ray(const DevScene& sc, const Ray& ray)
+{
+    SlabRay s = slab_ray(ray);
+    s.generic = s.generic || !(fmaxf(fabsf(ray.ox), fmaxf(fabsf(ray.oy), fabsf(ray.oz))) <= sc.o_bound);
+    return s;
+}
+
 // The walk of one bounce ray: WALK 0 = reference DFS order (any tree),
 // 2 = ordered four-wide (HNode, LDS stack).
 template <int WALK>
@@ -527,7 +541,11 @@ struct WideBounceWalk {  // WALK 2: four-wide; 4: four-wide, a step's leaf spher
     __device__ void step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr, uint32_t* stk,
                          float& bt, int& bs, Counters& cnt)
     {
-        wide_lane_step<FAST, false, WALK == 4>(sc, sr, sp, pr, w, stk, bt, bs, cnt, hc, hc_n);
+        // the bounded test in WALK 2; WALK 4 (trees past the L2) keeps the
+        // margins: with its batched leaf loads the bounded form spills more
+        // (4K/1M: -8%, MEASUREMENTS.md §D)
+        wide_lane_step<FAST, false, WALK == 4, kBoundedSlab && WALK != 4>(sc, sr, sp, pr, w, stk, bt, bs, cnt, hc,
+                                                                          hc_n);
     }
 };
 template <>
@@ -590,7 +608,7 @@ __device__ __forceinline__ bool shade_level(const DevScene& sc, const FrameConst
 // its stack moved from its source lane's column to the wave layout of
 // solo_step, each level walked with solo_step and shaded as shade_level
 // (lane 0 stores the pixel).
-template <bool FAST>
+template <bool FAST, bool BND>
 __device__ __forceinline__ void solo_chain(const DevScene& sc, const FrameConst& f, int l0, Ray ray, float best_t,
                                         int best_s, Prune pr, QuadWalk qw, int level, uint32_t k, uint32_t pixel,
                                         uint32_t base0, uint32_t src, uint32_t* wst, uint32_t* wcs,
@@ -616,16 +634,16 @@ __device__ __forceinline__ void solo_chain(const DevScene& sc, const FrameConst&
     __builtin_amdgcn_wave_barrier();
     if (lane < top) *solo_slot(wst, lane) = v;
     uint32_t* cs = wcs + src;  // the colour stack stays in the source column
-    SlabRay sr = slab_ray(ray);
+    SlabRay sr = bounce_slab_ray(sc, ray);
     SphRay sp = sph_ray(ray);
     SoloWalk w{lane < 4 ? cur : kPNone, lane < 4 ? end : 0u, top};
     for (;;) {
-        while (solo_step<FAST, kWideStack * 64>(sc, sr, sp, pr, w, wst, best_t, best_s, hc, hc_n)) {
+        while (solo_step<FAST, kWideStack * 64, BND>(sc, sr, sp, pr, w, wst, best_t, best_s, hc, hc_n)) {
         }
         if (!shade_level(sc, f, ray, best_t, best_s, level, k, chain_key(f, pixel), cs, kWideStride, base0, pixel, out,
                          acc, lane == 0))
             return;
-        sr = slab_ray(ray);
+        sr = bounce_slab_ray(sc, ray);
         sp = sph_ray(ray);
         w = SoloWalk{lane < 4 ? sc.wide_root : kPNone, 0u, 0u};
         best_t = INFINITY;
@@ -683,7 +701,7 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
     uint32_t seg = blockIdx.x % kQSeg, segs_left = kQSeg;  // wave-uniform
     bool has = false, exhausted = false;
     Ray ray{0, 0, 0, 0, 0, 0};
-    SlabRay sr = slab_ray(ray);
+    SlabRay sr = bounce_slab_ray(sc, ray);
     SphRay sp = sph_ray(ray);
     Prune pr = prune_off();
     BounceWalk<WALK> w;
@@ -716,7 +734,7 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                 if (idx < sz) {
                     const BounceRec rec = queue[lo + idx];
                     ray = Ray{rec.ox, rec.oy, rec.oz, rec.dx, rec.dy, rec.dz};
-                    sr = slab_ray(ray);
+                    sr = bounce_slab_ray(sc, ray);
                     sp = sph_ray(ray);
                     pixel = rec.pixel;
                     k = rec.k;
@@ -770,7 +788,7 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
             }
             if (shade_level(sc, f, ray, best_t, best_s, level, k, chain_key(f, pixel), cs, cstride, base0, pixel, out,
                             acc, true)) {
-                sr = slab_ray(ray);
+                sr = bounce_slab_ray(sc, ray);
                 sp = sph_ray(ray);
                 w.start(sc);
                 best_t = INFINITY;
@@ -811,7 +829,7 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
             QuadWalk qw{pull(lw.cur), pull(lw.end), pull(lw.top)};
             has = qhas;
             if (!qhas) qw.cur = kPNone;
-            sr = slab_ray(ray);
+            sr = bounce_slab_ray(sc, ray);
             sp = sph_ray(ray);
             // the ray's LDS stacks stay in its source lane's columns
             uint32_t* qstk = wstack + (threadIdx.x & ~63u) + src;
@@ -823,19 +841,21 @@ __global__ __launch_bounds__(256) MIRT_BOUNCE_ATTR void bounce_kernel(DevScene s
                     // one ray left in the wave: every quad of the wave walks it
                     const uint64_t rays = __ballot(has && (lane & 3) == 0);
                     if (__popcll(rays) == 1) {
-                        solo_chain<FAST>(sc, f, __builtin_ctzll(rays), ray, best_t, best_s, pr, qw, level, k, pixel,
+                        solo_chain<FAST, kBoundedSlab && WALK != 4>(sc, f, __builtin_ctzll(rays), ray, best_t, best_s, pr,
+                                                                    qw, level, k, pixel,
                                          base0, src, wstack + (threadIdx.x & ~63u), cstack + (threadIdx.x & ~63u),
                                          out, acc, (lds_uint4*)hcache, hc_n);
                         break;
                     }
                 }
                 if (has && qw.cur != kPNone)
-                    quad_step<FAST, kWideStride, kWideStack>(sc, sr, sp, pr, qw, qstk, best_t, best_s,
+                    quad_step<FAST, kWideStride, kWideStack, kBoundedSlab && WALK != 4>(sc, sr, sp, pr, qw, qstk, best_t,
+                                                                                        best_s,
                                                              (lds_uint4*)hcache, hc_n);
                 if (has && qw.cur == kPNone) {
                     if (shade_level(sc, f, ray, best_t, best_s, level, k, chain_key(f, pixel), qcs, kWideStride, base0, pixel, out,
                                     acc, (lane & 3) == 0)) {
-                        sr = slab_ray(ray);
+                        sr = bounce_slab_ray(sc, ray);
                         sp = sph_ray(ray);
                         qw = QuadWalk{sc.wide_root, 0u, 0u};
                         best_t = INFINITY;
@@ -1331,6 +1351,7 @@ struct mirt_ctx {
     uint32_t* d_overlay = nullptr;  // BVH overlay: per-pixel last line in draw order
     size_t overlay_cap = 0;
     float r_max = 0.0f, c_max = 0.0f;
+    float o_bound = 0.0f;       // the bounce walks' origin bound the HNode boxes were grown for
     int bounce_threshold = 20;  // wavefront: shade finished rays once fewer lanes walk (swept: profiles/r02thr_threshold_sweep.txt)
     int bounce_blocks = 0;      // wavefront: persistent workgroups (set in mirt_create)
     int bounce_blocks_opt = 0;  // MIRT_OPT_BOUNCE_BLOCKS override (0: occupancy x CUs)
@@ -1570,8 +1591,10 @@ uint16_t half_up(float v)
 // an HNode for each inner node that is some HNode's slot holds that node's
 // grandchildren (a leaf child standing in for its own); one leaf (sphere +
 // exact box) per leaf slot. Used only when the PNode conditions hold and the boxes nest.
+// grow > 0 (the bounce walks' bounded slab test): every slot box grown by `grow` on each face
+// before the outward fp16 rounding.
 void build_hnodes(const mirt_node* nd, int nn, const mirt_sphere* sp, int ns, std::vector<HNode>& hn,
-                  std::vector<HAux>& aux, std::vector<float4>& lgeo, std::vector<LeafBox>& lbox)
+                  std::vector<HAux>& aux, std::vector<float4>& lgeo, std::vector<LeafBox>& lbox, double grow)
 {
     hn.assign(1, HNode{});
     aux.assign(1, HAux{0xffffffffu, (uint32_t)nn});  // flat + 1 == 0: the whole tree
@@ -1586,8 +1609,14 @@ void build_hnodes(const mirt_node* nd, int nn, const mirt_sphere* sp, int ns, st
             return;
         }
         const mirt_node& n = nd[ci];
-        for (int a = 0; a < 3; a++)
-            h.slot[k].box[a] = (uint32_t)half_down(n.bmin[a]) | ((uint32_t)half_up(n.bmax[a]) << 16);
+        for (int a = 0; a < 3; a++) {
+            float lo = n.bmin[a], hi = n.bmax[a];
+            if (grow > 0.0) {   // rounded outward again: the float of lo - grow may lie above it
+                lo = std::nextafter((float)((double)lo - grow), -INFINITY);
+                hi = std::nextafter((float)((double)hi + grow), INFINITY);
+            }
+            h.slot[k].box[a] = (uint32_t)half_down(lo) | ((uint32_t)half_up(hi) << 16);
+        }
         uint32_t ref;
         if (n.skip & MIRT_NODE_EMPTY) {
             ref = kPNone;
@@ -1669,7 +1698,7 @@ DevScene dev_scene(const mirt_ctx* c)
     return DevScene{c->d_nodes, c->d_nodes32, c->d_geo, c->d_color, (uint32_t)c->num_nodes, c->num_spheres,
                     prune, c->r_max, c->c_max, c->d_pnodes, ordered, c->d_hnodes, c->d_haux,
                     (const float4*)c->d_leaves, (const LeafBox*)(c->d_leaves + c->leaf_box_off), ordered,
-                    ordered ? c->num_hnodes : 0u, c->wide_root};
+                    ordered ? c->num_hnodes : 0u, c->wide_root, c->o_bound};
 }
 
 AccumShare* accum_new(int device)
@@ -2141,7 +2170,20 @@ try {
     std::vector<HAux> hx;
     std::vector<float4> lgeo;
     std::vector<LeafBox> lbox;
-    build_hnodes(nodes, nn, spheres, ns, hn, hx, lgeo, lbox);
+    // the bounce walks' bounded slab test: C bounds every box coordinate and every sphere point
+    // (so every bounce-ray origin, up to rounding: the margin 2^-10 C + 2^-10),
+    // and the slot boxes grow by 2^-19 C (trace.h slab_cons_fast<BND>)
+    double cb = c_max;
+    for (int i = 0; i < nn; i++) {
+        if (nodes[i].skip & MIRT_NODE_EMPTY) continue;
+        for (int a = 0; a < 3; a++)
+            for (float v : {nodes[i].bmin[a], nodes[i].bmax[a]})
+                if (std::isfinite(v)) cb = std::max(cb, (double)std::fabs(v));
+    }
+    cb = cb * (1.0 + 0x1p-10) + 0x1p-10;
+    const bool bounded = encloses && cb < 6.0e4;   // fp16 range: the grown boxes stay finite
+    c->o_bound = bounded ? (float)cb : 0.0f;   // 0: every bounce ray takes the exact test
+    build_hnodes(nodes, nn, spheres, ns, hn, hx, lgeo, lbox, bounded ? cb * 0x1p-19 : 0.0);
     const size_t nl = lbox.size();
     const size_t box_off = (sizeof(float4) * nl + 255) & ~(size_t)255;
     HIP_TRY(hipMalloc((void**)&c->d_hnodes, sizeof(HNode) * hn.size()));

@@ -126,6 +126,9 @@ struct DevScene {
     // single slot is the root box, which every ray that can hit a leaf passes
     // (boxes nest), so its step is skipped -- or 0 when the root is a leaf
     uint32_t wide_root;
+    // |coordinate| bound C of every box and of the bounce
+    // rays' origins the HNode slot boxes were grown for (2^-19 C)
+    float o_bound;
 };
 
 // LDS-resident node data (address space 3: ds_read, never a flat load)
@@ -433,6 +436,19 @@ __device__ __forceinline__ bool slab_box(const SlabRay& r, const Prune& p, float
 // covered by slab_fast's margin 2^-20 (|tmin| + |tmax|) (16 u against the
 // 4.1 u needed), the absolute part by mo = 2^-22 max_k |o_k ix_k| (4 u, twice
 // the 2.02 u of two values), added to the margin and to the pruning growth.
+//
+// BND (the bounce kernel's walks over HNodes): no margin.
+// Every HNode slot box is stored grown by delta = 2^-19 C (DevScene::o_bound
+// = C bounds every box coordinate and every bounce-ray origin; a ray whose
+// origin lies outside takes the exact test, `generic`). In world units along
+// axis k, a plane's computed t misses the exact (b - o)/d by at most
+// (2.01 u |b - o| + 1.01 u |o|) / |d_k| <= 5.03 u C / |d_k| and hit.c's Q by
+// 2.01 u |b_e - o| / |d_k| <= 4.02 u C / |d_k| of its exact box's plane b_e;
+// the grown plane lies delta / |d_k| further out in t, 3.5x their sum. So
+// every axis's computed entry is <= hit.c's and its exit >= hit.c's, hence
+// tmin' <= tmin and tmax' >= tmax: a box hit.c passes passes here, and the
+// comparison needs no margin.
+template <bool BND = false>
 __device__ __forceinline__ bool slab_cons_fast(const SlabRay& r, const Prune& p, float x0, float y0, float z0,
                                                float x1, float y1, float z1, float& near)
 {
@@ -448,16 +464,27 @@ __device__ __forceinline__ bool slab_cons_fast(const SlabRay& r, const Prune& p,
     const float tmin = fmaxf(nx, fmaxf(ny, nz));
     const float tmax = fminf(fmaxf(tx1, tx2), fminf(fmaxf(ty1, ty2), fmaxf(tz1, tz2)));
     near = tmin;
+    if (BND) {
+        // the pruning entry without slab_fast's guards either: entry'_k =
+        // fl(nx'_k - m |ix_k|) is below the exact entry of the exact box
+        // grown by m (Prune) by the growth delta / |d_k| = 32 u C / |d_k| less
+        // at most 5.03 u C (the plane) + 2.1 u C (the fma's rounding of a
+        // value within 2.1 C / |d_k|) + u m (|ix|'s): a box pruned here is
+        // one the guarded test prunes
+        const float ent = fmaxf(fmaf(-p.m, fabsf(r.ix), nx), fmaxf(fmaf(-p.m, fabsf(r.iy), ny), fmaf(-p.m, fabsf(r.iz), nz)));
+        return !(ent > p.lim) & !(tmax < fmaxf(tmin, kEps));
+    }
     const float m = fmaf(fabsf(tmin) + fabsf(tmax), 0x1p-20f, 2.0f * mo);
     // tmax - tmin >= -m and tmax - eps >= -m as one comparison (m has 4x slack
     // over the rounding of either form; a NaN passes, as before)
     return !(entry > p.lim) & !(tmax + m < fmaxf(tmin, kEps));
 }
 
+template <bool BND = false>
 __device__ __forceinline__ bool slab_cons(const SlabRay& r, const Prune& p, float x0, float y0, float z0, float x1,
                                           float y1, float z1, float& near)
 {
-    bool pass = slab_cons_fast(r, p, x0, y0, z0, x1, y1, z1, near);
+    bool pass = slab_cons_fast<BND>(r, p, x0, y0, z0, x1, y1, z1, near);
     if (r.generic) {  // a lane branch taken only by rays with a zero/tiny component
         near = 0.0f;
         pass = !pruned_any(r, p, x0, y0, z0, x1, y1, z1) && slab_test(r, x0, y0, z0, x1, y1, z1);
@@ -992,7 +1019,7 @@ __device__ __forceinline__ void leaf_gate(const DevScene& sc, const SlabRay& sr,
 // every ray) staged in LDS by the caller; a node there is read from LDS
 // instead of through the vector-memory path (the bounce kernel's busiest
 // unit, TD: its cost is the bytes returned per lane, however coalesced).
-template <bool FAST, bool COUNT, bool BATCH = false>
+template <bool FAST, bool COUNT, bool BATCH = false, bool BND = false>
 __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
                                                WideWalk& w, uint32_t* stk, float& best_t, int& best_s, Counters& cnt,
                                                lds_uint4* hc = nullptr, uint32_t hc_n = 0)
@@ -1028,7 +1055,8 @@ __device__ __forceinline__ void wide_lane_step(const DevScene& sc, const SlabRay
         }
         auto test = [&](const uint4& q, float& e) {
             if (COUNT && q.w != kPNone) cnt.nodes++;
-            const bool pass = slab_cons(sr, pr, h_lo(q.x), h_lo(q.y), h_lo(q.z), h_hi(q.x), h_hi(q.y), h_hi(q.z), e);
+            const bool pass =
+                slab_cons<BND>(sr, pr, h_lo(q.x), h_lo(q.y), h_lo(q.z), h_hi(q.x), h_hi(q.y), h_hi(q.z), e);
             return pass & (q.w != kPNone);
         };
         h0 = test(s0, e0);
@@ -1147,7 +1175,7 @@ __device__ __forceinline__ void cand_merge(float& t, int& si)
 }
 
 // `stk`: this ray's LDS stack column (entry k at stk[k * STRIDE], CAP entries).
-template <bool FAST, int STRIDE, int CAP>
+template <bool FAST, int STRIDE, int CAP, bool BND = false>
 __device__ __forceinline__ void quad_step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
                                           QuadWalk& w, uint32_t* stk, float& best_t, int& best_s,
                                           lds_uint4* hc = nullptr, uint32_t hc_n = 0)
@@ -1173,7 +1201,7 @@ __device__ __forceinline__ void quad_step(const DevScene& sc, const SlabRay& sr,
     else
         q = ((const uint4*)(sc.hnodes + w.cur))[j];
     float e = 0.0f;
-    const bool pass = slab_cons(sr, pr, h_lo(q.x), h_lo(q.y), h_lo(q.z), h_hi(q.x), h_hi(q.y), h_hi(q.z), e) &
+    const bool pass = slab_cons<BND>(sr, pr, h_lo(q.x), h_lo(q.y), h_lo(q.z), h_hi(q.x), h_hi(q.y), h_hi(q.z), e) &
                       (q.w != kPNone);
     // a passing leaf: its exact gate and sphere give this lane's candidate
     float ct = INFINITY;
@@ -1256,7 +1284,7 @@ __device__ __forceinline__ uint32_t* solo_slot(uint32_t* wst, uint32_t k)
 
 // One step of the solo walk; false once every quad is idle and the stack is
 // empty. wst: the wave's LDS stack (column 0 of its 64), CAP entries.
-template <bool FAST, int CAP>
+template <bool FAST, int CAP, bool BND = false>
 __device__ __forceinline__ bool solo_step(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
                                           SoloWalk& w, uint32_t* wst, float& best_t, int& best_s, lds_uint4* hc,
                                           uint32_t hc_n)
@@ -1302,8 +1330,9 @@ __device__ __forceinline__ bool solo_step(const DevScene& sc, const SlabRay& sr,
             q = ((const uint4*)(sc.hnodes + w.cur))[j];
         qref = q.w;
         float e = 0.0f;
-        const bool pass = slab_cons(sr, pr, h_lo(q.x), h_lo(q.y), h_lo(q.z), h_hi(q.x), h_hi(q.y), h_hi(q.z), e) &
-                          (q.w != kPNone);
+        const bool pass =
+            slab_cons<BND>(sr, pr, h_lo(q.x), h_lo(q.y), h_lo(q.z), h_hi(q.x), h_hi(q.y), h_hi(q.z), e) &
+            (q.w != kPNone);
         if (pass && (q.w & kPLeaf)) {  // sphere first, the exact box only for a hit (wide_leaf)
             const float4* lp = (const float4*)(sc.leaf_box + (q.w & ~kPLeaf));
             const float t = sphere_t<FAST>(sp, sc.leaf_geo[q.w & ~kPLeaf], best_t);

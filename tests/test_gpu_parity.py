@@ -1135,3 +1135,45 @@ def test_leaf_batch_modes_identical(gpu, mirt, golden, small, batch):
         assert n >= 8
     finally:
         gpu.set_option(abi.OPT_LEAF_BATCH, 2)
+
+
+@pytest.mark.parametrize("case", ["tiny_far", "huge", "offset"])
+def test_bounded_slab_edge_scenes(gpu, mirt, oracle, case):
+    """The bounce walks test the four-wide tree's boxes without margins: the
+    boxes are grown by 2^-19 C at upload (C bounds every box and every sphere
+    point) and a bounce ray whose origin lies beyond C takes the exact test.
+    Scenes at the edges of that argument against the oracle, byte for byte:
+    a tiny scene (C < 1, a growth of 2^-20) seen from 300x its size, benchmark
+    spheres beyond the fp16 range (no growth: every bounce ray exact), and a
+    cloud far from the origin (C set by the offset, not the spread).
+    (Farther views of the tiny scene hit nothing in the reference either: its
+    float discriminant loses the radius.)"""
+    if case == "tiny_far":
+        s = mirt.create_random_spheres(2000, 3)
+        s["center"] *= np.float32(0.02)
+        s["radius"] *= np.float32(0.02)
+        cam = mirt.default_camera()
+        cam.position = mirt.abi.Vec3(0.0, 0.1, 300.0)   # 300x the scene's scale (the growth is 2^-19 C)
+        cam.fov = 0.3
+    elif case == "huge":
+        s = mirt.create_benchmark_spheres(3000, 5, world_size=2.0e5)
+        s["radius"] = np.float32(4000.0)
+        cam = mirt.default_camera()
+        cam.position = mirt.abi.Vec3(0.0, 0.0, 3.0e5)
+    else:
+        s = mirt.create_random_spheres(2000, 4)
+        s["center"][:, 0] += np.float32(3000.0)
+        cam = mirt.default_camera()
+        cam.position = mirt.abi.Vec3(3000.0, 4.0, 50.0)
+    s2 = s.copy()
+    gpu.upload(s, mirt.build_bvh(s))
+    t = oracle.build(s2)
+    try:
+        for W, H, depth, seed in ((96, 54, 5, 1), (77, 45, 3, 2)):
+            img = gpu.render_frame(cam, W, H, depth=depth, seed=seed)
+            ref = oracle.render(cam, W, H, s2, t, depth=depth, use_bvh=True, mode=1, seed=seed)
+            bad = int((img != ref).any(-1).sum())
+            assert bad == 0, f"{case} {W}x{H} depth {depth}: {bad} pixels differ"
+            assert len(np.unique(ref.reshape(-1, 4), axis=0)) > 50, case   # spheres in view, not just sky
+    finally:
+        oracle.free(t)
