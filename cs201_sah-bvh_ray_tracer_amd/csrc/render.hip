@@ -346,7 +346,9 @@ struct BounceRec {
 // ORD: the tree admits the ordered packet walk (DevScene::ordered), which
 // also takes zero-component rays -- that build has no deferred waves and no
 // other walk, so it keeps the register budget of the packet walk alone.
-template <bool FAST, bool ORD>
+// BND (ORD only): the camera is within 4C of the origin (DevScene::o_bound):
+// the packet walk tests the grown inner-child boxes without margins (trace.h).
+template <bool FAST, bool ORD, bool BND = false>
 // Register budget of the ordered camera-packet kernel (ORD): 8 waves per SIMD (64 VGPRs, no
 // scratch; 67 and 7 waves without the attribute). With four frames in flight
 // its waves share the CUs with the bounce passes, and the eighth wave hides
@@ -417,7 +419,7 @@ __global__ __launch_bounds__(256) MIRT_PRIMARY_ATTR void primary_kernel(DevScene
     float t;
     int s;
     if constexpr (ORD) {
-        closest_packet_ordered<FAST, false>(sc, ray, alive, t, s, cnt);
+        closest_packet_ordered<FAST, false, BND>(sc, ray, alive, t, s, cnt);
     } else
         closest_hit<true, FAST, false>(sc, ray, alive, t, s, cnt);
     const size_t i = (size_t)r * f.width + x;
@@ -1501,7 +1503,10 @@ uint32_t live_node(const mirt_node* nd, uint32_t ci, int ns)
 // reference's trees, whose build partitions the array in place) and the
 // inner depth must leave the packet walk's stack (one entry per level)
 // within 64.
-bool build_pnodes(const mirt_node* nd, int nn, const mirt_sphere* sp, int ns, std::vector<PNode>& pn)
+// grow > 0: an inner child's box grown by `grow` on each face (rounded
+// outward): the camera packets' margin-free test (trace.h); leaf children keep
+// their exact boxes, which gate every sphere.
+bool build_pnodes(const mirt_node* nd, int nn, const mirt_sphere* sp, int ns, std::vector<PNode>& pn, double grow)
 {
     std::vector<uint32_t> pidx((size_t)nn, kPNone);
     uint32_t np = 1;
@@ -1531,6 +1536,11 @@ bool build_pnodes(const mirt_node* nd, int nn, const mirt_sphere* sp, int ns, st
                 ref = kPLeaf | (uint32_t)n.sphere;
             }
         }
+        if (grow > 0.0 && ref != kPNone && !(ref & kPLeaf))
+            for (int a = 0; a < 3; a++) {
+                slot[a] = std::nextafter((float)((double)slot[a] - grow), -INFINITY);
+                slot[3 + a] = std::nextafter((float)((double)slot[3 + a] + grow), INFINITY);
+            }
         (k ? p.ref1 : p.ref0) = ref;
     };
     pn[0].ref0 = pn[0].ref1 = kPNone;
@@ -1850,6 +1860,14 @@ int launch_render(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_ac
     return MIRT_OK;
 }
 
+// The frame's camera rays may test the grown PNode inner-child boxes without
+// margins (trace.h slab_cons_fast<BND>): the camera within 4C.
+bool camera_bounded(const mirt_ctx* c, const FrameConst& f)
+{
+    const float o = std::max(std::fabs(f.px), std::max(std::fabs(f.py), std::fabs(f.pz)));
+    return c->o_bound > 0.0f && o <= 4.0f * c->o_bound;
+}
+
 int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float* d_acc, hipStream_t s, bool timed,
                        mirt_counts* d_counts, uint32_t* d_wave_stats, uint64_t* d_bdiag, AccumShare* chain)
 {
@@ -1934,7 +1952,10 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
         BounceRec* queue = (BounceRec*)((char*)c->d_queue + kQCtlBytes);
         const int ptiles = f.samples >= 4 ? ((f.width + 3) / 4) * ((f.shard_rows + 3) / 4) * ((f.samples + 3) / 4)
                                           : tiles;
-        primary_kernel<true, true><<<(ptiles + 3) / 4, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
+        if (camera_bounded(c, f))
+            primary_kernel<true, true, true><<<(ptiles + 3) / 4, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
+        else
+            primary_kernel<true, true><<<(ptiles + 3) / 4, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl);
         HIP_TRY(hipGetLastError());
         if (int rc2 = fold()) return rc2;
         if (timed) HIP_TRY(hipEventRecord(c->ev1, s));
@@ -1955,7 +1976,10 @@ int launch_render_body(mirt_ctx* c, const FrameConst& f, uint32_t* d_out, float*
         const int pblocks = (ptiles + 3) / 4 + dfr.blocks;
         const int bblocks = c->bounce_blocks_opt ? c->bounce_blocks_opt : c->bounce_blocks;
         const size_t blds = bounce_lds_bytes(f.depth);
-        if (c->fast_slab && sc.ordered)
+        if (c->fast_slab && sc.ordered && camera_bounded(c, f))
+            primary_kernel<true, true, true><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl,
+                                                                     octant_queue(c));
+        else if (c->fast_slab && sc.ordered)
             primary_kernel<true, true><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl, octant_queue(c));
         else if (c->fast_slab)
             primary_kernel<true, false><<<pblocks, 256, 0, s>>>(sc, f, d_out, d_acc, dfr, queue, qctl, octant_queue(c));
@@ -2162,15 +2186,7 @@ try {
     if (nn > 0) HIP_TRY(hipMemcpy(c->d_nodes32, nodes, sizeof(mirt_node) * (size_t)nn, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_geo, geo.data(), sizeof(float4) * geo.size(), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_color, col.data(), sizeof(uint32_t) * col.size(), hipMemcpyHostToDevice));
-    std::vector<PNode> pn;
-    const bool ordered = build_pnodes(nodes, nn, spheres, ns, pn);
-    HIP_TRY(hipMalloc((void**)&c->d_pnodes, sizeof(PNode) * pn.size()));
-    HIP_TRY(hipMemcpy(c->d_pnodes, pn.data(), sizeof(PNode) * pn.size(), hipMemcpyHostToDevice));
-    std::vector<HNode> hn;
-    std::vector<HAux> hx;
-    std::vector<float4> lgeo;
-    std::vector<LeafBox> lbox;
-    // the bounce walks' bounded slab test: C bounds every box coordinate and every sphere point
+    // the margin-free box tests (bounce walks, camera packets): C bounds every box coordinate and every sphere point
     // (so every bounce-ray origin, up to rounding: the margin 2^-10 C + 2^-10),
     // and the slot boxes grow by 2^-19 C (trace.h slab_cons_fast<BND>)
     double cb = c_max;
@@ -2183,6 +2199,14 @@ try {
     cb = cb * (1.0 + 0x1p-10) + 0x1p-10;
     const bool bounded = encloses && cb < 6.0e4;   // fp16 range: the grown boxes stay finite
     c->o_bound = bounded ? (float)cb : 0.0f;   // 0: every bounce ray takes the exact test
+    std::vector<PNode> pn;
+    const bool ordered = build_pnodes(nodes, nn, spheres, ns, pn, bounded ? cb * 0x1p-19 : 0.0);
+    HIP_TRY(hipMalloc((void**)&c->d_pnodes, sizeof(PNode) * pn.size()));
+    HIP_TRY(hipMemcpy(c->d_pnodes, pn.data(), sizeof(PNode) * pn.size(), hipMemcpyHostToDevice));
+    std::vector<HNode> hn;
+    std::vector<HAux> hx;
+    std::vector<float4> lgeo;
+    std::vector<LeafBox> lbox;
     build_hnodes(nodes, nn, spheres, ns, hn, hx, lgeo, lbox, bounded ? cb * 0x1p-19 : 0.0);
     const size_t nl = lbox.size();
     const size_t box_off = (sizeof(float4) * nl + 255) & ~(size_t)255;

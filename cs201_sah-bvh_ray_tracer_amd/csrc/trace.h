@@ -447,7 +447,9 @@ __device__ __forceinline__ bool slab_box(const SlabRay& r, const Prune& p, float
 // the grown plane lies delta / |d_k| further out in t, 3.5x their sum. So
 // every axis's computed entry is <= hit.c's and its exit >= hit.c's, hence
 // tmin' <= tmin and tmax' >= tmax: a box hit.c passes passes here, and the
-// comparison needs no margin.
+// comparison needs no margin. An origin within 4C (the camera rays of the
+// packet walk over PNodes, whose inner-child boxes are grown the same way)
+// still fits: (2.01 u 5C + 1.01 u 4C) + 2.01 u 5C = 24.1 u C < 32 u C.
 template <bool BND = false>
 __device__ __forceinline__ bool slab_cons_fast(const SlabRay& r, const Prune& p, float x0, float y0, float z0,
                                                float x1, float y1, float z1, float& near)
@@ -820,7 +822,7 @@ __device__ __forceinline__ void consider_sphere(const DevScene& sc, const SphRay
 // One child slot of a PNode for one lane: a leaf's box then its sphere; an
 // inner child's box. Returns whether the walk should enter the child (inner
 // and passed), with its entry estimate.
-template <bool FAST, bool COUNT>
+template <bool FAST, bool COUNT, bool BND = false>
 __device__ __forceinline__ bool visit_child(const DevScene& sc, const SlabRay& sr, const SphRay& sp, Prune& pr,
                                             uint32_t ref, float s0, float s1, float s2, float s3, float s4, float s5,
                                             float& near, float& best_t, int& best_s, Counters& cnt)
@@ -839,7 +841,7 @@ __device__ __forceinline__ bool visit_child(const DevScene& sc, const SlabRay& s
     // an inner box needs only a conservative test: the reference's test is
     // monotone under containment, so a ray that passes any leaf box below
     // passes this one too, and every leaf is still gated exactly
-    if (FAST) return slab_cons(sr, pr, s0, s1, s2, s3, s4, s5, near);
+    if (FAST) return slab_cons<BND>(sr, pr, s0, s1, s2, s3, s4, s5, near);
     return slab_box<FAST>(sr, pr, s0, s1, s2, s3, s4, s5, near);
 }
 
@@ -853,7 +855,7 @@ __device__ __forceinline__ bool visit_child(const DevScene& sc, const SlabRay& s
 // a stack kept one entry per lane (entry k in lane k). Pruning (Prune)
 // drops boxes beyond each lane's best hit. Stack depth <= tree depth + 1 <=
 // 64 (checked at upload).
-template <bool FAST, bool COUNT>
+template <bool FAST, bool COUNT, bool BND = false>
 __device__ __forceinline__ void closest_packet_ordered(const DevScene& sc, const Ray& ray, bool active, float& best_t,
                                                        int& best_s, Counters& cnt)
 {
@@ -874,10 +876,10 @@ __device__ __forceinline__ void closest_packet_ordered(const DevScene& sc, const
         float e0 = 0.0f, e1 = 0.0f;
         bool h0 = false, h1 = false;
         if (in) {
-            h0 = visit_child<FAST, COUNT>(sc, sr, sp, pr, nd.r0, nd.a0, nd.a1, nd.a2, nd.a3, nd.a4, nd.a5, e0, best_t,
-                                          best_s, cnt);
-            h1 = visit_child<FAST, COUNT>(sc, sr, sp, pr, nd.r1, nd.b0, nd.b1, nd.b2, nd.b3, nd.b4, nd.b5, e1, best_t,
-                                          best_s, cnt);
+            h0 = visit_child<FAST, COUNT, BND>(sc, sr, sp, pr, nd.r0, nd.a0, nd.a1, nd.a2, nd.a3, nd.a4, nd.a5, e0,
+                                               best_t, best_s, cnt);
+            h1 = visit_child<FAST, COUNT, BND>(sc, sr, sp, pr, nd.r1, nd.b0, nd.b1, nd.b2, nd.b3, nd.b4, nd.b5, e1,
+                                               best_t, best_s, cnt);
         }
         const uint64_t m0 = __ballot(h0), m1 = __ballot(h1);
         if (m0 && m1) {
